@@ -1,0 +1,209 @@
+"""ctypes binding of the C ABI in include/jg.h (libcapjwt.so).
+
+This is plumbing for tests / bench / the Python mirror of cap's jwt package;
+the product is the shared library.  There is deliberately no CPU fallback:
+if libcapjwt.so is missing or no HIP device is present, every entry point
+raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcapjwt.so")
+
+# jwt/algs.go:12-21
+ALG_IDS = {"RS256": 1, "RS384": 2, "RS512": 3, "PS256": 4, "PS384": 5, "PS512": 6,
+           "ES256": 7, "ES384": 8, "ES512": 9, "EdDSA": 10}
+KEY_RSA, KEY_EC, KEY_ED25519 = 1, 2, 3
+CURVE_IDS = {"P-256": 1, "P-384": 2, "P-521": 3}
+
+# every symbol include/jg.h declares
+EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_last_error",
+           "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_sync",
+           "jg_batch_free", "jg_batch_kernel_times", "jg_version"]
+
+
+class JgKey(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("curve", ctypes.c_int32),
+                ("n", ctypes.c_void_p), ("n_len", ctypes.c_int32), ("e", ctypes.c_uint64),
+                ("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("coord_len", ctypes.c_int32)]
+
+
+class JgTok(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_uint64), ("sig_in_len", ctypes.c_uint32), ("sig_rel_off", ctypes.c_uint32),
+                ("sig_b64_len", ctypes.c_uint32), ("key_idx", ctypes.c_uint16), ("alg", ctypes.c_uint8),
+                ("flags", ctypes.c_uint8)]
+
+
+assert ctypes.sizeof(JgTok) == 24
+
+_lib = None
+
+
+class JgError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libcapjwt.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise JgError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.jg_create.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        L.jg_create.restype = vp
+        L.jg_destroy.argtypes = [vp]
+        L.jg_keys_load.argtypes = [vp, ctypes.POINTER(JgKey), ctypes.c_int]
+        L.jg_verify_batch.argtypes = [vp, vp, sz, ctypes.POINTER(JgTok), sz, vp]
+        L.jg_last_error.argtypes = [vp]
+        L.jg_last_error.restype = ctypes.c_char_p
+        L.jg_host_alloc.argtypes = [sz]
+        L.jg_host_alloc.restype = vp
+        L.jg_host_free.argtypes = [vp]
+        L.jg_batch_stage.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.POINTER(JgTok), sz, ctypes.POINTER(vp)]
+        L.jg_batch_run.argtypes = [vp, vp, vp]
+        L.jg_batch_sync.argtypes = [vp, vp]
+        L.jg_batch_free.argtypes = [vp, vp]
+        L.jg_batch_kernel_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
+                                            ctypes.c_int]
+        L.jg_version.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+class Key:
+    """A public key handed to jg_keys_load (bytes are big-endian; Ed25519: raw 32 bytes)."""
+
+    def __init__(self, kind, n=b"", e=0, curve=0, x=b"", y=b""):
+        self.kind, self.n, self.e, self.curve, self.x, self.y = kind, n, e, curve, x, y
+
+    @staticmethod
+    def rsa(n: bytes, e: int):
+        return Key(KEY_RSA, n=n, e=e)
+
+    @staticmethod
+    def ec(curve: str, x: bytes, y: bytes):
+        return Key(KEY_EC, curve=CURVE_IDS[curve], x=x, y=y)
+
+    @staticmethod
+    def ed25519(pub: bytes):
+        return Key(KEY_ED25519, x=pub)
+
+
+class Arena:
+    """Packed job list: signing inputs and base64url signatures in one buffer."""
+
+    def __init__(self):
+        self.buf = bytearray()
+        self.toks = []
+
+    def add(self, signing_input: bytes, sig_b64: bytes, alg: str, key_idx: int):
+        sig_b64 = sig_b64.rstrip(b"=")
+        off = len(self.buf)
+        self.buf += signing_input + b"." + sig_b64
+        self.toks.append((off, len(signing_input), len(signing_input) + 1, len(sig_b64), key_idx,
+                          ALG_IDS.get(alg, 0)))
+        return len(self.toks) - 1
+
+    def tok_array(self):
+        arr = (JgTok * max(1, len(self.toks)))()
+        for i, t in enumerate(self.toks):
+            arr[i].off, arr[i].sig_in_len, arr[i].sig_rel_off, arr[i].sig_b64_len, arr[i].key_idx, arr[i].alg = t
+        return arr
+
+
+class Context:
+    """Owns a jg_ctx on the given HIP devices."""
+
+    def __init__(self, devices=None):
+        L = lib()
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            self.h = L.jg_create(arr, len(devices))
+        else:
+            self.h = L.jg_create(None, 0)
+        if not self.h:
+            raise JgError("jg_create failed: " + (L.jg_last_error(None) or b"").decode())
+        self._keep = []
+
+    def close(self):
+        if self.h:
+            lib().jg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def error(self):
+        return (lib().jg_last_error(self.h) or b"").decode()
+
+    def load_keys(self, keys):
+        arr = (JgKey * max(1, len(keys)))()
+        keep = []
+        for i, k in enumerate(keys):
+            arr[i].kind = k.kind
+            arr[i].curve = k.curve
+            for fld in ("n", "x", "y"):
+                b = getattr(k, fld)
+                if b:
+                    cb = ctypes.create_string_buffer(bytes(b), len(b))
+                    keep.append(cb)
+                    setattr(arr[i], fld, ctypes.cast(cb, ctypes.c_void_p))
+            arr[i].n_len = len(k.n)
+            arr[i].e = k.e
+            arr[i].coord_len = len(k.x) if k.kind != KEY_RSA else 0
+        rc = lib().jg_keys_load(self.h, arr, len(keys))
+        if rc != 0:
+            raise JgError(f"jg_keys_load rc={rc}: {self.error()}")
+
+    def verify(self, arena: Arena):
+        n = len(arena.toks)
+        out = (ctypes.c_uint8 * max(1, n))()
+        buf = bytes(arena.buf) or b"\0"
+        rc = lib().jg_verify_batch(self.h, buf, len(arena.buf), arena.tok_array(), n, out)
+        if rc != 0:
+            raise JgError(f"jg_verify_batch rc={rc}: {self.error()}")
+        return bytes(out[:n])
+
+    # ---- device-resident batches (bench)
+    def stage(self, arena: Arena, slot=0):
+        h = ctypes.c_void_p()
+        buf = bytes(arena.buf) or b"\0"
+        rc = lib().jg_batch_stage(self.h, slot, buf, len(arena.buf), arena.tok_array(), len(arena.toks),
+                                  ctypes.byref(h))
+        if rc != 0:
+            raise JgError(f"jg_batch_stage rc={rc}: {self.error()}")
+        return Batch(self, h, len(arena.toks))
+
+
+class Batch:
+    def __init__(self, ctx, h, n):
+        self.ctx, self.h, self.n = ctx, h, n
+
+    def run(self, want_verdicts=False):
+        out = (ctypes.c_uint8 * max(1, self.n))() if want_verdicts else None
+        rc = lib().jg_batch_run(self.ctx.h, self.h, out)
+        if rc != 0:
+            raise JgError(f"jg_batch_run rc={rc}: {self.ctx.error()}")
+        return bytes(out[:self.n]) if want_verdicts else None
+
+    def sync(self):
+        rc = lib().jg_batch_sync(self.ctx.h, self.h)
+        if rc != 0:
+            raise JgError(f"jg_batch_sync rc={rc}: {self.ctx.error()}")
+
+    def kernel_times(self):
+        names = (ctypes.c_char_p * 64)()
+        ms = (ctypes.c_float * 64)()
+        n = lib().jg_batch_kernel_times(self.h, names, ms, 64)
+        return [(names[i].decode(), ms[i]) for i in range(min(n, 64))]
+
+    def free(self):
+        if self.h:
+            lib().jg_batch_free(self.ctx.h, self.h)
+            self.h = None

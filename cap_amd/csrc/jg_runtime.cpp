@@ -1,0 +1,743 @@
+// jg_runtime.cpp -- host runtime behind include/jg.h.
+//
+// Owns the per-device state (stream, generator / base-point comb tables, the
+// staged key table) and turns a flat job list into a dispatch plan:
+//   1. classify every (alg, key) pair into a kernel class (RSA-2K/3K/4K, P-256,
+//      P-384, P-521, Ed25519, or reject -- go-jose newVerifier/verifyPayload
+//      type dispatch);
+//   2. counting-sort the jobs by (class, key) and pad every key's run to a
+//      whole 64-lane wave, so each wave's key is uniform (scalar key loads,
+//      broadcast modulus limbs);
+//   3. launch prep (base64url + SHA-2) and the class's arithmetic kernels over
+//      the padded ranges on the device's stream; scatter verdicts back.
+// Multiple devices: jobs are split into contiguous chunks weighted by the
+// per-alg cost model and run concurrently, one host thread per device.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstddef>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/jg.h"
+#include "kernels/batch.hpp"
+#include "kernels/common.hpp"
+#include "kernels/ecdsa.hpp"
+#include "kernels/ed25519.hpp"
+#include "kernels/prep.hpp"
+#include "kernels/rsa.hpp"
+
+static_assert(sizeof(jg_tok) == sizeof(jg_tok_dev), "jg_tok layout");
+static_assert(offsetof(jg_tok, key_idx) == offsetof(jg_tok_dev, key_idx), "jg_tok layout");
+static_assert(offsetof(jg_tok, alg) == offsetof(jg_tok_dev, alg), "jg_tok layout");
+
+using namespace jgk;
+
+namespace {
+
+constexpr size_t ARENA_SLACK = 256;   // aligned SHA word reads may run past the last string
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+int cls_rows_sig(int c) {
+  switch (c) {
+    case CLS_RSA2K: case CLS_RSA3K: case CLS_RSA4K: return rsa_sig_rows(c);
+    case CLS_P256: case CLS_P384: case CLS_P521: return EC_S_ROW + 17;
+    case CLS_ED25519: return 16;
+    default: return 0;
+  }
+}
+int cls_rows_scratch(int c) {
+  switch (c) {
+    case CLS_RSA2K: case CLS_RSA3K: case CLS_RSA4K: return 2 * rsa_limbs(c) + SIGW_ROWS;
+    case CLS_P256: case CLS_P384: case CLS_P521: return ec_windows(c) + 2 * ec_limbs(c);
+    case CLS_ED25519: return 3 * ED_L;
+    default: return 0;
+  }
+}
+// relative cost per token, for splitting a batch over devices
+double cls_cost(int c) {
+  switch (c) {
+    case CLS_RSA2K: return 1.0;
+    case CLS_RSA3K: return 3.3;
+    case CLS_RSA4K: return 7.5;
+    case CLS_P256: return 1.0;
+    case CLS_P384: return 3.0;
+    case CLS_P521: return 7.0;
+    case CLS_ED25519: return 0.9;
+    default: return 0.01;
+  }
+}
+
+struct Grow {                     // grow-only device allocation
+  void* p = nullptr;
+  size_t cap = 0;
+  void* get(size_t n) {
+    if (n == 0) n = 16;
+    if (n > cap) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      HIPCHK(hipMalloc(&p, n));
+      cap = n;
+    }
+    return p;
+  }
+  ~Grow() { if (p) (void)hipFree(p); }
+};
+
+struct HostKey {
+  int kind = 0, cls = CLS_REJECT, valid = 0;
+};
+
+struct Device {
+  int id = 0;
+  hipStream_t stream = nullptr;
+  uint32_t* gtab[NCLS] = {};
+  uint32_t* btab = nullptr;
+  DevKey* dkeys = nullptr;
+  uint32_t* dblob = nullptr;
+  int32_t* didx = nullptr;
+  std::mutex mu;
+  std::unique_ptr<struct Bufs> sync_bufs;
+};
+
+struct Bufs {
+  Grow arena, toks, perm, wave_key, sigw, dig, status, siglen, vpad, verdict, rows, pss, exc, exc_cnt;
+};
+
+}  // namespace
+
+struct jg_batch {
+  jg_ctx* ctx = nullptr;
+  Device* dev = nullptr;
+  std::unique_ptr<Bufs> own;
+  Bufs* b = nullptr;
+  int64_t ntok = 0, npad = 0;
+  size_t arena_len = 0;
+  int sig_rows = 0, scratch_rows = 0;
+  int64_t pss_tokens = 0;
+  ClassRange ranges[NCLS] = {};
+  uint64_t epoch = 0;
+  bool timing = true;
+  std::vector<std::string> mark_names;
+  std::vector<hipEvent_t> mark_events;
+  std::vector<std::string> tnames;
+  std::vector<float> tms;
+  ~jg_batch() {
+    for (auto e : mark_events) (void)hipEventDestroy(e);
+  }
+};
+
+struct jg_ctx {
+  std::vector<std::unique_ptr<Device>> devs;
+  std::vector<HostKey> keys;
+  uint64_t epoch = 0;
+  std::mutex key_mu;
+  std::mutex err_mu;
+  std::string err;
+  void set_err(const std::string& s) {
+    std::lock_guard<std::mutex> g(err_mu);
+    err = s;
+  }
+};
+
+namespace {
+
+// big-endian bytes -> 28-bit little-endian limbs; false if the value needs more than L limbs
+bool be_to_limbs(const uint8_t* b, size_t n, uint32_t* out, int L) {
+  std::memset(out, 0, sizeof(uint32_t) * L);
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t v = b[n - 1 - i];
+    if (!v) continue;
+    for (int k = 0; k < 8; ++k) {
+      if (!((v >> k) & 1)) continue;
+      const size_t bit = i * 8 + k;
+      if (bit / 28 >= (size_t)L) return false;
+      out[bit / 28] |= 1u << (bit % 28);
+    }
+  }
+  return true;
+}
+
+int bitlen_be(const uint8_t* b, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    if (b[i]) {
+      int k = 8;
+      while (!((b[i] >> (k - 1)) & 1)) --k;
+      return (int)((n - 1 - i) * 8) + k;
+    }
+  return 0;
+}
+
+int alg_family(int alg) {         // 1 RSA, 2 EC, 3 Ed, 0 none
+  if (alg >= JG_RS256 && alg <= JG_PS512) return JG_KEY_RSA;
+  if (alg >= JG_ES256 && alg <= JG_ES512) return JG_KEY_EC;
+  if (alg == JG_EDDSA) return JG_KEY_ED25519;
+  return 0;
+}
+
+int classify(const jg_ctx* ctx, const jg_tok& t) {
+  if (t.key_idx >= ctx->keys.size()) return -1;
+  const HostKey& k = ctx->keys[t.key_idx];
+  if (!k.valid || alg_family(t.alg) != k.kind) return CLS_REJECT;
+  return k.cls;
+}
+
+void mark(jg_batch* b, const char* name) {
+  if (!b->timing) return;
+  hipEvent_t e;
+  HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventRecord(e, b->dev->stream));
+  b->mark_names.emplace_back(name);
+  b->mark_events.push_back(e);
+}
+
+const char* cls_name(int c) {
+  static const char* n[NCLS] = {"reject", "rsa2048", "rsa3072", "rsa4096", "p256", "p384", "p521", "ed25519"};
+  return n[c];
+}
+
+// Build the plan and upload everything for toks[0..ntok) (indices are the caller's).
+void stage(jg_ctx* ctx, jg_batch* b, const uint8_t* arena, size_t arena_len, const jg_tok* toks, size_t ntok) {
+  Device* d = b->dev;
+  HIPCHK(hipSetDevice(d->id));
+  const int nkeys = (int)ctx->keys.size();
+  const size_t nbuck = (size_t)NCLS * (nkeys > 0 ? nkeys : 1);
+  std::vector<int64_t> cnt(nbuck, 0);
+  std::vector<int> tcls(ntok);
+  for (size_t i = 0; i < ntok; ++i) {
+    const int c = classify(ctx, toks[i]);
+    if (c < 0) throw std::invalid_argument("jg_tok.key_idx out of range of the loaded key table");
+    tcls[i] = c;
+    cnt[(size_t)c * nkeys + (c == CLS_REJECT ? 0 : toks[i].key_idx)]++;
+  }
+  // bucket order: classes 1..NCLS-1 by key, then the reject bucket
+  std::vector<int64_t> off(nbuck, 0);
+  int64_t pos = 0;
+  for (int c = 1; c <= NCLS; ++c) {
+    const int cc = c % NCLS;
+    b->ranges[cc].begin = pos;
+    const int kmax = cc == CLS_REJECT ? 1 : nkeys;
+    for (int k = 0; k < kmax; ++k) {
+      const size_t i = (size_t)cc * nkeys + k;
+      off[i] = pos;
+      pos += (cnt[i] + WAVE - 1) / WAVE * WAVE;
+    }
+    b->ranges[cc].end = pos;
+  }
+  const int64_t npad = pos > 0 ? pos : WAVE;
+  b->npad = npad;
+  b->ntok = (int64_t)ntok;
+  std::vector<int32_t> perm((size_t)npad, -1);
+  std::vector<int32_t> wkey((size_t)(npad / WAVE), 0);
+  std::vector<int64_t> fill = off;
+  for (size_t i = 0; i < ntok; ++i) {
+    const int c = tcls[i];
+    const size_t bi = (size_t)c * nkeys + (c == CLS_REJECT ? 0 : toks[i].key_idx);
+    const int64_t p = fill[bi]++;
+    perm[(size_t)p] = (int32_t)i;
+    wkey[(size_t)(p / WAVE)] = c == CLS_REJECT ? 0 : toks[i].key_idx;
+  }
+  b->sig_rows = 1;
+  b->scratch_rows = 1;
+  b->pss_tokens = 0;
+  for (int c = 1; c < NCLS; ++c) {
+    if (b->ranges[c].end <= b->ranges[c].begin) continue;
+    b->sig_rows = std::max(b->sig_rows, cls_rows_sig(c));
+    b->scratch_rows = std::max(b->scratch_rows, cls_rows_scratch(c));
+    if (c <= CLS_RSA4K) b->pss_tokens = std::max(b->pss_tokens, b->ranges[c].end - b->ranges[c].begin);
+  }
+  Bufs* B = b->b;
+  hipStream_t s = d->stream;
+  b->arena_len = arena_len;
+  uint8_t* da = (uint8_t*)B->arena.get(arena_len + ARENA_SLACK);
+  HIPCHK(hipMemcpyAsync(da, arena, arena_len, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(da + arena_len, 0, ARENA_SLACK, s));
+  HIPCHK(hipMemcpyAsync(B->toks.get(sizeof(jg_tok) * std::max<size_t>(ntok, 1)), toks, sizeof(jg_tok) * ntok,
+                        hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(B->perm.get(sizeof(int32_t) * npad), perm.data(), sizeof(int32_t) * npad,
+                        hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(B->wave_key.get(sizeof(int32_t) * wkey.size()), wkey.data(), sizeof(int32_t) * wkey.size(),
+                        hipMemcpyHostToDevice, s));
+  B->sigw.get(sizeof(uint32_t) * b->sig_rows * npad);
+  B->dig.get(sizeof(uint32_t) * DIG_ROWS * npad);
+  B->status.get(npad);
+  B->siglen.get(sizeof(uint16_t) * npad);
+  B->vpad.get(npad);
+  B->verdict.get(std::max<size_t>(ntok, 1));
+  B->rows.get(sizeof(uint32_t) * (size_t)b->scratch_rows * npad);
+  B->pss.get((size_t)std::max<int64_t>(b->pss_tokens, 1) * 1024);
+  B->exc.get(sizeof(int32_t) * npad);
+  B->exc_cnt.get(sizeof(uint32_t) * 4);
+  // the host vectors die here: the copies above must complete first
+  HIPCHK(hipStreamSynchronize(s));
+  b->epoch = ctx->epoch;
+}
+
+void run(jg_ctx* ctx, jg_batch* b) {
+  Device* d = b->dev;
+  HIPCHK(hipSetDevice(d->id));
+  if (b->epoch != ctx->epoch) throw std::runtime_error("key table reloaded since this batch was staged");
+  Bufs* B = b->b;
+  hipStream_t s = d->stream;
+  for (auto e : b->mark_events) (void)hipEventDestroy(e);
+  b->mark_events.clear();
+  b->mark_names.clear();
+  const int64_t np = b->npad;
+  mark(b, "begin");
+  HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, s));
+  PrepArgs pa{};
+  pa.arena = (const uint8_t*)B->arena.p;
+  pa.toks = (const jg_tok_dev*)B->toks.p;
+  pa.perm = (const int32_t*)B->perm.p;
+  pa.wave_key = (const int32_t*)B->wave_key.p;
+  pa.keys = d->dkeys;
+  pa.keyblob = d->dblob;
+  pa.sigw = (uint32_t*)B->sigw.p;
+  pa.dig = (uint32_t*)B->dig.p;
+  pa.status = (uint8_t*)B->status.p;
+  pa.siglen = (uint16_t*)B->siglen.p;
+  pa.npad = np;
+  uint32_t* rows = (uint32_t*)B->rows.p;
+  for (int c = 1; c < NCLS; ++c) {
+    const ClassRange r = b->ranges[c];
+    if (r.end <= r.begin) continue;
+    pa.begin = r.begin;
+    pa.end = r.end;
+    pa.zrows = cls_rows_sig(c);
+    launch_prep(c, pa, s);
+    mark(b, (std::string("prep_") + cls_name(c)).c_str());
+    if (c <= CLS_RSA4K) {
+      RsaArgs ra{};
+      ra.toks = pa.toks; ra.perm = pa.perm; ra.wave_key = pa.wave_key; ra.keys = pa.keys; ra.keyblob = pa.keyblob;
+      ra.sigw = pa.sigw; ra.dig = pa.dig;
+      const int L = rsa_limbs(c);
+      ra.xmw = rows;
+      ra.xlr = rows + (size_t)L * np;
+      ra.yw = rows + (size_t)2 * L * np;
+      ra.status = pa.status; ra.siglen = pa.siglen; ra.verdict_pad = (uint8_t*)B->vpad.p;
+      ra.pss_scratch = (uint8_t*)B->pss.p;
+      ra.npad = np; ra.begin = r.begin; ra.end = r.end;
+      launch_rsa(c, ra, s);
+      mark(b, cls_name(c));
+    } else if (c <= CLS_P521) {
+      if (!d->gtab[c]) throw std::runtime_error("curve table missing");
+      EcArgs ea{};
+      ea.toks = pa.toks; ea.perm = pa.perm; ea.wave_key = pa.wave_key; ea.keys = pa.keys; ea.keyblob = pa.keyblob;
+      ea.sigw = pa.sigw; ea.dig = pa.dig; ea.status = pa.status; ea.verdict_pad = (uint8_t*)B->vpad.p;
+      ea.digs = rows;
+      ea.u1w = rows + (size_t)ec_windows(c) * np;
+      ea.u2w = rows + (size_t)(ec_windows(c) + ec_limbs(c)) * np;
+      ea.gtab = d->gtab[c];
+      ea.exc_list = (int32_t*)B->exc.p;
+      ea.exc_count = (uint32_t*)B->exc_cnt.p;
+      ea.npad = np; ea.begin = r.begin; ea.end = r.end;
+      launch_ec(c, ea, s);
+      mark(b, cls_name(c));
+    } else {
+      EdArgs ea{};
+      ea.perm = pa.perm; ea.wave_key = pa.wave_key; ea.keys = pa.keys; ea.keyblob = pa.keyblob;
+      ea.sigw = pa.sigw; ea.dig = pa.dig; ea.status = pa.status; ea.siglen = pa.siglen;
+      ea.verdict_pad = (uint8_t*)B->vpad.p;
+      ea.xyz = rows;
+      ea.btab = d->btab;
+      ea.npad = np; ea.begin = r.begin; ea.end = r.end;
+      launch_ed(ea, s);
+      mark(b, cls_name(c));
+    }
+  }
+  launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s);
+  mark(b, "scatter");
+  HIPCHK(hipGetLastError());
+}
+
+void collect_times(jg_batch* b) {
+  b->tnames.clear();
+  b->tms.clear();
+  for (size_t i = 1; i < b->mark_events.size(); ++i) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, b->mark_events[i - 1], b->mark_events[i]) == hipSuccess) {
+      b->tnames.push_back(b->mark_names[i]);
+      b->tms.push_back(ms);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- keys
+struct StagedKeys {
+  std::vector<DevKey> dk;
+  std::vector<uint32_t> blob;
+  std::vector<int32_t> rsa_idx, ec_idx[NCLS], ed_idx;
+};
+
+uint64_t blob_alloc(std::vector<uint32_t>& blob, size_t words) {
+  const uint64_t off = (blob.size() + 3) & ~size_t(3);          // 16-byte aligned
+  blob.resize(off + words, 0);
+  return off;
+}
+
+void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
+  ctx->keys.assign((size_t)nkeys, HostKey{});
+  S.dk.assign((size_t)nkeys, DevKey{});
+  for (int i = 0; i < nkeys; ++i) {
+    const jg_key& k = keys[i];
+    HostKey& hk = ctx->keys[i];
+    DevKey& K = S.dk[i];
+    hk.kind = K.kind = k.kind;
+    K.cls = CLS_REJECT;
+    if (k.kind == JG_KEY_RSA) {
+      const uint8_t* n = k.n;
+      size_t nl = k.n_len > 0 && n ? (size_t)k.n_len : 0;
+      while (nl > 0 && n[0] == 0) { ++n; --nl; }
+      const int bits = bitlen_be(n, nl);
+      // crypto/rsa (Go >= 1.24) public-key checks: odd N of >= 1024 bits
+      // (rsa1024min), odd E with 2 <= E <= 2^31-1   [SURVEY R12]
+      bool ok = nl > 0 && bits >= 1024 && (n[nl - 1] & 1) && k.e >= 2 && k.e <= 0x7fffffffULL && (k.e & 1);
+      int cls = bits <= 74 * 28 - 2 ? CLS_RSA2K : bits <= 112 * 28 - 2 ? CLS_RSA3K : bits <= 148 * 28 - 2 ? CLS_RSA4K : -1;
+      if (cls < 0) {
+        ok = false;
+        ctx->set_err("RSA key " + std::to_string(i) + " has " + std::to_string(bits) +
+                     " bits; the GPU path supports up to 4142-bit moduli (key marked unusable)");
+        cls = CLS_RSA4K;
+      }
+      const int L = rsa_limbs(cls);
+      K.cls = cls;
+      K.valid = ok;
+      K.kbytes = (bits + 7) / 8;
+      K.embits = bits - 1;
+      K.e_lo = (uint32_t)k.e;
+      K.e_hi = (uint32_t)(k.e >> 32);
+      K.nlimbs = (uint32_t)L;
+      K.n_off = blob_alloc(S.blob, L);
+      K.rr_off = blob_alloc(S.blob, L);
+      if (nl > 0) be_to_limbs(n, nl, S.blob.data() + K.n_off, L);
+      if (ok) S.rsa_idx.push_back(i);
+      hk.cls = cls;
+      hk.valid = ok;
+    } else if (k.kind == JG_KEY_EC) {
+      const int cls = k.curve == JG_P256 ? CLS_P256 : k.curve == JG_P384 ? CLS_P384 : k.curve == JG_P521 ? CLS_P521 : -1;
+      if (cls < 0) { hk.valid = 0; continue; }
+      const int L = ec_limbs(cls);
+      const int cb = cls == CLS_P256 ? 32 : cls == CLS_P384 ? 48 : 66;
+      K.cls = cls;
+      K.kbytes = cb;
+      K.aux_off = blob_alloc(S.blob, 2 * L);
+      K.tab_off = blob_alloc(S.blob, (size_t)ec_table_words(cls));
+      const size_t cl = k.coord_len > 0 ? (size_t)k.coord_len : 0;
+      // crypto/ecdsa pointFromAffine: coordinates must fit the curve's bit size
+      bool ok = k.x && k.y && cl > 0 && bitlen_be(k.x, cl) <= (cls == CLS_P521 ? 521 : cb * 8) &&
+                bitlen_be(k.y, cl) <= (cls == CLS_P521 ? 521 : cb * 8);
+      if (ok) {
+        be_to_limbs(k.x, cl, S.blob.data() + K.aux_off, L);
+        be_to_limbs(k.y, cl, S.blob.data() + K.aux_off + L, L);
+      }
+      K.valid = ok;
+      if (ok) S.ec_idx[cls].push_back(i);
+      hk.cls = cls;
+      hk.valid = ok;              // on-curve check happens on the device
+    } else if (k.kind == JG_KEY_ED25519) {
+      K.cls = CLS_ED25519;
+      K.kbytes = 32;
+      K.aux_off = blob_alloc(S.blob, 8 + 2 * ED_L);
+      K.tab_off = blob_alloc(S.blob, (size_t)ED_TABLE_WORDS);
+      // crypto/ed25519.Verify panics on len(pub) != 32; go-jose never hands it one
+      const bool ok = k.x && k.coord_len == 32;
+      if (ok) std::memcpy(S.blob.data() + K.aux_off, k.x, 32);
+      K.valid = ok;
+      if (ok) S.ed_idx.push_back(i);
+      hk.cls = CLS_ED25519;
+      hk.valid = ok;
+    } else {
+      hk.valid = 0;
+    }
+  }
+}
+
+void ensure_tables(Device* d, const StagedKeys& S) {
+  HIPCHK(hipSetDevice(d->id));
+  for (int c = CLS_P256; c <= CLS_P521; ++c) {
+    if (S.ec_idx[c].empty() || d->gtab[c]) continue;
+    HIPCHK(hipMalloc(&d->gtab[c], sizeof(uint32_t) * ec_table_words(c)));
+    launch_ec_gtable(c, d->gtab[c], d->stream);
+  }
+  if (!S.ed_idx.empty() && !d->btab) {
+    HIPCHK(hipMalloc(&d->btab, sizeof(uint32_t) * ED_TABLE_WORDS));
+    launch_ed_btable(d->btab, d->stream);
+  }
+}
+
+void load_keys_device(Device* d, const StagedKeys& S) {
+  HIPCHK(hipSetDevice(d->id));
+  hipStream_t s = d->stream;
+  HIPCHK(hipStreamSynchronize(s));
+  if (d->dkeys) (void)hipFree(d->dkeys);
+  if (d->dblob) (void)hipFree(d->dblob);
+  if (d->didx) (void)hipFree(d->didx);
+  d->dkeys = nullptr; d->dblob = nullptr; d->didx = nullptr;
+  const size_t nk = std::max<size_t>(S.dk.size(), 1);
+  HIPCHK(hipMalloc(&d->dkeys, sizeof(DevKey) * nk));
+  HIPCHK(hipMalloc(&d->dblob, sizeof(uint32_t) * std::max<size_t>(S.blob.size(), 4)));
+  if (!S.dk.empty()) HIPCHK(hipMemcpyAsync(d->dkeys, S.dk.data(), sizeof(DevKey) * S.dk.size(), hipMemcpyHostToDevice, s));
+  if (!S.blob.empty())
+    HIPCHK(hipMemcpyAsync(d->dblob, S.blob.data(), sizeof(uint32_t) * S.blob.size(), hipMemcpyHostToDevice, s));
+  // one index array: rsa | p256 | p384 | p521 | ed
+  std::vector<int32_t> idx;
+  std::vector<size_t> at;
+  auto push = [&](const std::vector<int32_t>& v) { at.push_back(idx.size()); idx.insert(idx.end(), v.begin(), v.end()); };
+  push(S.rsa_idx);
+  for (int c = CLS_P256; c <= CLS_P521; ++c) push(S.ec_idx[c]);
+  push(S.ed_idx);
+  HIPCHK(hipMalloc(&d->didx, sizeof(int32_t) * std::max<size_t>(idx.size(), 1)));
+  if (!idx.empty()) HIPCHK(hipMemcpyAsync(d->didx, idx.data(), sizeof(int32_t) * idx.size(), hipMemcpyHostToDevice, s));
+  ensure_tables(d, S);
+  if (!S.dk.empty()) launch_rsa_keyprep(d->dkeys, d->dblob, (int)S.dk.size(), s);
+  for (int c = CLS_P256; c <= CLS_P521; ++c)
+    launch_ec_keyprep(c, d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(), s);
+  launch_ed_keyprep(d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), s);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+}
+
+thread_local std::string g_tls_err;
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+jg_ctx* jg_create(const int* devices, int ndev) {
+  try {
+    auto ctx = std::make_unique<jg_ctx>();
+    int count = 0;
+    HIPCHK(hipGetDeviceCount(&count));
+    if (count <= 0) throw std::runtime_error("no HIP device");
+    std::vector<int> ids;
+    if (!devices || ndev <= 0) ids.push_back(0);
+    else ids.assign(devices, devices + ndev);
+    for (int id : ids) {
+      if (id < 0 || id >= count) throw std::runtime_error("bad device id " + std::to_string(id));
+      auto d = std::make_unique<Device>();
+      d->id = id;
+      HIPCHK(hipSetDevice(id));
+      HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+      d->sync_bufs = std::make_unique<Bufs>();
+      ctx->devs.push_back(std::move(d));
+    }
+    return ctx.release();
+  } catch (const std::exception& e) {
+    g_tls_err = e.what();
+    return nullptr;
+  }
+}
+
+void jg_destroy(jg_ctx* ctx) {
+  if (!ctx) return;
+  for (auto& d : ctx->devs) {
+    (void)hipSetDevice(d->id);
+    (void)hipStreamSynchronize(d->stream);
+    d->sync_bufs.reset();
+    for (auto& t : d->gtab) if (t) (void)hipFree(t);
+    if (d->btab) (void)hipFree(d->btab);
+    if (d->dkeys) (void)hipFree(d->dkeys);
+    if (d->dblob) (void)hipFree(d->dblob);
+    if (d->didx) (void)hipFree(d->didx);
+    (void)hipStreamDestroy(d->stream);
+  }
+  delete ctx;
+}
+
+int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys) {
+  if (!ctx || nkeys < 0 || (nkeys > 0 && !keys)) return -1;
+  if (nkeys > 65535) { ctx->set_err("at most 65535 keys"); return -1; }
+  try {
+    std::lock_guard<std::mutex> g(ctx->key_mu);
+    for (auto& d : ctx->devs) d->mu.lock();
+    StagedKeys S;
+    build_keys(ctx, keys, nkeys, S);
+    try {
+      for (auto& d : ctx->devs) load_keys_device(d.get(), S);
+    } catch (...) {
+      for (auto& d : ctx->devs) d->mu.unlock();
+      throw;
+    }
+    // device-side validity (on-curve, Ed25519 decoding) back into the host view
+    Device* d0 = ctx->devs[0].get();
+    std::vector<DevKey> back(S.dk.size());
+    if (!back.empty()) {
+      HIPCHK(hipSetDevice(d0->id));
+      HIPCHK(hipMemcpy(back.data(), d0->dkeys, sizeof(DevKey) * back.size(), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < back.size(); ++i) ctx->keys[i].valid = ctx->keys[i].valid && back[i].valid;
+    }
+    ++ctx->epoch;
+    for (auto& d : ctx->devs) d->mu.unlock();
+    return 0;
+  } catch (const std::exception& e) {
+    ctx->set_err(e.what());
+    return -2;
+  }
+}
+
+int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t arena_len,
+                   const jg_tok* toks, size_t ntok, jg_batch** out) {
+  if (!ctx || !out || (ntok > 0 && (!toks || !arena))) return -1;
+  if (device_slot < 0 || device_slot >= (int)ctx->devs.size()) return -1;
+  if (ntok > (size_t)INT32_MAX / 2) { ctx->set_err("batch too large"); return -1; }
+  try {
+    auto b = std::make_unique<jg_batch>();
+    b->ctx = ctx;
+    b->dev = ctx->devs[device_slot].get();
+    b->own = std::make_unique<Bufs>();
+    b->b = b->own.get();
+    std::lock_guard<std::mutex> g(b->dev->mu);
+    stage(ctx, b.get(), arena, arena_len, toks, ntok);
+    *out = b.release();
+    return 0;
+  } catch (const std::invalid_argument& e) {
+    ctx->set_err(e.what());
+    return -1;
+  } catch (const std::exception& e) {
+    ctx->set_err(e.what());
+    return -2;
+  }
+}
+
+int jg_batch_run(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out) {
+  if (!ctx || !b) return -1;
+  try {
+    std::lock_guard<std::mutex> g(b->dev->mu);
+    run(ctx, b);
+    if (verdict_out) {
+      if (b->ntok > 0)
+        HIPCHK(hipMemcpyAsync(verdict_out, b->b->verdict.p, (size_t)b->ntok, hipMemcpyDeviceToHost, b->dev->stream));
+      HIPCHK(hipStreamSynchronize(b->dev->stream));
+      collect_times(b);
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    ctx->set_err(e.what());
+    return -2;
+  }
+}
+
+int jg_batch_sync(jg_ctx* ctx, jg_batch* b) {
+  if (!ctx || !b) return -1;
+  try {
+    HIPCHK(hipSetDevice(b->dev->id));
+    HIPCHK(hipStreamSynchronize(b->dev->stream));
+    collect_times(b);
+    return 0;
+  } catch (const std::exception& e) {
+    ctx->set_err(e.what());
+    return -2;
+  }
+}
+
+void jg_batch_free(jg_ctx* ctx, jg_batch* b) {
+  (void)ctx;
+  if (!b) return;
+  (void)hipSetDevice(b->dev->id);
+  (void)hipStreamSynchronize(b->dev->stream);
+  delete b;
+}
+
+int jg_batch_kernel_times(jg_batch* b, const char** names, float* ms, int cap) {
+  if (!b) return 0;
+  const int n = (int)b->tms.size();
+  for (int i = 0; i < n && i < cap; ++i) {
+    if (names) names[i] = b->tnames[i].c_str();
+    if (ms) ms[i] = b->tms[i];
+  }
+  return n;
+}
+
+int jg_verify_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
+                    const jg_tok* toks, size_t ntok, uint8_t* verdict_out) {
+  if (!ctx || (ntok > 0 && (!toks || !arena || !verdict_out))) return -1;
+  if (ntok == 0) return 0;
+  // split over devices by the cost model
+  const size_t nd = ctx->devs.size();
+  std::vector<size_t> cut(nd + 1, 0);
+  cut[nd] = ntok;
+  if (nd > 1) {
+    std::vector<double> pre(ntok + 1, 0.0);
+    for (size_t i = 0; i < ntok; ++i) {
+      int c = classify(ctx, toks[i]);
+      pre[i + 1] = pre[i] + cls_cost(c < 0 ? 0 : c);
+    }
+    size_t j = 0;
+    for (size_t k = 1; k < nd; ++k) {
+      const double target = pre[ntok] * (double)k / (double)nd;
+      while (j < ntok && pre[j] < target) ++j;
+      cut[k] = j;
+    }
+  }
+  std::vector<int> rc(nd, 0);
+  std::vector<std::string> errs(nd);
+  auto work = [&](size_t k) {
+    Device* d = ctx->devs[k].get();
+    const size_t lo = cut[k], hi = cut[k + 1];
+    if (hi <= lo) return;
+    try {
+      std::lock_guard<std::mutex> g(d->mu);
+      jg_batch b;
+      b.ctx = ctx;
+      b.dev = d;
+      b.b = d->sync_bufs.get();
+      b.timing = false;
+      stage(ctx, &b, arena, arena_len, toks + lo, hi - lo);
+      run(ctx, &b);
+      HIPCHK(hipMemcpyAsync(verdict_out + lo, b.b->verdict.p, hi - lo, hipMemcpyDeviceToHost, d->stream));
+      HIPCHK(hipStreamSynchronize(d->stream));
+    } catch (const std::invalid_argument& e) {
+      rc[k] = -1;
+      errs[k] = e.what();
+    } catch (const std::exception& e) {
+      rc[k] = -2;
+      errs[k] = e.what();
+    }
+  };
+  if (nd == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
+    for (auto& t : th) t.join();
+  }
+  for (size_t k = 0; k < nd; ++k)
+    if (rc[k]) {
+      ctx->set_err(errs[k]);
+      return rc[k];
+    }
+  return 0;
+}
+
+const char* jg_last_error(jg_ctx* ctx) {
+  if (!ctx) return g_tls_err.c_str();
+  std::lock_guard<std::mutex> g(ctx->err_mu);
+  g_tls_err = ctx->err;
+  return g_tls_err.c_str();
+}
+
+void* jg_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void jg_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+const char* jg_version(void) { return "capjwt 0.1 (gfx950, HIP)"; }
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// common.hpp -- structures shared by the HIP kernels and the host runtime.
+#pragma once
+#include <cstdint>
+
+namespace jgk {
+
+// Kernel classes a (token, key) pair is bucketed into.  Every token of a class
+// runs the same kernel chain; within a class tokens are sorted by key and each
+// key's run is padded to a whole wave, so the key is wave-uniform.
+enum Cls : int {
+  CLS_REJECT = 0,   // alg/key-type mismatch, unsupported alg, invalid key
+  CLS_RSA2K = 1,    // RSA, modulus <= 2070 bits  (74 x 28-bit limbs)
+  CLS_RSA3K = 2,    // RSA, modulus <= 3078 bits  (110 limbs)
+  CLS_RSA4K = 3,    // RSA, modulus <= 4114 bits  (147 limbs)
+  CLS_P256 = 4,
+  CLS_P384 = 5,
+  CLS_P521 = 6,
+  CLS_ED25519 = 7,
+  NCLS = 8
+};
+
+constexpr int WAVE = 64;
+
+// per-token status codes in the scratch status byte
+enum : uint8_t { ST_OK = 0, ST_REJECT = 1, ST_EXCEPTIONAL = 2 };
+
+// scratch rows (each row holds one 32-bit word per padded token, SoA)
+constexpr int SIGW_ROWS = 128;      // decoded signature, up to 512 bytes
+constexpr int EC_S_ROW = 32;        // ECDSA: s starts at row 32 (r at row 0)
+constexpr int DIG_ROWS = 16;        // digest, big-endian 32-bit words
+
+// Device view of one loaded key (arrays live in the key blob, word offsets).
+struct DevKey {
+  int32_t kind;        // jg_key_kind
+  int32_t cls;         // Cls of (this key, a matching alg)
+  int32_t valid;       // 0 => every token verifies false
+  int32_t kbytes;      // RSA: modulus bytes k; EC: coord bytes; Ed: 32
+  uint32_t e_lo, e_hi; // RSA public exponent
+  uint32_t np;         // RSA: -n^-1 mod 2^28
+  uint32_t nlimbs;     // RSA: limb count used (74/110/147)
+  uint64_t n_off;      // RSA: n (28-bit limbs)        -- word offset in blob
+  uint64_t rr_off;     // RSA: R^2 mod n (28-bit limbs)
+  uint64_t tab_off;    // EC: comb table of Q / Ed: comb table of -A
+  uint64_t aux_off;    // EC: Q affine Montgomery (x,y) / Ed: raw public key words
+  int32_t embits;      // RSA: bitlen(n) - 1
+  int32_t pad_;
+};
+
+// Comb tables: 8-bit signed windows, entries 1..128 per window.
+constexpr int COMB_W = 8;
+constexpr int COMB_ENTRIES = 128;
+
+// Per-class launch range inside a staged batch (padded token index space).
+struct ClassRange {
+  int64_t begin, end;   // multiples of WAVE
+};
+
+}  // namespace jgk

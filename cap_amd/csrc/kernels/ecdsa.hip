@@ -1,0 +1,522 @@
+// ecdsa.hip -- ECDSA P-256 / P-384 / P-521 verification on gfx950.
+//
+// Replaces go-jose ecEncrypterVerifier.verifyPayload -> crypto/ecdsa.Verify
+// (rules R18-R22).  Per token:
+//   k_ec_scalar : r, s in [1, n-1] (sizes from the alg, curve from the key),
+//                 e = leftmost bits of H, w = s^-1, u1 = e w, u2 = r w (mod n),
+//                 u1/u2 recoded to signed 8-bit windows
+//   k_ec_point  : R = u1 G + u2 Q as a sum of one precomputed affine multiple of
+//                 G and one of Q per window (comb tables in HBM / L2: entries
+//                 d * 2^(8w) * P, d = 1..128), mixed Jacobian+affine additions,
+//                 no doublings; accept iff X == r Z^2 or (r+n) Z^2 (no inversion)
+//   k_ec_exact  : tokens whose fast sum hit an exceptional case of the group
+//                 law (Z == 0: a doubling, an inverse pair, or R = infinity) --
+//                 recomputed with complete case handling; rare
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "ecdsa.hpp"
+#include "mp.hpp"
+
+using namespace jgk;
+
+namespace {
+
+struct CurveP256 { using Fp = P256P; using Fn = P256N; using C = P256C; static constexpr int CLS = CLS_P256; };
+struct CurveP384 { using Fp = P384P; using Fn = P384N; using C = P384C; static constexpr int CLS = CLS_P384; };
+struct CurveP521 { using Fp = P521P; using Fn = P521N; using C = P521C; static constexpr int CLS = CLS_P521; };
+
+__device__ __forceinline__ int es_size(int alg) { return alg == 7 ? 32 : alg == 8 ? 48 : 66; }
+__device__ __forceinline__ int es_hash_bytes(int alg) { return alg == 7 ? 32 : alg == 8 ? 48 : 64; }
+
+// plain-integer compare of normalized limbs: a < b
+template <int L>
+__device__ __forceinline__ bool lt_limbs(const uint32_t* a, const uint32_t* b) {
+  int lt = 0, gt = 0;
+#pragma unroll
+  for (int j = L - 1; j >= 0; --j) {
+    const int und = !(lt | gt);
+    lt |= und & (a[j] < b[j]);
+    gt |= und & (a[j] > b[j]);
+  }
+  return lt;
+}
+template <int L>
+__device__ __forceinline__ bool zero_limbs(const uint32_t* a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < L; ++j) o |= a[j];
+  return o == 0;
+}
+
+// ------------------------------------------------------------------ scalar
+template <class CV>
+__global__ void __launch_bounds__(64) k_ec_scalar(EcArgs a) {
+  using Fn = typename CV::Fn;
+  constexpr int L = Fn::L;
+  constexpr int CB = CV::C::BYTES;
+  constexpr int NWIN = ec_windows(CV::CLS);
+  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
+  const int64_t np = a.npad;
+  const int32_t t = a.perm[p];
+  if (t < 0) return;
+  const int kidx = __builtin_amdgcn_readfirstlane(a.wave_key[p / WAVE]);
+  bool ok = a.status[p] == ST_OK && a.keys[kidx].valid;
+  const int alg = a.toks[t].alg;
+
+  // r, s: big-endian ks-byte integers decoded into LE words by k_prep; any bit
+  // beyond the curve's byte size makes them >= n
+  uint32_t rw[17], sw[17];
+#pragma unroll
+  for (int q = 0; q < 17; ++q) {
+    rw[q] = a.sigw[(int64_t)q * np + p];
+    sw[q] = a.sigw[(int64_t)(EC_S_ROW + q) * np + p];
+  }
+#pragma unroll
+  for (int q = 0; q < 17; ++q) {
+    if (4 * q >= CB) ok = ok && rw[q] == 0 && sw[q] == 0;
+    else if (4 * q + 4 > CB) {
+      const uint32_t hi = ~0u << (8 * (CB - 4 * q));
+      ok = ok && (rw[q] & hi) == 0 && (sw[q] & hi) == 0;
+    }
+  }
+  uint32_t r[L], s[L], e[L];
+  mp::words_to_limbs<L, 17>(r, rw);
+  mp::words_to_limbs<L, 17>(s, sw);
+  uint32_t nl[L];
+  mp::set_const<Fn>(nl, Fn::M);
+  ok = ok && !zero_limbs<L>(r) && !zero_limbs<L>(s) && lt_limbs<L>(r, nl) && lt_limbs<L>(s, nl);
+  // e = leftmost min(hlen, orderBytes) bytes of H (every order here is byte-aligned
+  // except P-521's, whose 66 bytes exceed every hash: no shift needed)  [R21]
+  {
+    const int hl = es_hash_bytes(alg) < CB ? es_hash_bytes(alg) : CB;   // multiple of 4
+    uint32_t ew[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int src = hl / 4 - 1 - q;
+      ew[q] = src >= 0 ? a.dig[(int64_t)(src < 0 ? 0 : src) * np + p] : 0u;
+    }
+    mp::words_to_limbs<L, 16>(e, ew);
+    mp::csub<Fn>(e);                       // e < 2n for every curve/hash pairing
+  }
+  // w = s^-1 (Fermat), u1 = e w, u2 = r w
+  uint32_t sm[L], wm[L], u1[L], u2[L];
+  mp::to_mont<Fn>(sm, s);
+  mp::inv<Fn>(wm, sm);
+  mp::mul<Fn>(u1, e, wm); mp::csub<Fn>(u1);
+  mp::mul<Fn>(u2, r, wm); mp::csub<Fn>(u2);
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    a.u1w[(int64_t)j * np + p] = u1[j];
+    a.u2w[(int64_t)j * np + p] = u2[j];
+  }
+  // signed 8-bit windows: u = sum d_w 2^(8w), d_w in [-127, 128]
+  int c1 = 0, c2 = 0;
+#pragma unroll
+  for (int w = 0; w < NWIN; ++w) {
+    const int bit = 8 * w, q = bit / MP_W, sh = bit % MP_W;
+    uint32_t b1 = q < L ? (u1[q] >> sh) : 0u, b2 = q < L ? (u2[q] >> sh) : 0u;
+    if (sh > MP_W - 8 && q + 1 < L) { b1 |= u1[q + 1] << (MP_W - sh); b2 |= u2[q + 1] << (MP_W - sh); }
+    int v1 = (int)(b1 & 0xffu) + c1, v2 = (int)(b2 & 0xffu) + c2;
+    c1 = v1 > 128; c2 = v2 > 128;
+    v1 -= c1 << 8; v2 -= c2 << 8;
+    a.digs[(int64_t)w * np + p] = ((uint32_t)v1 & 0xffu) | (((uint32_t)v2 & 0xffu) << 8);
+  }
+  if (!ok) a.status[p] = ST_REJECT;
+}
+
+// ------------------------------------------------------------------ point ops
+// Mixed addition P1 (Jacobian, normalized < 2p) += P2 (affine x2, y2).
+// 8M + 3S, lazy; X3, Y3 value-reduced (freduce) so they can be subtrahends.
+// An exceptional pair (P1 == +-P2) yields H == 0 and so Z3 == 0, which is
+// absorbing in later additions and is detected at the end.
+template <class Fp>
+__device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, const uint32_t* x2, const uint32_t* y2) {
+  constexpr int L = Fp::L;
+  uint32_t z1z1[L], u2[L], t[L], s2[L], h[L], r[L], hh[L], hhh[L], v[L];
+  mp::sqr<Fp>(z1z1, Z);
+  mp::mul<Fp>(u2, x2, z1z1);
+  mp::mul<Fp>(t, Z, z1z1);
+  mp::mul<Fp>(s2, y2, t);
+  mp::sub<Fp>(h, u2, X);
+  mp::sub<Fp>(r, s2, Y);
+  mp::sqr<Fp>(hh, h);
+  mp::mul<Fp>(hhh, h, hh);
+  mp::mul<Fp>(v, X, hh);
+  mp::mul<Fp>(Z, Z, h);
+  // X3 = r^2 - (hhh + 2v)
+  mp::add<Fp>(t, hhh, v); mp::add<Fp>(t, t, v); mp::freduce<Fp>(t);
+  uint32_t r2[L];
+  mp::sqr<Fp>(r2, r);
+  uint32_t y1[L];
+  mp::copy<Fp>(y1, Y);
+  mp::sub<Fp>(X, r2, t); mp::freduce<Fp>(X);
+  // Y3 = r (v - X3) - Y1 hhh
+  mp::sub<Fp>(t, v, X);
+  mp::mul<Fp>(Y, r, t);
+  mp::mul<Fp>(t, y1, hhh);
+  mp::sub<Fp>(Y, Y, t); mp::freduce<Fp>(Y);
+}
+
+template <class CV>
+__device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z, bool& empty,
+                                           const uint32_t* __restrict__ tab, int w, int d) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS);
+  if (d == 0) return;
+  const int ad = d < 0 ? -d : d;
+  const uint32_t* ent = tab + ((int64_t)w * COMB_ENTRIES + (ad - 1)) * STRIDE;
+  uint32_t x2[L], y2[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) { x2[j] = ent[j]; y2[j] = ent[L + j]; }
+  if (d < 0) mp::neg<Fp>(y2, y2);
+  if (empty) {
+    mp::copy<Fp>(X, x2);
+    mp::copy<Fp>(Y, y2); mp::freduce<Fp>(Y);
+    mp::set_const<Fp>(Z, Fp::ONE);
+    empty = false;
+  } else {
+    madd<Fp>(X, Y, Z, x2, y2);
+  }
+}
+
+template <class CV>
+__global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
+  using Fp = typename CV::Fp;
+  using Fn = typename CV::Fn;
+  constexpr int L = Fp::L;
+  constexpr int NWIN = ec_windows(CV::CLS);
+  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
+  const int64_t np = a.npad;
+  const int32_t t = a.perm[p];
+  if (t < 0) return;
+  if (a.status[p] != ST_OK) { a.verdict_pad[p] = 0; return; }
+  const int kidx = __builtin_amdgcn_readfirstlane(a.wave_key[p / WAVE]);
+  const uint32_t* __restrict__ qtab = a.keyblob + a.keys[kidx].tab_off;
+  const uint32_t* __restrict__ gtab = a.gtab;
+
+  uint32_t X[L], Y[L], Z[L];
+  bool empty = true;
+  for (int w = 0; w < NWIN; ++w) {
+    const uint32_t dd = a.digs[(int64_t)w * np + p];
+    const int d1 = (int)(int8_t)(dd & 0xffu);
+    const int d2 = (int)(int8_t)((dd >> 8) & 0xffu);
+    add_window<CV>(X, Y, Z, empty, gtab, w, d1);
+    add_window<CV>(X, Y, Z, empty, qtab, w, d2);
+  }
+  if (empty) { a.verdict_pad[p] = 0; return; }           // R = infinity (unreachable: u2 != 0)
+  uint32_t zc[L];
+  mp::copy<Fp>(zc, Z);
+  mp::canon<Fp>(zc);
+  if (mp::is_zero_canon<Fp>(zc)) {                        // exceptional case: exact recompute
+    const uint32_t idx = atomicAdd(a.exc_count, 1u);
+    a.exc_list[idx] = (int32_t)p;
+    a.status[p] = ST_EXCEPTIONAL;
+    return;
+  }
+  // x(R) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2)
+  uint32_t rw[17], r[L];
+#pragma unroll
+  for (int q = 0; q < 17; ++q) rw[q] = a.sigw[(int64_t)q * np + p];
+  mp::words_to_limbs<L, 17>(r, rw);
+  uint32_t zz[L], rm[L], tt[L];
+  mp::sqr<Fp>(zz, Z);
+  mp::to_mont<Fp>(rm, r);
+  mp::mul<Fp>(tt, rm, zz);
+  bool ok = mp::eq_mod<Fp>(X, tt);
+  if (!ok) {
+    uint32_t rn[L], pl[L];
+    mp::add<Fp>(rn, r, Fn::M);
+    mp::norm<Fp>(rn);
+    mp::set_const<Fp>(pl, Fp::M);
+    if (lt_limbs<L>(rn, pl)) {
+      mp::to_mont<Fp>(rm, rn);
+      mp::mul<Fp>(tt, rm, zz);
+      ok = mp::eq_mod<Fp>(X, tt);
+    }
+  }
+  a.verdict_pad[p] = ok;
+}
+
+// ------------------------------------------------------------------ exact path
+// Jacobian points with an explicit infinity flag; every coordinate kept
+// normalized (< 2p) so any of them can be a subtrahend.
+template <class Fp>
+struct JPt { uint32_t X[Fp::L], Y[Fp::L], Z[Fp::L]; bool inf; };
+
+template <class Fp>
+__device__ bool is_zero_mod(const uint32_t* a) {
+  uint32_t c[Fp::L];
+  mp::copy<Fp>(c, a);
+  mp::canon<Fp>(c);
+  return mp::is_zero_canon<Fp>(c);
+}
+
+template <class Fp>
+__device__ void times2(uint32_t* r, const uint32_t* a) {     // r = 2a, normalized
+  mp::add<Fp>(r, a, a);
+  mp::freduce<Fp>(r);
+}
+
+template <class CV>
+__device__ void jdbl(JPt<typename CV::Fp>& R, const JPt<typename CV::Fp>& P) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  if (P.inf || is_zero_mod<Fp>(P.Y)) { R.inf = true; return; }
+  uint32_t delta[L], gamma[L], beta[L], t1[L], t2[L], alpha[L], b2[L], b4[L], b8[L], x3[L], y3[L], z3[L];
+  mp::sqr<Fp>(delta, P.Z);
+  mp::sqr<Fp>(gamma, P.Y);
+  mp::mul<Fp>(beta, P.X, gamma);
+  mp::sub<Fp>(t1, P.X, delta);
+  mp::add<Fp>(t2, P.X, delta);
+  mp::mul<Fp>(alpha, t1, t2);
+  uint32_t three[L];
+  mp::set_const<Fp>(three, CV::C::THREE_M);
+  mp::mul<Fp>(alpha, alpha, three);                 // 3 (X - delta)(X + delta)
+  times2<Fp>(b2, beta); times2<Fp>(b4, b2); times2<Fp>(b8, b4);
+  mp::sqr<Fp>(x3, alpha);
+  mp::sub<Fp>(x3, x3, b8); mp::freduce<Fp>(x3);     // X3 = alpha^2 - 8 beta
+  mp::mul<Fp>(z3, P.Y, P.Z);
+  times2<Fp>(z3, z3);                               // Z3 = 2 Y Z
+  mp::sub<Fp>(t1, b4, x3);
+  mp::mul<Fp>(y3, alpha, t1);
+  mp::sqr<Fp>(t2, gamma);
+  times2<Fp>(t2, t2); times2<Fp>(t2, t2); times2<Fp>(t2, t2);
+  mp::sub<Fp>(y3, y3, t2); mp::freduce<Fp>(y3);     // Y3 = alpha (4 beta - X3) - 8 gamma^2
+  mp::copy<Fp>(R.X, x3); mp::copy<Fp>(R.Y, y3); mp::copy<Fp>(R.Z, z3);
+  R.inf = false;
+}
+
+template <class CV>
+__device__ void jadd(JPt<typename CV::Fp>& R, const JPt<typename CV::Fp>& P, const JPt<typename CV::Fp>& Q) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  if (P.inf) { R = Q; return; }
+  if (Q.inf) { R = P; return; }
+  uint32_t z1z1[L], z2z2[L], u1[L], u2[L], s1[L], s2[L], t[L], h[L], rr[L];
+  mp::sqr<Fp>(z1z1, P.Z); mp::sqr<Fp>(z2z2, Q.Z);
+  mp::mul<Fp>(u1, P.X, z2z2); mp::mul<Fp>(u2, Q.X, z1z1);
+  mp::mul<Fp>(t, Q.Z, z2z2); mp::mul<Fp>(s1, P.Y, t);
+  mp::mul<Fp>(t, P.Z, z1z1); mp::mul<Fp>(s2, Q.Y, t);
+  mp::sub<Fp>(h, u2, u1); mp::freduce<Fp>(h);
+  mp::sub<Fp>(rr, s2, s1); mp::freduce<Fp>(rr);
+  if (is_zero_mod<Fp>(h)) {
+    if (is_zero_mod<Fp>(rr)) { jdbl<CV>(R, P); return; }
+    R.inf = true;
+    return;
+  }
+  uint32_t hh[L], hhh[L], v[L], x3[L], y3[L], z3[L];
+  mp::sqr<Fp>(hh, h); mp::mul<Fp>(hhh, h, hh); mp::mul<Fp>(v, u1, hh);
+  mp::add<Fp>(t, hhh, v); mp::add<Fp>(t, t, v); mp::freduce<Fp>(t);
+  mp::sqr<Fp>(x3, rr); mp::sub<Fp>(x3, x3, t); mp::freduce<Fp>(x3);
+  mp::sub<Fp>(t, v, x3); mp::mul<Fp>(y3, rr, t);
+  mp::mul<Fp>(t, s1, hhh); mp::sub<Fp>(y3, y3, t); mp::freduce<Fp>(y3);
+  mp::mul<Fp>(t, P.Z, Q.Z); mp::mul<Fp>(z3, t, h);
+  mp::copy<Fp>(R.X, x3); mp::copy<Fp>(R.Y, y3); mp::copy<Fp>(R.Z, z3);
+  R.inf = false;
+}
+
+template <class CV>
+__device__ void affine_point(JPt<typename CV::Fp>& P, const uint32_t* xm, const uint32_t* ym) {
+  using Fp = typename CV::Fp;
+  mp::copy<Fp>(P.X, xm); mp::copy<Fp>(P.Y, ym); mp::set_const<Fp>(P.Z, Fp::ONE);
+  P.inf = false;
+}
+
+template <class CV>
+__global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
+  using Fp = typename CV::Fp;
+  using Fn = typename CV::Fn;
+  constexpr int L = Fp::L;
+  const uint32_t cnt = *a.exc_count;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    const int64_t p = a.exc_list[i];
+    const int64_t np = a.npad;
+    const int kidx = a.wave_key[p / WAVE];
+    const uint32_t* aux = a.keyblob + a.keys[kidx].aux_off;
+    uint32_t u1[L], u2[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) { u1[j] = a.u1w[(int64_t)j * np + p]; u2[j] = a.u2w[(int64_t)j * np + p]; }
+    JPt<Fp> G, Q, GQ, R;
+    uint32_t gx[L], gy[L];
+    mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
+    affine_point<CV>(G, gx, gy);
+    affine_point<CV>(Q, aux, aux + L);
+    jadd<CV>(GQ, G, Q);
+    R.inf = true;
+    for (int b = Fn::BITS - 1; b >= 0; --b) {
+      jdbl<CV>(R, R);
+      const int q = b / MP_W, sh = b % MP_W;
+      const bool b1 = (u1[q] >> sh) & 1u, b2 = (u2[q] >> sh) & 1u;
+      if (b1 && b2) jadd<CV>(R, R, GQ);
+      else if (b1) jadd<CV>(R, R, G);
+      else if (b2) jadd<CV>(R, R, Q);
+    }
+    bool ok = false;
+    if (!R.inf) {
+      uint32_t zi[L], zi2[L], xa[L], x[L];
+      mp::inv<Fp>(zi, R.Z);
+      mp::sqr<Fp>(zi2, zi);
+      mp::mul<Fp>(xa, R.X, zi2);
+      mp::from_mont<Fp>(x, xa);                  // canonical x < p
+      // x mod n (x < p < 2n)
+      uint32_t nl[L], d[L];
+      mp::set_const<Fp>(nl, Fn::M);
+      if (!lt_limbs<L>(x, nl)) {
+        int32_t br = 0;
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const int32_t tt = (int32_t)x[j] - (int32_t)nl[j] + br;
+          d[j] = (uint32_t)tt & MP_MASK;
+          br = tt >> MP_W;
+        }
+        mp::copy<Fp>(x, d);
+      }
+      uint32_t rw[17], r[L];
+#pragma unroll
+      for (int q = 0; q < 17; ++q) rw[q] = a.sigw[(int64_t)q * np + p];
+      mp::words_to_limbs<L, 17>(r, rw);
+      uint32_t o = 0;
+#pragma unroll
+      for (int j = 0; j < L; ++j) o |= x[j] ^ r[j];
+      ok = o == 0;
+    }
+    a.verdict_pad[p] = ok;
+    a.status[p] = ST_OK;
+  }
+}
+
+// ------------------------------------------------------------------ staging
+// thread per key: validate (coordinates < p, on the curve) and convert to Montgomery
+template <class CV>
+__global__ void k_ec_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DevKey& K = keys[idx[i]];
+  uint32_t* aux = blob + K.aux_off;
+  uint32_t x[L], y[L], pl[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) { x[j] = aux[j]; y[j] = aux[L + j]; }
+  mp::set_const<Fp>(pl, Fp::M);
+  bool ok = K.valid && lt_limbs<L>(x, pl) && lt_limbs<L>(y, pl);
+  uint32_t xm[L], ym[L], lhs[L], rhs[L], t[L], three[L], b[L];
+  mp::to_mont<Fp>(xm, x);
+  mp::to_mont<Fp>(ym, y);
+  mp::sqr<Fp>(lhs, ym);
+  mp::sqr<Fp>(t, xm); mp::mul<Fp>(rhs, t, xm);
+  mp::set_const<Fp>(three, CV::C::THREE_M);
+  mp::mul<Fp>(t, xm, three);
+  mp::sub<Fp>(rhs, rhs, t);
+  mp::set_const<Fp>(b, CV::C::B_M);
+  mp::add<Fp>(rhs, rhs, b);
+  ok = ok && mp::eq_mod<Fp>(rhs, lhs);
+  mp::canon<Fp>(xm); mp::canon<Fp>(ym);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { aux[j] = xm[j]; aux[L + j] = ym[j]; }
+  K.valid = ok ? 1 : 0;
+}
+
+// thread per (window w, digit d): entry = d * 2^(8w) * B in affine Montgomery form
+template <class CV>
+__device__ void table_entry(uint32_t* out, const uint32_t* bx, const uint32_t* by, int w, int d) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  JPt<Fp> P, acc;
+  affine_point<CV>(P, bx, by);
+  for (int i = 0; i < 8 * w; ++i) jdbl<CV>(P, P);
+  acc.inf = true;
+  for (int bit = 7; bit >= 0; --bit) {
+    jdbl<CV>(acc, acc);
+    if ((d >> bit) & 1) jadd<CV>(acc, acc, P);
+  }
+  uint32_t zi[L], zi2[L], zi3[L], x[L], y[L];
+  mp::inv<Fp>(zi, acc.Z);
+  mp::sqr<Fp>(zi2, zi);
+  mp::mul<Fp>(zi3, zi2, zi);
+  mp::mul<Fp>(x, acc.X, zi2);
+  mp::mul<Fp>(y, acc.Y, zi3);
+  mp::canon<Fp>(x); mp::canon<Fp>(y);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { out[j] = x[j]; out[L + j] = y[j]; }
+}
+
+template <class CV>
+__global__ void k_ec_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  constexpr int NWIN = ec_windows(CV::CLS), STRIDE = ec_stride(CV::CLS);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (k >= n || e >= NWIN * COMB_ENTRIES) return;
+  const DevKey& K = keys[idx[k]];
+  if (!K.valid) return;
+  const uint32_t* aux = blob + K.aux_off;
+  const int w = e / COMB_ENTRIES, d = e % COMB_ENTRIES + 1;
+  table_entry<CV>(blob + K.tab_off + (int64_t)e * STRIDE, aux, aux + CV::Fp::L, w, d);
+}
+
+template <class CV>
+__global__ void k_ec_table_g(uint32_t* tab) {
+  constexpr int NWIN = ec_windows(CV::CLS), STRIDE = ec_stride(CV::CLS);
+  using Fp = typename CV::Fp;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= NWIN * COMB_ENTRIES) return;
+  uint32_t gx[Fp::L], gy[Fp::L];
+  mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
+  table_entry<CV>(tab + (int64_t)e * STRIDE, gx, gy, e / COMB_ENTRIES, e % COMB_ENTRIES + 1);
+}
+
+template <class CV>
+void launch_chain(const EcArgs& a, hipStream_t s) {
+  const int64_t waves = (a.end - a.begin) / WAVE;
+  dim3 g((unsigned)waves), b(WAVE);
+  (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_ec_scalar<CV>, g, b, 0, s, a);
+  hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
+  hipLaunchKernelGGL(k_ec_exact<CV>, dim3(64), b, 0, s, a);
+}
+
+}  // namespace
+
+void launch_ec(int cls, const EcArgs& a, hipStream_t s) {
+  if (a.end <= a.begin) return;
+  switch (cls) {
+    case CLS_P256: launch_chain<CurveP256>(a, s); break;
+    case CLS_P384: launch_chain<CurveP384>(a, s); break;
+    case CLS_P521: launch_chain<CurveP521>(a, s); break;
+    default: break;
+  }
+}
+
+void launch_ec_keyprep(int cls, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
+  if (n <= 0) return;
+  dim3 g1((n + 63) / 64), b(64);
+  const int nwin = ec_windows(cls);
+  dim3 g2((nwin * COMB_ENTRIES + 63) / 64, n);
+  switch (cls) {
+    case CLS_P256:
+      hipLaunchKernelGGL(k_ec_keyprep<CurveP256>, g1, b, 0, s, keys, blob, idx, n);
+      hipLaunchKernelGGL(k_ec_table_keys<CurveP256>, g2, b, 0, s, keys, blob, idx, n);
+      break;
+    case CLS_P384:
+      hipLaunchKernelGGL(k_ec_keyprep<CurveP384>, g1, b, 0, s, keys, blob, idx, n);
+      hipLaunchKernelGGL(k_ec_table_keys<CurveP384>, g2, b, 0, s, keys, blob, idx, n);
+      break;
+    case CLS_P521:
+      hipLaunchKernelGGL(k_ec_keyprep<CurveP521>, g1, b, 0, s, keys, blob, idx, n);
+      hipLaunchKernelGGL(k_ec_table_keys<CurveP521>, g2, b, 0, s, keys, blob, idx, n);
+      break;
+    default: break;
+  }
+}
+
+void launch_ec_gtable(int cls, uint32_t* tab, hipStream_t s) {
+  const int nwin = ec_windows(cls);
+  dim3 g((nwin * COMB_ENTRIES + 63) / 64), b(64);
+  switch (cls) {
+    case CLS_P256: hipLaunchKernelGGL(k_ec_table_g<CurveP256>, g, b, 0, s, tab); break;
+    case CLS_P384: hipLaunchKernelGGL(k_ec_table_g<CurveP384>, g, b, 0, s, tab); break;
+    case CLS_P521: hipLaunchKernelGGL(k_ec_table_g<CurveP521>, g, b, 0, s, tab); break;
+    default: break;
+  }
+}

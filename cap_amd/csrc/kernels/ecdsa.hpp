@@ -1,0 +1,41 @@
+// ecdsa.hpp -- launch interface of the ECDSA kernels (ecdsa.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "common.hpp"
+#include "prep.hpp"
+
+struct EcArgs {
+  const jg_tok_dev* toks;
+  const int32_t* perm;
+  const int32_t* wave_key;
+  const jgk::DevKey* keys;
+  const uint32_t* keyblob;
+  const uint32_t* sigw;       // r at rows 0.., s at rows EC_S_ROW.. (LE words)
+  const uint32_t* dig;        // digest rows (big-endian words)
+  uint8_t* status;
+  uint8_t* verdict_pad;
+  uint32_t* digs;             // per window: packed signed digits (d1 | d2 << 8)
+  uint32_t* u1w;              // u1, u2 canonical 28-bit limb rows (exact path)
+  uint32_t* u2w;
+  const uint32_t* gtab;       // comb table of the generator for this curve
+  int32_t* exc_list;          // padded indices needing the exact path
+  uint32_t* exc_count;
+  int64_t npad, begin, end;
+};
+
+// table geometry per curve: words per entry (x,y Montgomery limbs, 16-B aligned)
+constexpr int ec_limbs(int cls) { return cls == jgk::CLS_P256 ? 10 : cls == jgk::CLS_P384 ? 15 : 20; }
+constexpr int ec_stride(int cls) { return (2 * ec_limbs(cls) + 3) & ~3; }
+constexpr int ec_windows(int cls) { return cls == jgk::CLS_P256 ? 33 : cls == jgk::CLS_P384 ? 49 : 66; }
+constexpr int64_t ec_table_words(int cls) {
+  return (int64_t)ec_windows(cls) * jgk::COMB_ENTRIES * ec_stride(cls);
+}
+
+void launch_ec(int cls, const EcArgs& a, hipStream_t s);
+// key staging: validate each listed key (plain 28-bit limbs x,y at aux_off), write
+// Montgomery affine coordinates back to aux_off and build its comb table.
+void launch_ec_keyprep(int cls, jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);
+// generator table for a curve into `tab` (ec_table_words(cls) words)
+void launch_ec_gtable(int cls, uint32_t* tab, hipStream_t s);

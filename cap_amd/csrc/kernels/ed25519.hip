@@ -1,0 +1,295 @@
+// ed25519.hip -- Ed25519 verification on gfx950.
+//
+// Replaces go-jose edEncrypterVerifier -> crypto/ed25519.Verify (SURVEY.md a11,
+// rules R23-R26): len(sig) == 64, sig[63] & 0xE0 == 0, S < L,
+// k = SHA-512(R || A || M) mod L, R' = [S]B + [k](-A) (cofactorless), accept iff
+// encode(R') == sig[:32] byte for byte.
+//   k_ed_point  : S and k recoded to signed 8-bit windows; R' as a sum of one
+//                 precomputed multiple of B and one of -A per window (Niels-form
+//                 comb tables), extended twisted-Edwards coordinates with the
+//                 complete a = -1 addition law (no exceptional cases at all)
+//   k_ed_finish : Z^-1, canonical encoding, byte compare with R
+// Key staging decodes A with filippo.io/edwards25519 SetBytes semantics
+// (non-canonical y accepted, x = 0 with the sign bit set accepted).
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "ed25519.hpp"
+#include "mp.hpp"
+
+using namespace jgk;
+
+namespace {
+
+using Fp = ED25519P;
+using Fl = ED25519L;
+constexpr int L = Fp::L;
+
+__device__ __forceinline__ bool lt_limbs(const uint32_t* a, const uint32_t* b) {
+  int lt = 0, gt = 0;
+#pragma unroll
+  for (int j = L - 1; j >= 0; --j) {
+    const int und = !(lt | gt);
+    lt |= und & (a[j] < b[j]);
+    gt |= und & (a[j] > b[j]);
+  }
+  return lt;
+}
+
+struct EPt { uint32_t X[L], Y[L], Z[L], T[L]; };
+
+// extended + Niels (y+x, y-x, 2dxy) affine -> extended (complete, a = -1)
+__device__ __forceinline__ void add_niels(EPt& P, const uint32_t* ypx, const uint32_t* ymx, const uint32_t* t2d) {
+  uint32_t t[L], A[L], B[L], C[L], D[L], E[L], F[L], G[L], H[L];
+  mp::sub<Fp>(t, P.Y, P.X); mp::mul<Fp>(A, t, ymx);
+  mp::add<Fp>(t, P.Y, P.X); mp::mul<Fp>(B, t, ypx);
+  mp::mul<Fp>(C, P.T, t2d);
+  mp::add<Fp>(D, P.Z, P.Z); mp::norm<Fp>(D);
+  mp::sub<Fp>(E, B, A); mp::sub<Fp>(F, D, C); mp::add<Fp>(G, D, C); mp::add<Fp>(H, B, A);
+  mp::mul<Fp>(P.X, E, F); mp::mul<Fp>(P.Y, G, H); mp::mul<Fp>(P.T, E, H); mp::mul<Fp>(P.Z, F, G);
+}
+
+// extended + extended (complete)
+__device__ void add_full(EPt& R, const EPt& P, const EPt& Q) {
+  uint32_t t[L], u[L], A[L], B[L], C[L], D[L], E[L], F[L], G[L], H[L], d2[L];
+  mp::sub<Fp>(t, P.Y, P.X); mp::sub<Fp>(u, Q.Y, Q.X); mp::mul<Fp>(A, t, u);
+  mp::add<Fp>(t, P.Y, P.X); mp::add<Fp>(u, Q.Y, Q.X); mp::mul<Fp>(B, t, u);
+  mp::set_const<Fp>(d2, ED25519C::D2_M);
+  mp::mul<Fp>(t, P.T, d2); mp::mul<Fp>(C, t, Q.T);
+  mp::mul<Fp>(t, P.Z, Q.Z); mp::add<Fp>(D, t, t); mp::norm<Fp>(D);
+  mp::sub<Fp>(E, B, A); mp::sub<Fp>(F, D, C); mp::add<Fp>(G, D, C); mp::add<Fp>(H, B, A);
+  mp::mul<Fp>(R.X, E, F); mp::mul<Fp>(R.Y, G, H); mp::mul<Fp>(R.T, E, H); mp::mul<Fp>(R.Z, F, G);
+}
+
+__device__ __forceinline__ void add_window(EPt& P, const uint32_t* __restrict__ tab, int w, int d) {
+  if (d == 0) return;
+  const int ad = d < 0 ? -d : d;
+  const uint32_t* ent = tab + ((int64_t)w * COMB_ENTRIES + (ad - 1)) * ED_STRIDE;
+  uint32_t ypx[L], ymx[L], t2d[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) { ypx[j] = ent[j]; ymx[j] = ent[L + j]; t2d[j] = ent[2 * L + j]; }
+  if (d < 0) {                                // -(x, y) = (-x, y): swap y+x / y-x, negate 2dxy
+    mp::neg<Fp>(t2d, t2d);
+    add_niels(P, ymx, ypx, t2d);
+  } else {
+    add_niels(P, ypx, ymx, t2d);
+  }
+}
+
+__device__ __forceinline__ void recode(int* dg, const uint32_t* s) {
+  int c = 0;
+#pragma unroll
+  for (int w = 0; w < ED_WINDOWS; ++w) {
+    const int bit = 8 * w, q = bit / MP_W, sh = bit % MP_W;
+    uint32_t b = q < L ? (s[q] >> sh) : 0u;
+    if (sh > MP_W - 8 && q + 1 < L) b |= s[q + 1] << (MP_W - sh);
+    int v = (int)(b & 0xffu) + c;
+    c = v > 128;
+    dg[w] = v - (c << 8);
+  }
+}
+
+__global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
+  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
+  const int64_t np = a.npad;
+  const int32_t t = a.perm[p];
+  if (t < 0) return;
+  const int kidx = __builtin_amdgcn_readfirstlane(a.wave_key[p / WAVE]);
+  const DevKey& K = a.keys[kidx];
+  bool ok = a.status[p] == ST_OK && K.valid && a.siglen[p] == 64;
+  // S: canonical, and sig[63] & 0xE0 == 0
+  uint32_t sw[8], s[L];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) sw[q] = a.sigw[(int64_t)(8 + q) * np + p];
+  ok = ok && (sw[7] & 0xE0000000u) == 0;
+  mp::words_to_limbs<L, 8>(s, sw);
+  uint32_t lord[L];
+  mp::set_const<Fl>(lord, Fl::M);
+  ok = ok && lt_limbs(s, lord);
+  // k = H mod L  (H little-endian, 512 bits)
+  uint32_t k[L];
+  {
+    uint32_t hw[16], hl[2 * L];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t x = a.dig[(int64_t)q * np + p];
+      hw[q] = (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+    }
+    mp::words_to_limbs<2 * L, 16>(hl, hw);
+    uint64_t tt[2 * L];
+#pragma unroll
+    for (int j = 0; j < 2 * L; ++j) tt[j] = hl[j];
+    uint32_t kr[L], rr[L];
+    mp::mont_reduce<Fl>(kr, tt);            // H / R mod L
+    mp::set_const<Fl>(rr, Fl::RR);
+    mp::mul<Fl>(k, kr, rr);                 // H mod L (< 2L)
+    mp::csub<Fl>(k);
+  }
+  int d1[ED_WINDOWS], d2[ED_WINDOWS];
+  recode(d1, s);
+  recode(d2, k);
+  EPt P;
+#pragma unroll
+  for (int j = 0; j < L; ++j) { P.X[j] = 0; P.T[j] = 0; P.Y[j] = Fp::ONE[j]; P.Z[j] = Fp::ONE[j]; }
+  const uint32_t* __restrict__ atab = a.keyblob + K.tab_off;
+#pragma unroll 1
+  for (int w = 0; w < ED_WINDOWS; ++w) {
+    int e1 = 0, e2 = 0;
+#pragma unroll
+    for (int i = 0; i < ED_WINDOWS; ++i) if (i == w) { e1 = d1[i]; e2 = d2[i]; }
+    add_window(P, a.btab, w, e1);
+    add_window(P, atab, w, e2);
+  }
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    a.xyz[(int64_t)j * np + p] = P.X[j];
+    a.xyz[(int64_t)(L + j) * np + p] = P.Y[j];
+    a.xyz[(int64_t)(2 * L + j) * np + p] = P.Z[j];
+  }
+  if (!ok) a.status[p] = ST_REJECT;
+}
+
+__global__ void __launch_bounds__(64) k_ed_finish(EdArgs a) {
+  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
+  const int64_t np = a.npad;
+  const int32_t t = a.perm[p];
+  if (t < 0) return;
+  if (a.status[p] != ST_OK) { a.verdict_pad[p] = 0; return; }
+  uint32_t X[L], Y[L], Z[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    X[j] = a.xyz[(int64_t)j * np + p];
+    Y[j] = a.xyz[(int64_t)(L + j) * np + p];
+    Z[j] = a.xyz[(int64_t)(2 * L + j) * np + p];
+  }
+  uint32_t zi[L], x[L], y[L], tt[L];
+  mp::inv<Fp>(zi, Z);
+  mp::mul<Fp>(tt, X, zi); mp::from_mont<Fp>(x, tt);
+  mp::mul<Fp>(tt, Y, zi); mp::from_mont<Fp>(y, tt);
+  uint32_t enc[8];
+  mp::limbs_to_words<L, 8>(enc, y);
+  enc[7] = (enc[7] & 0x7fffffffu) | ((x[0] & 1u) << 31);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) diff |= enc[q] ^ a.sigw[(int64_t)q * np + p];
+  a.verdict_pad[p] = diff == 0;
+}
+
+// ------------------------------------------------------------------ staging
+__device__ void niels_entry(uint32_t* out, const EPt& P) {
+  uint32_t zi[L], x[L], y[L], t[L], d2[L];
+  mp::inv<Fp>(zi, P.Z);
+  mp::mul<Fp>(x, P.X, zi); mp::canon<Fp>(x);
+  mp::mul<Fp>(y, P.Y, zi); mp::canon<Fp>(y);
+  uint32_t ypx[L], ymx[L], t2d[L];
+  mp::add<Fp>(ypx, y, x); mp::canon<Fp>(ypx);
+  mp::sub<Fp>(ymx, y, x); mp::canon<Fp>(ymx);
+  mp::mul<Fp>(t, x, y);
+  mp::set_const<Fp>(d2, ED25519C::D2_M);
+  mp::mul<Fp>(t2d, t, d2); mp::canon<Fp>(t2d);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { out[j] = ypx[j]; out[L + j] = ymx[j]; out[2 * L + j] = t2d[j]; }
+}
+
+__device__ void table_entry(uint32_t* out, const uint32_t* bx, const uint32_t* by, int w, int d) {
+  EPt P, acc;
+  mp::copy<Fp>(P.X, bx); mp::copy<Fp>(P.Y, by); mp::set_const<Fp>(P.Z, Fp::ONE);
+  mp::mul<Fp>(P.T, bx, by);
+  for (int i = 0; i < 8 * w; ++i) add_full(P, P, P);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { acc.X[j] = 0; acc.T[j] = 0; acc.Y[j] = Fp::ONE[j]; acc.Z[j] = Fp::ONE[j]; }
+  for (int bit = 7; bit >= 0; --bit) {
+    add_full(acc, acc, acc);
+    if ((d >> bit) & 1) add_full(acc, acc, P);
+  }
+  niels_entry(out, acc);
+}
+
+__global__ void k_ed_table_b(uint32_t* tab) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ED_WINDOWS * COMB_ENTRIES) return;
+  uint32_t bx[L], by[L];
+  mp::set_const<Fp>(bx, ED25519C::BX_M); mp::set_const<Fp>(by, ED25519C::BY_M);
+  table_entry(tab + (int64_t)e * ED_STRIDE, bx, by, e / COMB_ENTRIES, e % COMB_ENTRIES + 1);
+}
+
+// thread per key: decode A (SetBytes semantics), store -A affine at aux + 8
+__global__ void k_ed_decode(DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DevKey& K = keys[idx[i]];
+  uint32_t* aux = blob + K.aux_off;
+  uint32_t w[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) w[q] = aux[q];
+  const uint32_t sign = w[7] >> 31;
+  w[7] &= 0x7fffffffu;
+  uint32_t y[L];
+  mp::words_to_limbs<L, 8>(y, w);
+  mp::csub<Fp>(y);                              // y < 2^255 < 2p: reduce non-canonical y
+  uint32_t ym[L], yy[L], u[L], v[L], vi[L], xx[L], x[L], c[L], one[L], dm[L];
+  mp::to_mont<Fp>(ym, y);
+  mp::sqr<Fp>(yy, ym);
+  mp::set_const<Fp>(one, Fp::ONE);
+  mp::sub<Fp>(u, yy, one);                      // y^2 - 1
+  mp::set_const<Fp>(dm, ED25519C::D_M);
+  mp::mul<Fp>(v, yy, dm); mp::add<Fp>(v, v, one);   // d y^2 + 1
+  mp::inv<Fp>(vi, v);
+  mp::mul<Fp>(xx, u, vi);                       // x^2
+  mp::pow_e<Fp>(x, xx, ED25519C::EXP_SQRT, ED25519C::EXP_SQRT_BITS, false);
+  mp::sqr<Fp>(c, x);
+  bool ok = mp::eq_mod<Fp>(c, xx);
+  if (!ok) {
+    uint32_t sm[L];
+    mp::set_const<Fp>(sm, ED25519C::SQRTM1_M);
+    mp::mul<Fp>(x, x, sm);
+    mp::sqr<Fp>(c, x);
+    ok = mp::eq_mod<Fp>(c, xx);
+  }
+  uint32_t xp[L];
+  mp::from_mont<Fp>(xp, x);
+  mp::canon<Fp>(x);
+  if ((xp[0] & 1u) != sign) {                   // select the root with the requested sign
+    uint32_t nx[L];
+    mp::neg<Fp>(nx, x); mp::canon<Fp>(nx);
+    mp::copy<Fp>(x, nx);
+  }
+  // -A = (-x, y)
+  uint32_t nx[L];
+  mp::neg<Fp>(nx, x); mp::canon<Fp>(nx);
+  mp::canon<Fp>(ym);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { aux[8 + j] = nx[j]; aux[8 + L + j] = ym[j]; }
+  K.valid = (K.valid && ok) ? 1 : 0;
+}
+
+__global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (k >= n || e >= ED_WINDOWS * COMB_ENTRIES) return;
+  const DevKey& K = keys[idx[k]];
+  if (!K.valid) return;
+  const uint32_t* aux = blob + K.aux_off + 8;
+  table_entry(blob + K.tab_off + (int64_t)e * ED_STRIDE, aux, aux + L, e / COMB_ENTRIES, e % COMB_ENTRIES + 1);
+}
+
+}  // namespace
+
+void launch_ed(const EdArgs& a, hipStream_t s) {
+  const int64_t waves = (a.end - a.begin) / WAVE;
+  if (waves <= 0) return;
+  dim3 g((unsigned)waves), b(WAVE);
+  hipLaunchKernelGGL(k_ed_point, g, b, 0, s, a);
+  hipLaunchKernelGGL(k_ed_finish, g, b, 0, s, a);
+}
+
+void launch_ed_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_ed_decode, dim3((n + 63) / 64), dim3(64), 0, s, keys, blob, idx, n);
+  hipLaunchKernelGGL(k_ed_table_keys, dim3((ED_WINDOWS * COMB_ENTRIES + 63) / 64, n), dim3(64), 0, s,
+                     keys, blob, idx, n);
+}
+
+void launch_ed_btable(uint32_t* tab, hipStream_t s) {
+  hipLaunchKernelGGL(k_ed_table_b, dim3((ED_WINDOWS * COMB_ENTRIES + 63) / 64), dim3(64), 0, s, tab);
+}

@@ -1,0 +1,275 @@
+// mp.hpp -- fixed-modulus multi-precision arithmetic for the EC / Ed25519
+// verify kernels on gfx950.
+//
+// Representation: L limbs of 28 bits held in 32-bit VGPRs ("lazy"): limbs may
+// temporarily exceed 28 bits and values may exceed the modulus by a small
+// multiple.  Products accumulate in 64-bit VGPR pairs with v_mad_u64_u32
+// (one instruction per 28x28 partial product, no carry chains: on gfx950 a
+// v_mad_u64_u32 issues at the rate of a plain add, profiles/r01_int_rates.json,
+// so eliminating carry instructions halves the instruction count).
+//
+// Bounds (checked in tools/gen_field_consts.py, R = 2^(28L) > 4096 m):
+//   mul/sqr inputs : limbs < 3*2^28, value(a)*value(b) < R*m
+//   mul/sqr output : limbs < 2^28, value < 2m          ("normalized")
+//   sub(a, b)      : b limbs < 2^28 and value(b) < 2m; result = a + KSUB - b,
+//                    KSUB = 4m limb-padded so no limb goes negative
+//   freduce        : any non-negative value < 2^(FOLD_S+32) -> normalized, < 2m
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "field_consts.hpp"
+#include "mad.hpp"
+
+#define MP_W 28
+#define MP_MASK 0x0fffffffu
+#define MPD __device__ __forceinline__
+
+namespace mp {
+
+template <class F>
+MPD void mont_reduce(uint32_t* r, uint64_t* t) {
+  constexpr int L = F::L;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const uint32_t m = ((uint32_t)t[i] * F::NP) & MP_MASK;
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+      if (F::M[j] != 0) mad64s(t[i + j], m, F::M[j]);
+    t[i + 1] += t[i] >> MP_W;
+  }
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    const uint64_t v = t[L + j] + c;
+    r[j] = (uint32_t)v & MP_MASK;
+    c = v >> MP_W;
+  }
+}
+
+// r = a*b/R mod m
+template <class F>
+MPD void mul(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  constexpr int L = F::L;
+  uint64_t t[2 * L];
+#pragma unroll
+  for (int k = 0; k < 2 * L; ++k) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i)
+#pragma unroll
+    for (int j = 0; j < L; ++j) mad64(t[i + j], a[i], b[j]);
+  mont_reduce<F>(r, t);
+}
+
+// r = a^2/R mod m  (cross products once, doubled operand)
+template <class F>
+MPD void sqr(uint32_t* r, const uint32_t* a) {
+  constexpr int L = F::L;
+  uint64_t t[2 * L];
+  uint32_t a2[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) a2[i] = a[i] << 1;
+#pragma unroll
+  for (int k = 0; k < 2 * L; ++k) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    mad64(t[2 * i], a[i], a[i]);
+#pragma unroll
+    for (int j = i + 1; j < L; ++j) mad64(t[i + j], a2[i], a[j]);
+  }
+  mont_reduce<F>(r, t);
+}
+
+template <class F>
+MPD void add(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+#pragma unroll
+  for (int j = 0; j < F::L; ++j) r[j] = a[j] + b[j];
+}
+
+template <class F>
+MPD void sub(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+#pragma unroll
+  for (int j = 0; j < F::L; ++j) r[j] = a[j] + F::KSUB[j] - b[j];
+}
+
+// m - b (negation of a normalized value), result limbs < 2^29 + 2^28
+template <class F>
+MPD void neg(uint32_t* r, const uint32_t* b) {
+#pragma unroll
+  for (int j = 0; j < F::L; ++j) r[j] = F::KSUB[j] - b[j];
+}
+
+template <class F>
+MPD void copy(uint32_t* r, const uint32_t* a) {
+#pragma unroll
+  for (int j = 0; j < F::L; ++j) r[j] = a[j];
+}
+
+// carry-propagate: limbs < 2^28, value unchanged (value must be < 2^(28L))
+template <class F>
+MPD void norm(uint32_t* r) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < F::L; ++j) {
+    const uint32_t v = r[j] + c;
+    r[j] = v & MP_MASK;
+    c = v >> MP_W;
+  }
+}
+
+// value reduction for pseudo-Mersenne-shaped primes: fold bits >= FOLD_S by 2^FOLD_S mod m
+template <class F>
+MPD void freduce(uint32_t* r) {
+  constexpr int L = F::L;
+  constexpr int q = F::FOLD_S / MP_W, s = F::FOLD_S % MP_W;
+  norm<F>(r);
+  uint32_t h = r[q] >> s;
+  if constexpr (q + 1 < L) h |= r[q + 1] << (MP_W - s);
+  r[q] &= (1u << s) - 1u;
+#pragma unroll
+  for (int j = q + 1; j < L; ++j) r[j] = 0;
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    uint64_t v = (uint64_t)r[j] + c;
+    if (F::FOLDC[j] != 0) mad64s(v, h, F::FOLDC[j]);
+    r[j] = (uint32_t)v & MP_MASK;
+    c = v >> MP_W;
+  }
+}
+
+// normalized value < 2m  ->  canonical [0, m)
+template <class F>
+MPD void csub(uint32_t* r) {
+  uint32_t d[F::L];
+  int32_t br = 0;
+#pragma unroll
+  for (int j = 0; j < F::L; ++j) {
+    const int32_t v = (int32_t)r[j] - (int32_t)F::M[j] + br;
+    d[j] = (uint32_t)v & MP_MASK;
+    br = v >> MP_W;                       // arithmetic shift: 0 or -1
+  }
+  const bool keep = br < 0;
+#pragma unroll
+  for (int j = 0; j < F::L; ++j) r[j] = keep ? r[j] : d[j];
+}
+
+template <class F>
+MPD void canon(uint32_t* r) {
+  freduce<F>(r);
+  csub<F>(r);
+}
+
+template <class F>
+MPD bool is_zero_canon(const uint32_t* r) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < F::L; ++j) o |= r[j];
+  return o == 0;
+}
+
+template <class F>
+MPD void set_const(uint32_t* r, const uint32_t* c) {
+#pragma unroll
+  for (int j = 0; j < F::L; ++j) r[j] = c[j];
+}
+
+// plain integer (28-bit limbs, value < m) -> Montgomery form
+template <class F>
+MPD void to_mont(uint32_t* r, const uint32_t* a) {
+  uint32_t rr[F::L];
+  set_const<F>(rr, F::RR);
+  mul<F>(r, a, rr);
+}
+
+// Montgomery form -> canonical plain integer in [0, m)
+template <class F>
+MPD void from_mont(uint32_t* r, const uint32_t* a) {
+  constexpr int L = F::L;
+  uint64_t t[2 * L];
+#pragma unroll
+  for (int k = 0; k < 2 * L; ++k) t[k] = k < L ? a[k] : 0;
+  mont_reduce<F>(r, t);
+  csub<F>(r);
+}
+
+// r = x^E for an exponent held in a constexpr array of 28-bit limbs (read with
+// wave-uniform indices -> scalar loads).  `minus2` subtracts 2 from limb 0
+// (E = m - 2 for Fermat inversion; every modulus here has limb 0 >= 2).
+// Left-to-right 4-bit fixed window; the window value is uniform across the
+// wave, so the table select is a uniform compare chain, not a divergent branch.
+template <class F>
+MPD void pow_e(uint32_t* r, const uint32_t* x, const uint32_t* E, int ebits, bool minus2) {
+  constexpr int L = F::L;
+  uint32_t tab[16][L];
+  set_const<F>(tab[0], F::ONE);
+  copy<F>(tab[1], x);
+#pragma unroll
+  for (int i = 2; i < 16; ++i) mul<F>(tab[i], tab[i - 1], x);
+  uint32_t acc[L];
+  set_const<F>(acc, F::ONE);
+  const int top = (ebits + 3) & ~3;
+  for (int b = top - 4; b >= 0; b -= 4) {
+    sqr<F>(acc, acc); sqr<F>(acc, acc); sqr<F>(acc, acc); sqr<F>(acc, acc);
+    const int w = b / MP_W, o = b % MP_W;
+    const uint32_t lo = E[w] - ((minus2 && w == 0) ? 2u : 0u);
+    uint32_t nib = lo >> o;
+    if (o > MP_W - 4 && w + 1 < L) nib |= E[w + 1] << (MP_W - o);
+    nib &= 15u;
+    uint32_t sel[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) sel[j] = tab[0][j];
+#pragma unroll
+    for (int i = 1; i < 16; ++i)
+      if (nib == (uint32_t)i) {
+#pragma unroll
+        for (int j = 0; j < L; ++j) sel[j] = tab[i][j];
+      }
+    mul<F>(acc, acc, sel);
+  }
+  copy<F>(r, acc);
+}
+
+// Fermat inverse r = x^(m-2), Montgomery form in and out (m prime)
+template <class F>
+MPD void inv(uint32_t* r, const uint32_t* x) {
+  pow_e<F>(r, x, F::M, F::BITS, true);
+}
+
+// canonical equality of two normalized values < 2m (reduces both)
+template <class F>
+MPD bool eq_mod(const uint32_t* a, const uint32_t* b) {
+  uint32_t d[F::L];
+  sub<F>(d, a, b);
+  canon<F>(d);
+  return is_zero_canon<F>(d);
+}
+
+// load a big-endian byte string's integer (given as little-endian 32-bit words
+// w[0..nw)) into 28-bit limbs (truncating to L limbs)
+template <int L, int NW>
+MPD void words_to_limbs(uint32_t* r, const uint32_t* w) {
+  constexpr int nw = NW;
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    const int bit = MP_W * j, q = bit / 32, s = bit % 32;
+    uint32_t v = q < nw ? (w[q] >> s) : 0u;
+    if (s > 32 - MP_W && q + 1 < nw) v |= w[q + 1] << (32 - s);
+    r[j] = v & MP_MASK;
+  }
+}
+
+template <int L, int NW>
+MPD void limbs_to_words(uint32_t* w, const uint32_t* r) {
+  constexpr int nw = NW;
+#pragma unroll
+  for (int q = 0; q < nw; ++q) w[q] = 0;
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    const int bit = MP_W * j, q = bit / 32, s = bit % 32;
+    if (q < nw) w[q] |= r[j] << s;
+    if (s > 32 - MP_W && q + 1 < nw) w[q + 1] |= r[j] >> (32 - s);
+  }
+}
+
+}  // namespace mp

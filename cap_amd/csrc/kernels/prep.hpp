@@ -1,0 +1,34 @@
+// prep.hpp -- launch interface of the prep kernel (prep.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "common.hpp"
+
+// device mirror of jg_tok (include/jg.h); layout checked by static_assert in the runtime
+struct jg_tok_dev {
+  uint64_t off;
+  uint32_t sig_in_len;
+  uint32_t sig_rel_off;
+  uint32_t sig_b64_len;
+  uint16_t key_idx;
+  uint8_t alg;
+  uint8_t flags;
+};
+
+struct PrepArgs {
+  const uint8_t* arena;
+  const jg_tok_dev* toks;
+  const int32_t* perm;        // padded index -> token index (-1 = padding)
+  const int32_t* wave_key;    // per wave: key index
+  const jgk::DevKey* keys;
+  const uint32_t* keyblob;
+  uint32_t* sigw;             // SIGW_ROWS x npad
+  uint32_t* dig;              // DIG_ROWS x npad
+  uint8_t* status;            // npad
+  uint16_t* siglen;           // npad
+  int64_t npad, begin, end;
+  int32_t zrows;              // signature rows the class's kernel reads
+};
+
+void launch_prep(int cls, const PrepArgs& a, hipStream_t s);

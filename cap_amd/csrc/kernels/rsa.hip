@@ -1,0 +1,470 @@
+// rsa.hip -- RSA public operation + PKCS#1 v1.5 / PSS checks on gfx950.
+//
+// Replaces crypto/rsa VerifyPKCS1v15 / VerifyPSS(opts=nil) behind go-jose's
+// rsaEncrypterVerifier.verifyPayload (rules R12-R17).
+//
+// k_rsa_modexp<L,U>: one thread per token, one 64-lane wave per key-uniform
+// run of tokens.  s^e mod n by left-to-right square-and-multiply on Montgomery
+// products in 28-bit limbs (L limbs, R = 2^(28L) > 4n so no final subtraction
+// until the end).  Montgomery product = lazy CIOS:
+//   for i: T += a_i * v ; m = T0 * n' mod 2^28 ; T += m * n ; T >>= 28 (limb shift)
+// with T in 64-bit VGPR pairs (v_mad_u64_u32, no carry chains), v in VGPRs,
+// the per-lane a_i streamed from LDS (lane-contiguous, conflict-free) and the
+// modulus limbs n_j wave-uniform (scalar loads / SGPR operands).  The limb
+// shift is a register rename inside a U-times unrolled block; one physical
+// shift per block (amortised 1/U).
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "rsa.hpp"
+#include "sha2.hpp"
+#include "mad.hpp"
+
+using namespace jgk;
+
+#define W28 28
+#define M28 0x0fffffffu
+
+namespace {
+
+// ---------------------------------------------------------------- cross-lane
+// Token = group of G consecutive lanes (G = 2 or 4, inside one DPP quad);
+// lane g of the group holds limbs [g*H, (g+1)*H) of every multi-limb value.
+template <int G>
+__device__ __forceinline__ uint32_t bcast0(uint32_t x) {        // value of group lane 0
+  constexpr int ctrl = G == 2 ? 0xA0 /* quad_perm 0,0,2,2 */ : 0x00 /* 0,0,0,0 */;
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, 0xF, 0xF, false);
+}
+template <int G>
+__device__ __forceinline__ uint32_t bcast_last(uint32_t x) {    // value of group lane G-1
+  constexpr int ctrl = G == 2 ? 0xF5 /* quad_perm 1,1,3,3 */ : 0xFF /* 3,3,3,3 */;
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, 0xF, 0xF, false);
+}
+template <int G>
+__device__ __forceinline__ uint32_t from_next(uint32_t x) {     // value of group lane g+1
+  constexpr int ctrl = G == 2 ? 0xF5 /* 1,1,3,3 */ : 0xF9 /* 1,2,3,3 */;
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, 0xF, 0xF, false);
+}
+template <int G>
+__device__ __forceinline__ uint32_t from_prev(uint32_t x) {     // value of group lane g-1
+  constexpr int ctrl = G == 2 ? 0xA0 /* quad_perm 0,0,2,2 */ : 0x90 /* 0,0,1,2 */;
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, 0xF, 0xF, false);
+}
+
+// One CIOS iteration on this lane's window T[0..H) of the token's accumulator.
+//   T += a_i * v ; m = T0 * n' (group lane 0, broadcast) ; T += m * n ;
+//   lane 0: T1 += T0 >> 28 ; every lane hands T0 to the lane below, which
+//   places it in its fresh top slot T[H] (the limb shift across lanes).
+template <int H, int G>
+__device__ __forceinline__ void cios_step(uint64_t* T, uint32_t ai, const uint32_t* v, const uint32_t* n,
+                                          uint32_t np, bool lane0, bool lastl) {
+#pragma unroll
+  for (int j = 0; j < H; ++j) mad64(T[j], ai, v[j]);
+  const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
+#pragma unroll
+  for (int j = 0; j < H; ++j) mad64(T[j], m, n[j]);
+  const uint64_t c = lane0 ? (T[0] >> W28) : 0ull;
+  T[1] += c;
+  const uint32_t lo = from_next<G>((uint32_t)T[0]);
+  const uint32_t hi = from_next<G>((uint32_t)(T[0] >> 32));
+  T[H] = lastl ? 0ull : (((uint64_t)hi << 32) | lo);
+}
+
+// v <- (a * v) / R mod n with a streamed from LDS (la[i * TPW], shared by the
+// group's lanes: a broadcast read).  R = 2^(28 H G).  In: v < 2n limb-normalized.
+// Out: v < 2n, limbs < 2^28 (carries rippled across the group).
+template <int H, int G, int U, int TPW>
+__device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const uint32_t* n, uint32_t np,
+                                         bool lane0, bool lastl) {
+  constexpr int L = H * G, NB = L / U, REM = L % U;
+  uint64_t P[H + U];
+#pragma unroll
+  for (int j = 0; j < H + U; ++j) P[j] = 0;
+  for (int ib = 0; ib < NB; ++ib) {
+    uint32_t a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = la[(ib * U + u) * TPW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cios_step<H, G>(P + u, a[u], v, n, np, lane0, lastl);
+    if constexpr (2 * L > 250) {
+      // keep every 64-bit column < 2^64 (2L products of < 2^56): normalise half-way
+      if (ib == NB / 2) {
+#pragma unroll
+        for (int j = U; j < U + H - 1; ++j) { P[j + 1] += P[j] >> W28; P[j] &= M28; }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) P[j] = P[j + U];
+#pragma unroll
+    for (int j = H; j < H + U; ++j) P[j] = 0;
+  }
+#pragma unroll
+  for (int u = 0; u < REM; ++u) cios_step<H, G>(P + u, la[(NB * U + u) * TPW], v, n, np, lane0, lastl);
+  // normalise within the lane, then ripple the carries up the group: each
+  // round moves every pending carry one lane up (the top lane's carry-out is
+  // zero because the value is < 2n < 2^(28L)).
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const uint64_t t = P[REM + j] + c;
+    v[j] = (uint32_t)t & M28;
+    c = t >> W28;
+  }
+#pragma unroll
+  for (int r = 0; r < G - 1; ++r) {
+    const uint32_t clo = from_prev<G>((uint32_t)c), chi = from_prev<G>((uint32_t)(c >> 32));
+    uint64_t cin = lane0 ? 0ull : (((uint64_t)chi << 32) | clo);
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const uint64_t t = (uint64_t)v[j] + cin;
+      v[j] = (uint32_t)t & M28;
+      cin = t >> W28;
+    }
+    c = cin;
+  }
+}
+
+template <int H, int TPW>
+__device__ __forceinline__ void lds_store(uint32_t* la, const uint32_t* v, int g) {
+#pragma unroll
+  for (int j = 0; j < H; ++j) la[(g * H + j) * TPW] = v[j];
+}
+
+// limbs [gH, gH+H) of the integer held as LE 32-bit words in SoA rows
+template <int H>
+__device__ __forceinline__ void load_limbs_from_words(uint32_t* v, const uint32_t* rows, int64_t np, int64_t p,
+                                                      int g, int nrows) {
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const int bit = W28 * (g * H + j), q = bit >> 5, s = bit & 31;
+    const uint32_t w0 = q < nrows ? rows[(int64_t)q * np + p] : 0u;
+    const uint32_t w1 = (q + 1) < nrows ? rows[(int64_t)(q + 1) * np + p] : 0u;
+    const uint64_t ww = ((uint64_t)w1 << 32) | w0;
+    v[j] = (uint32_t)(ww >> s) & M28;
+  }
+}
+
+// Row-major SoA scratch: limb j of lane segment g of token p lives at
+// rows[(g*H + j) * np + p].  Addressed as (rows + j*np) [uniform, SGPR base]
+// + loff (one 32-bit VGPR lane offset, loff = g*H*np + p), so the H loads share
+// a single address VGPR instead of H 64-bit addresses.
+template <int H>
+__device__ __forceinline__ void load_limb_rows(uint32_t* v, const uint32_t* rows, int64_t np, uint32_t loff) {
+#pragma unroll
+  for (int j = 0; j < H; ++j) v[j] = (rows + (int64_t)j * np)[loff];
+}
+template <int H>
+__device__ __forceinline__ void store_limb_rows(uint32_t* rows, int64_t np, uint32_t loff, const uint32_t* v) {
+#pragma unroll
+  for (int j = 0; j < H; ++j) (rows + (int64_t)j * np)[loff] = v[j];
+}
+
+template <int H, int G, int U>
+__global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
+  constexpr int L = H * G, TPW = WAVE / G;
+  constexpr int NWOUT = (W28 * L + 31) / 32 < SIGW_ROWS ? (W28 * L + 31) / 32 : SIGW_ROWS;
+  __shared__ uint32_t lds[L * TPW];
+  const int lane = threadIdx.x;
+  const int g = lane % G, tl = lane / G;
+  const bool lane0 = g == 0, lastl = g == G - 1;
+  const int64_t pbase = a.begin + (int64_t)blockIdx.x * TPW;
+  const int64_t p = pbase + tl;
+  const int64_t np = a.npad;
+  const int kidx = __builtin_amdgcn_readfirstlane(a.wave_key[pbase / WAVE]);
+  const DevKey K = a.keys[kidx];
+  const uint32_t* __restrict__ N = a.keyblob + K.n_off;
+  const uint32_t* __restrict__ RR = a.keyblob + K.rr_off;
+  const uint32_t np28 = K.np;
+  const uint64_t e = ((uint64_t)K.e_hi << 32) | K.e_lo;
+  uint32_t* la = lds + tl;
+
+  uint32_t n[H];
+#pragma unroll
+  for (int j = 0; j < H; ++j) n[j] = N[g * H + j];
+
+  bool act = a.perm[p] >= 0 && a.status[p] == ST_OK && a.siglen[p] == (uint16_t)K.kbytes && K.valid;
+
+  const uint32_t loff = (uint32_t)((int64_t)g * H * np + p);
+  uint32_t v[H];
+  load_limbs_from_words<H>(v, a.sigw, np, p, g, SIGW_ROWS);
+  store_limb_rows<H>(a.xlr, np, loff, v);        // x as limb rows (MULX operand)
+  // sig < N (Go >= 1.20, R14): per-lane compare, the highest differing lane decides
+  {
+    int lt = 0, gt = 0;
+#pragma unroll
+    for (int j = H - 1; j >= 0; --j) {
+      const int und = !(lt | gt);
+      lt |= und & (v[j] < n[j]);
+      gt |= und & (v[j] > n[j]);
+    }
+    int code = lt ? 1 : (gt ? 2 : 0);        // 1: x<n here, 2: x>n here, 0: equal
+    // walk from the top lane down: the first lane with code != 0 decides
+    int dec = code;
+#pragma unroll
+    for (int r = 0; r < G - 1; ++r) {
+      const int up = (int)from_next<G>((uint32_t)dec);
+      dec = (!lastl && up != 0) ? up : dec;
+    }
+    dec = (int)bcast0<G>((uint32_t)dec);
+    act = act && dec == 1;
+  }
+
+  // Exponentiation as one loop over Montgomery products (one inlined copy of
+  // the product body).  Ops, left-to-right over the bits of e:
+  //   TOMONT  v = Mont(x, R^2) = xR      SQUARE  v = Mont(v, v)
+  //   MULXM   v = Mont(v, xR)            (set bits other than bit 0)
+  //   MULX    v = Mont(v, x)             (bit 0 set: leaves the Montgomery domain)
+  //   MULONE  v = Mont(v, 1)             (bit 0 clear)
+  enum { TOMONT, SQUARE, MULXM, MULX, MULONE };
+  const int ebits = 64 - __builtin_clzll(e);
+  const bool mid = ((e >> 1) & ((1ull << (ebits - 2)) - 1ull)) != 0;
+  int op = TOMONT, bit = ebits - 2;
+  for (;;) {
+    // opaque zero: stops LICM from hoisting the ~2H per-limb load addresses of
+    // the operand loads below out of the loop (they would stay live in VGPRs)
+    uint32_t z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    lds_store<H, TPW>(la, v, g);
+    if (op == TOMONT) {
+      const uint32_t* rr = RR + z + g * H;
+#pragma unroll
+      for (int j = 0; j < H; ++j) v[j] = rr[j];
+    } else if (op == MULXM) {
+      load_limb_rows<H>(v, a.xmw + z, np, loff);
+    } else if (op == MULX) {
+      load_limb_rows<H>(v, a.xlr + z, np, loff);
+    } else if (op == MULONE) {
+#pragma unroll
+      for (int j = 0; j < H; ++j) v[j] = (j == 0 && lane0) ? 1u : 0u;
+    }
+    mont_mul<H, G, U, TPW>(v, la, n, np28, lane0, lastl);
+    if (op == TOMONT) {
+      if (mid) store_limb_rows<H>(a.xmw, np, loff, v);
+      op = SQUARE;
+    } else if (op == SQUARE) {
+      if ((e >> bit) & 1ull) op = bit > 0 ? MULXM : MULX;
+      else if (bit == 0) op = MULONE;
+      else --bit;
+    } else if (op == MULXM) {
+      --bit;
+      op = SQUARE;
+    } else {
+      break;
+    }
+  }
+
+  // canonical: v < 2n -> v mod n.  d = v - n with the borrow rippled up the
+  // group (G rounds), then the top lane's final borrow picks v or d.
+  {
+    uint32_t d[H];
+    int32_t bout = 0;
+#pragma unroll
+    for (int r = 0; r < G; ++r) {
+      int32_t br = lane0 ? 0 : (int32_t)from_prev<G>((uint32_t)bout);
+#pragma unroll
+      for (int j = 0; j < H; ++j) {
+        const int32_t t = (int32_t)v[j] - (int32_t)n[j] + br;
+        d[j] = (uint32_t)t & M28;
+        br = t >> W28;
+      }
+      bout = br;
+    }
+    const int32_t b_top = (int32_t)bcast_last<G>((uint32_t)bout);
+#pragma unroll
+    for (int j = 0; j < H; ++j) v[j] = b_top < 0 ? v[j] : d[j];
+  }
+  // y as LE 32-bit words: stage limbs in LDS, each group lane converts a slice
+  lds_store<H, TPW>(la, v, g);
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): own-group LDS writes visible to the group
+  __builtin_amdgcn_wave_barrier();
+  constexpr int PER = (NWOUT + G - 1) / G;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int q = g * PER + k;
+    if (q < NWOUT) {
+      const int bit = 32 * q, j0 = bit / W28, s0 = bit % W28;
+      uint64_t acc = (uint64_t)la[j0 * TPW] >> s0;
+      int have = W28 - s0;
+      int j = j0 + 1;
+      while (have < 32 && j < L) { acc |= (uint64_t)la[j * TPW] << have; have += W28; ++j; }
+      if (act) a.yw[(int64_t)q * np + p] = (uint32_t)acc;
+    }
+  }
+  if (!act && lane0) a.status[p] = ST_REJECT;
+}
+
+// ------------------------------------------------------------------ padding
+__constant__ uint8_t DI256[19] = {0x30,0x31,0x30,0x0d,0x06,0x09,0x60,0x86,0x48,0x01,0x65,0x03,0x04,0x02,0x01,0x05,0x00,0x04,0x20};
+__constant__ uint8_t DI384[19] = {0x30,0x41,0x30,0x0d,0x06,0x09,0x60,0x86,0x48,0x01,0x65,0x03,0x04,0x02,0x02,0x05,0x00,0x04,0x30};
+__constant__ uint8_t DI512[19] = {0x30,0x51,0x30,0x0d,0x06,0x09,0x60,0x86,0x48,0x01,0x65,0x03,0x04,0x02,0x03,0x05,0x00,0x04,0x40};
+
+__device__ __forceinline__ uint32_t ybyte(const uint32_t* yw, int64_t np, int64_t p, int k, int pos) {
+  const int j = k - 1 - pos;                 // integer byte index (little-endian)
+  return (yw[(int64_t)(j >> 2) * np + p] >> ((j & 3) * 8)) & 0xffu;
+}
+__device__ __forceinline__ uint32_t dbyte(const uint32_t* dig, int64_t np, int64_t p, int i) {
+  return (dig[(int64_t)(i >> 2) * np + p] >> (24 - 8 * (i & 3))) & 0xffu;
+}
+
+// hash `len` bytes at buf (4-byte aligned) -> big-endian words
+__device__ void hash_buf(int hb, const uint8_t* buf, uint32_t len, uint32_t* out16) {
+  sha2::MemString m;
+  m.aligned = reinterpret_cast<const uint32_t*>(buf);
+  m.shift = 0;
+  m.len = len;
+  if (hb == 256) {
+    uint32_t h[8];
+    sha2::sha256_mem(h, m);
+    for (int k = 0; k < 8; ++k) out16[k] = h[k];
+  } else {
+    uint64_t h[8];
+    sha2::sha512_mem(h, hb == 384, m, nullptr, 0);
+    for (int k = 0; k < 8; ++k) { out16[2 * k] = (uint32_t)(h[k] >> 32); out16[2 * k + 1] = (uint32_t)h[k]; }
+  }
+}
+
+__global__ void __launch_bounds__(64) k_rsa_pad(RsaArgs a) {
+  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
+  const int64_t np = a.npad;
+  const int32_t t = a.perm[p];
+  if (t < 0) return;
+  uint8_t verdict = 0;
+  if (a.status[p] == ST_OK) {
+    const int kidx = a.wave_key[p / WAVE];
+    const DevKey K = a.keys[kidx];
+    const int k = K.kbytes;
+    const int alg = a.toks[t].alg;
+    const int hb = (alg == 1 || alg == 4) ? 256 : (alg == 2 || alg == 5) ? 384 : 512;
+    const int hlen = hb / 8;
+    if (alg <= 3) {
+      // PKCS#1 v1.5: EM == 00 01 FF..FF 00 || DigestInfo || H   (R15)
+      const int tlen = 19 + hlen;
+      const uint8_t* DI = hb == 256 ? DI256 : hb == 384 ? DI384 : DI512;
+      bool ok = k >= tlen + 11;
+      for (int pos = 0; pos < k && ok; ++pos) {
+        uint32_t ex;
+        if (pos == 0) ex = 0;
+        else if (pos == 1) ex = 1;
+        else if (pos < k - tlen - 1) ex = 0xff;
+        else if (pos == k - tlen - 1) ex = 0;
+        else if (pos < k - hlen) ex = DI[pos - (k - tlen)];
+        else ex = dbyte(a.dig, np, p, pos - (k - hlen));
+        ok = ybyte(a.yw, np, p, k, pos) == ex;
+      }
+      verdict = ok;
+    } else {
+      // EMSA-PSS-VERIFY with auto salt length (R16)
+      const int embits = K.embits;
+      const int emlen = (embits + 7) / 8;
+      const int lead = k - emlen;                       // 0 or 1
+      bool ok = true;
+      for (int i = 0; i < lead; ++i) ok = ok && ybyte(a.yw, np, p, k, i) == 0;
+      ok = ok && emlen >= hlen + 2;
+      ok = ok && ybyte(a.yw, np, p, k, lead + emlen - 1) == 0xbc;
+      const uint32_t bitmask = 0xffu >> (8 * emlen - embits);
+      ok = ok && (ybyte(a.yw, np, p, k, lead) & ~bitmask) == 0;
+      if (ok) {
+        uint8_t* buf = a.pss_scratch + (p - a.begin) * 1024;   // [0,512): DB ; [512,1024): work
+        uint8_t* wk = buf + 512;
+        const int dblen = emlen - hlen - 1;
+        // H = EM[dblen .. dblen+hlen)
+        for (int i = 0; i < hlen; ++i) wk[i] = (uint8_t)ybyte(a.yw, np, p, k, lead + dblen + i);
+        // DB = maskedDB ^ MGF1(H, dblen)
+        uint32_t mask[16];
+        for (int c = 0; c * hlen < dblen; ++c) {
+          wk[hlen] = (uint8_t)(c >> 24); wk[hlen + 1] = (uint8_t)(c >> 16);
+          wk[hlen + 2] = (uint8_t)(c >> 8); wk[hlen + 3] = (uint8_t)c;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          hash_buf(hb, wk, (uint32_t)hlen + 4, mask);
+          for (int i = 0; i < hlen && c * hlen + i < dblen; ++i) {
+            const int di = c * hlen + i;
+            const uint32_t mb = (mask[i >> 2] >> (24 - 8 * (i & 3))) & 0xffu;
+            buf[di] = (uint8_t)(ybyte(a.yw, np, p, k, lead + di) ^ mb);
+          }
+        }
+        buf[0] &= (uint8_t)bitmask;
+        int ps = 0;
+        while (ps < dblen && buf[ps] == 0) ++ps;
+        ok = ps < dblen && buf[ps] == 0x01;
+        if (ok) {
+          const int slen = dblen - ps - 1;
+          // M' = 0^8 || mHash || salt   (into the work area, H copied out first)
+          uint32_t Hw[16];
+          for (int i = 0; i < 16; ++i) Hw[i] = 0;
+          for (int i = 0; i < hlen; ++i) Hw[i >> 2] |= (uint32_t)wk[i] << (24 - 8 * (i & 3));
+          for (int i = 0; i < 8; ++i) wk[i] = 0;
+          for (int i = 0; i < hlen; ++i) wk[8 + i] = (uint8_t)dbyte(a.dig, np, p, i);
+          for (int i = 0; i < slen; ++i) wk[8 + hlen + i] = buf[ps + 1 + i];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          uint32_t h2[16];
+          hash_buf(hb, wk, (uint32_t)(8 + hlen + slen), h2);
+          uint32_t diff = 0;
+          for (int i = 0; i < hlen / 4; ++i) diff |= h2[i] ^ Hw[i];
+          ok = diff == 0;
+        }
+      }
+      verdict = ok;
+    }
+  }
+  a.verdict_pad[p] = verdict;
+}
+
+// ------------------------------------------------------------------ key staging
+// One thread per RSA key: n' = -n^-1 mod 2^28 and R^2 mod n (R = 2^(28 L)) by
+// modular doubling.  Runs once per jg_keys_load.
+__global__ void k_rsa_keyprep(DevKey* keys, uint32_t* blob, int nkeys) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nkeys) return;
+  DevKey& K = keys[i];
+  if (K.kind != 1 || !K.valid) return;
+  const int L = (int)K.nlimbs;
+  const uint32_t* N = blob + K.n_off;
+  uint32_t* RR = blob + K.rr_off;
+  uint32_t inv = 1;
+  for (int k = 0; k < 5; ++k) inv *= 2u - N[0] * inv;       // N[0]^-1 mod 2^32
+  K.np = (0u - inv) & M28;
+  // r = 1; double 2*28*L times mod n
+  for (int j = 0; j < L; ++j) RR[j] = j == 0 ? 1u : 0u;
+  for (int it = 0; it < 2 * W28 * L; ++it) {
+    uint32_t c = 0;
+    for (int j = 0; j < L; ++j) {
+      const uint32_t t2 = (RR[j] << 1) | c;
+      c = t2 >> W28;
+      RR[j] = t2 & M28;
+    }
+    // compare (c, RR) >= N ?
+    bool ge = c != 0;
+    if (!ge) {
+      int cmp = 0;
+      for (int j = L - 1; j >= 0 && cmp == 0; --j) cmp = (RR[j] > N[j]) - (RR[j] < N[j]);
+      ge = cmp >= 0;
+    }
+    if (ge) {
+      int32_t br = 0;
+      for (int j = 0; j < L; ++j) {
+        const int32_t t2 = (int32_t)RR[j] - (int32_t)N[j] + br;
+        RR[j] = (uint32_t)t2 & M28;
+        br = t2 >> W28;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+void launch_rsa(int cls, const RsaArgs& a, hipStream_t s) {
+  const int64_t waves = (a.end - a.begin) / WAVE;
+  if (waves <= 0) return;
+  dim3 g((unsigned)waves), b(WAVE);
+  switch (cls) {
+    case CLS_RSA2K: hipLaunchKernelGGL((k_rsa_modexp<37, 2, 8>), dim3((unsigned)(waves * 2)), b, 0, s, a); break;
+    case CLS_RSA3K: hipLaunchKernelGGL((k_rsa_modexp<28, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a); break;
+    case CLS_RSA4K: hipLaunchKernelGGL((k_rsa_modexp<37, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a); break;
+    default: return;
+  }
+  hipLaunchKernelGGL(k_rsa_pad, g, b, 0, s, a);
+}
+
+void launch_rsa_keyprep(jgk::DevKey* keys, uint32_t* blob, int nkeys, hipStream_t s) {
+  hipLaunchKernelGGL(k_rsa_keyprep, dim3((nkeys + 63) / 64), dim3(64), 0, s, keys, blob, nkeys);
+}

@@ -1,0 +1,127 @@
+/*
+ * jg.h -- C ABI of the MI355X batched JWS signature verifier (libcapjwt.so).
+ *
+ * This is the drop-in boundary for cap's signature-verification hot path.  A Go
+ * maintainer binds it with cgo underneath a GPU-backed
+ * implementation of cap's KeySet interface:
+ *
+ *   type KeySet interface {                                 jwt/keyset.go:27-32
+ *     VerifySignature(ctx, token string) (map[string]interface{}, error)
+ *   }
+ *
+ * Each entry point replaces one piece of the reference's per-token call stack
+ *  with a batched, device-side equivalent:
+ *
+ *   jg_keys_load     <- key ingestion: NewStaticKeySet (jwt/keyset.go:142-150),
+ *                       JWKS decode in go-oidc RemoteKeySet (jwt/keyset.go:101,120)
+ *   jg_verify_batch  <- the signature arithmetic of parsedJWT.Claims(key, ...)
+ *                       (jwt/keyset.go:163) / remoteJWKS.VerifySignature
+ *                       (jwt/keyset.go:127): go-jose verifyPayload -> crypto/rsa
+ *                       VerifyPKCS1v15 | VerifyPSS, crypto/ecdsa.Verify,
+ *                       crypto/ed25519.Verify, for MANY (token, key) pairs at once
+ *
+ * Plain C types only: pointers + sizes, no Go or torch types.  All byte strings
+ * are big-endian as in JWK / Go's big.Int.Bytes(), except the Ed25519 public key
+ * (32 raw bytes, RFC 8032 encoding).
+ */
+#ifndef CAPJWT_JG_H
+#define CAPJWT_JG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* JWS algorithms -- jwt/algs.go:12-21 */
+enum jg_alg {
+  JG_ALG_NONE = 0, /* anything not in jwt/algs.go:24-35 (HS256, none, ...) -> reject */
+  JG_RS256 = 1, JG_RS384 = 2, JG_RS512 = 3,
+  JG_PS256 = 4, JG_PS384 = 5, JG_PS512 = 6,
+  JG_ES256 = 7, JG_ES384 = 8, JG_ES512 = 9,
+  JG_EDDSA = 10
+};
+
+enum jg_key_kind { JG_KEY_RSA = 1, JG_KEY_EC = 2, JG_KEY_ED25519 = 3 };
+enum jg_curve { JG_P256 = 1, JG_P384 = 2, JG_P521 = 3 };
+
+/* One public key: *rsa.PublicKey | *ecdsa.PublicKey | ed25519.PublicKey. */
+typedef struct jg_key {
+  int32_t kind;            /* jg_key_kind */
+  int32_t curve;           /* jg_curve, EC only */
+  const uint8_t* n;        /* RSA modulus, big-endian (leading zeros allowed) */
+  int32_t n_len;
+  uint64_t e;              /* RSA public exponent as decoded (Go rejects e<2, e>2^31-1) */
+  const uint8_t* x;        /* EC X / Ed25519 public key (32 bytes) */
+  const uint8_t* y;        /* EC Y */
+  int32_t coord_len;       /* EC coordinate length in bytes (32/48/66) */
+} jg_key;
+
+/* One verification job.  `off`/`sig_in_len` locate the JWS signing input
+ * (go-jose computeAuthData: BASE64URL(protected) '.' BASE64URL(payload), or the
+ * raw payload when b64=false) inside the arena; the signature is the base64url
+ * string at arena[off + sig_rel_off, +sig_b64_len) with any trailing '='
+ * already trimmed by the caller (go-jose base64URLDecode).
+ * The verdict is the crypto outcome for (alg, key) on those bytes. */
+typedef struct jg_tok {
+  uint64_t off;
+  uint32_t sig_in_len;
+  uint32_t sig_rel_off;
+  uint32_t sig_b64_len;
+  uint16_t key_idx;        /* index into the last jg_keys_load table */
+  uint8_t alg;             /* jg_alg */
+  uint8_t flags;           /* reserved, 0 */
+} jg_tok;
+
+/* verdict_out[i] values */
+enum { JG_REJECT = 0, JG_ACCEPT = 1 };
+
+typedef struct jg_ctx jg_ctx;
+typedef struct jg_batch jg_batch;
+
+/* Create a context on the given HIP devices (NULL/0 = device 0). */
+jg_ctx* jg_create(const int* devices, int ndev);
+void jg_destroy(jg_ctx* ctx);
+
+/* Replace the key table (copied; may be reloaded on JWKS refresh).  Invalid
+ * keys (off-curve EC point, Ed25519 point that does not decode, even or
+ * unusable RSA modulus, e out of range) load fine and verify nothing -- the
+ * same outcome Go produces per token.  Returns 0 or a negative error. */
+int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys);
+
+/* Verify ntok jobs, blocking.  Host buffers; copied to the device(s).  Returns
+ * 0 on success, <0 on an infrastructure error (see jg_last_error); per-token
+ * outcomes are only in verdict_out[i] (JG_ACCEPT / JG_REJECT). */
+int jg_verify_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
+                    const jg_tok* toks, size_t ntok, uint8_t* verdict_out);
+
+const char* jg_last_error(jg_ctx* ctx);
+
+/* Pinned host memory for arenas / job arrays (hipHostMalloc). */
+void* jg_host_alloc(size_t bytes);
+void jg_host_free(void* p);
+
+/* ---- device-resident batches (throughput measurement, pipelining) ----
+ * jg_batch_stage copies a batch to the device of `device_slot` and precomputes
+ * its dispatch plan (bucketing by algorithm family and key); jg_batch_run runs
+ * the verify kernels on the resident inputs (no H2D) and, if verdict_out is
+ * non-NULL, copies verdicts back.  jg_batch_run is asynchronous when
+ * verdict_out is NULL; jg_batch_sync waits. */
+int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t arena_len,
+                   const jg_tok* toks, size_t ntok, jg_batch** out);
+int jg_batch_run(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out);
+int jg_batch_sync(jg_ctx* ctx, jg_batch* b);
+void jg_batch_free(jg_ctx* ctx, jg_batch* b);
+
+/* Per-kernel device time (ms) of the last jg_batch_run, measured with HIP
+ * events on the batch's stream.  names/ms arrays of length cap; returns count. */
+int jg_batch_kernel_times(jg_batch* b, const char** names, float* ms, int cap);
+
+/* Library build information (gfx target, version). */
+const char* jg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAPJWT_JG_H */
