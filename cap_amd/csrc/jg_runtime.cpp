@@ -207,6 +207,25 @@ const char* cls_name(int c) {
   return n[c];
 }
 
+struct MarkCtx {
+  jg_batch* b;
+  int cls;
+};
+thread_local MarkCtx g_mark_ctx;
+
+void mark_cb(void* p, const char* kname) {
+  MarkCtx* m = (MarkCtx*)p;
+  mark(m->b, (std::string(cls_name(m->cls)) + "_" + kname).c_str());
+}
+
+Marker marker(jg_batch* b, int cls) {
+  g_mark_ctx = MarkCtx{b, cls};
+  Marker mk;
+  mk.ctx = &g_mark_ctx;
+  mk.fn = mark_cb;
+  return mk;
+}
+
 // Build the plan and upload everything for toks[0..ntok) (indices are the caller's).
 void stage(jg_ctx* ctx, jg_batch* b, const uint8_t* arena, size_t arena_len, const jg_tok* toks, size_t ntok) {
   Device* d = b->dev;
@@ -316,7 +335,7 @@ void run(jg_ctx* ctx, jg_batch* b) {
     pa.end = r.end;
     pa.zrows = cls_rows_sig(c);
     launch_prep(c, pa, s);
-    mark(b, (std::string("prep_") + cls_name(c)).c_str());
+    mark(b, (std::string(cls_name(c)) + "_prep").c_str());
     if (c <= CLS_RSA4K) {
       RsaArgs ra{};
       ra.toks = pa.toks; ra.perm = pa.perm; ra.wave_key = pa.wave_key; ra.keys = pa.keys; ra.keyblob = pa.keyblob;
@@ -328,8 +347,7 @@ void run(jg_ctx* ctx, jg_batch* b) {
       ra.status = pa.status; ra.siglen = pa.siglen; ra.verdict_pad = (uint8_t*)B->vpad.p;
       ra.pss_scratch = (uint8_t*)B->pss.p;
       ra.npad = np; ra.begin = r.begin; ra.end = r.end;
-      launch_rsa(c, ra, s);
-      mark(b, cls_name(c));
+      launch_rsa(c, ra, s, marker(b, c));
     } else if (c <= CLS_P521) {
       if (!d->gtab[c]) throw std::runtime_error("curve table missing");
       EcArgs ea{};
@@ -342,8 +360,7 @@ void run(jg_ctx* ctx, jg_batch* b) {
       ea.exc_list = (int32_t*)B->exc.p;
       ea.exc_count = (uint32_t*)B->exc_cnt.p;
       ea.npad = np; ea.begin = r.begin; ea.end = r.end;
-      launch_ec(c, ea, s);
-      mark(b, cls_name(c));
+      launch_ec(c, ea, s, marker(b, c));
     } else {
       EdArgs ea{};
       ea.perm = pa.perm; ea.wave_key = pa.wave_key; ea.keys = pa.keys; ea.keyblob = pa.keyblob;
@@ -352,8 +369,7 @@ void run(jg_ctx* ctx, jg_batch* b) {
       ea.xyz = rows;
       ea.btab = d->btab;
       ea.npad = np; ea.begin = r.begin; ea.end = r.end;
-      launch_ed(ea, s);
-      mark(b, cls_name(c));
+      launch_ed(ea, s, marker(b, c));
     }
   }
   launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s);

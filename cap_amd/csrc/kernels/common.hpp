@@ -50,6 +50,16 @@ struct DevKey {
 constexpr int COMB_W = 8;
 constexpr int COMB_ENTRIES = 128;
 
+// Timing hook: the runtime records a HIP event on the batch's stream after
+// each kernel a launcher enqueues (names: "<class>_<kernel>").
+struct Marker {
+  void* ctx = nullptr;
+  void (*fn)(void*, const char*) = nullptr;
+  void operator()(const char* name) const {
+    if (fn) fn(ctx, name);
+  }
+};
+
 // Per-class launch range inside a staged batch (padded token index space).
 struct ClassRange {
   int64_t begin, end;   // multiples of WAVE

@@ -110,7 +110,8 @@ __global__ void __launch_bounds__(64) k_ec_scalar(EcArgs a) {
     a.u1w[(int64_t)j * np + p] = u1[j];
     a.u2w[(int64_t)j * np + p] = u2[j];
   }
-  // signed 8-bit windows: u = sum d_w 2^(8w), d_w in [-127, 128]
+  // signed 8-bit windows: u = sum d_w 2^(8w), d_w in [-128, 127] (fits the
+  // packed int8; |d| <= 128 indexes the 128-entry tables)
   int c1 = 0, c2 = 0;
 #pragma unroll
   for (int w = 0; w < NWIN; ++w) {
@@ -118,7 +119,7 @@ __global__ void __launch_bounds__(64) k_ec_scalar(EcArgs a) {
     uint32_t b1 = q < L ? (u1[q] >> sh) : 0u, b2 = q < L ? (u2[q] >> sh) : 0u;
     if (sh > MP_W - 8 && q + 1 < L) { b1 |= u1[q + 1] << (MP_W - sh); b2 |= u2[q + 1] << (MP_W - sh); }
     int v1 = (int)(b1 & 0xffu) + c1, v2 = (int)(b2 & 0xffu) + c2;
-    c1 = v1 > 128; c2 = v2 > 128;
+    c1 = v1 >= 128; c2 = v2 >= 128;
     v1 -= c1 << 8; v2 -= c2 << 8;
     a.digs[(int64_t)w * np + p] = ((uint32_t)v1 & 0xffu) | (((uint32_t)v2 & 0xffu) << 8);
   }
@@ -467,23 +468,26 @@ __global__ void k_ec_table_g(uint32_t* tab) {
 }
 
 template <class CV>
-void launch_chain(const EcArgs& a, hipStream_t s) {
+void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   dim3 g((unsigned)waves), b(WAVE);
   (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_ec_scalar<CV>, g, b, 0, s, a);
+  mk("scalar");
   hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
+  mk("point");
   hipLaunchKernelGGL(k_ec_exact<CV>, dim3(64), b, 0, s, a);
+  mk("exact");
 }
 
 }  // namespace
 
-void launch_ec(int cls, const EcArgs& a, hipStream_t s) {
+void launch_ec(int cls, const EcArgs& a, hipStream_t s, const Marker& mk) {
   if (a.end <= a.begin) return;
   switch (cls) {
-    case CLS_P256: launch_chain<CurveP256>(a, s); break;
-    case CLS_P384: launch_chain<CurveP384>(a, s); break;
-    case CLS_P521: launch_chain<CurveP521>(a, s); break;
+    case CLS_P256: launch_chain<CurveP256>(a, s, mk); break;
+    case CLS_P384: launch_chain<CurveP384>(a, s, mk); break;
+    case CLS_P521: launch_chain<CurveP521>(a, s, mk); break;
     default: break;
   }
 }

@@ -33,7 +33,7 @@ constexpr int64_t ec_table_words(int cls) {
   return (int64_t)ec_windows(cls) * jgk::COMB_ENTRIES * ec_stride(cls);
 }
 
-void launch_ec(int cls, const EcArgs& a, hipStream_t s);
+void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);
 // key staging: validate each listed key (plain 28-bit limbs x,y at aux_off), write
 // Montgomery affine coordinates back to aux_off and build its comb table.
 void launch_ec_keyprep(int cls, jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);

@@ -275,12 +275,14 @@ __global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_
 
 }  // namespace
 
-void launch_ed(const EdArgs& a, hipStream_t s) {
+void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   if (waves <= 0) return;
   dim3 g((unsigned)waves), b(WAVE);
   hipLaunchKernelGGL(k_ed_point, g, b, 0, s, a);
+  mk("point");
   hipLaunchKernelGGL(k_ed_finish, g, b, 0, s, a);
+  mk("finish");
 }
 
 void launch_ed_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {

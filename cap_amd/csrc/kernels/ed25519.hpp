@@ -26,7 +26,7 @@ constexpr int ED_STRIDE = 32;                   // 3 x 10 limbs, padded to 16 B
 constexpr int ED_WINDOWS = 33;
 constexpr int64_t ED_TABLE_WORDS = (int64_t)ED_WINDOWS * jgk::COMB_ENTRIES * ED_STRIDE;
 
-void launch_ed(const EdArgs& a, hipStream_t s);
+void launch_ed(const EdArgs& a, hipStream_t s, const jgk::Marker& mk);
 // key staging: decode each listed key's 32 public-key bytes (words at aux_off),
 // mark validity and build the comb table of -A at tab_off
 void launch_ed_keyprep(jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);

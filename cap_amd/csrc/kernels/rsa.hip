@@ -452,7 +452,7 @@ __global__ void k_rsa_keyprep(DevKey* keys, uint32_t* blob, int nkeys) {
 
 }  // namespace
 
-void launch_rsa(int cls, const RsaArgs& a, hipStream_t s) {
+void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   if (waves <= 0) return;
   dim3 g((unsigned)waves), b(WAVE);
@@ -462,7 +462,9 @@ void launch_rsa(int cls, const RsaArgs& a, hipStream_t s) {
     case CLS_RSA4K: hipLaunchKernelGGL((k_rsa_modexp<37, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a); break;
     default: return;
   }
+  mk("modexp");
   hipLaunchKernelGGL(k_rsa_pad, g, b, 0, s, a);
+  mk("pad");
 }
 
 void launch_rsa_keyprep(jgk::DevKey* keys, uint32_t* blob, int nkeys, hipStream_t s) {

@@ -32,5 +32,5 @@ constexpr int rsa_limbs(int cls) {
   return cls == jgk::CLS_RSA2K ? 74 : cls == jgk::CLS_RSA3K ? 112 : 148;
 }
 
-void launch_rsa(int cls, const RsaArgs& a, hipStream_t s);
+void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const jgk::Marker& mk);
 void launch_rsa_keyprep(jgk::DevKey* keys, uint32_t* blob, int nkeys, hipStream_t s);

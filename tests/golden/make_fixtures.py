@@ -327,6 +327,7 @@ def main():
     K.rsa("rsa2047-a", 2047)       # odd size: top two EM bits must be clear (R16)
     K.rsa("rsa2049-a", 2049)       # emLen < k: PSS strips a leading zero byte (R16)
     K.ec("p256-a", "P-256"); K.ec("p256-b", "P-256")
+    K.ec("p256-c", "P-256"); K.ec("p256-d", "P-256")     # 4-kid JWKS workload (bench)
     K.ec("p384-a", "P-384"); K.ec("p521-a", "P-521")
     K.ed("ed-a"); K.ed("ed-b")
 
