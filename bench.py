@@ -118,20 +118,31 @@ def measure(ctx, arena, toks, steps, warmup, dist):
     b = _lib.Batch(ctx, h, len(toks))
     v = np.frombuffer(b.run(want_verdicts=True), dtype=np.uint8)
     accepted = int(v.sum())
-    for _ in range(warmup):
+    pinned = _lib.PinnedBuffer(len(toks))
+    # per-kernel device times: average over synchronous runs (the warmup)
+    times = {}
+    for _ in range(max(1, warmup)):
         b.run(want_verdicts=True)
+        for name, ms in b.kernel_times():
+            times.setdefault(name, []).append(ms)
     if dist:
         import torch
         import torch.distributed as td
         torch.cuda.synchronize()
         td.barrier()
-    times = {}
+    # timed region: K steps streamed back to back (kernels + verdict D2H into
+    # pinned memory each step), one synchronisation at the end
     t0 = time.perf_counter()
     for _ in range(steps):
-        b.run(want_verdicts=True)          # synchronous: kernels + verdict D2H
-        for name, ms in b.kernel_times():
-            times.setdefault(name, []).append(ms)
+        b.enqueue(pinned)
+    b.sync()
     elapsed = time.perf_counter() - t0
+    for name, ms in b.kernel_times():          # last timed step
+        times.setdefault(name, []).append(ms)
+    last = np.frombuffer(pinned.bytes(), dtype=np.uint8)
+    if int(last.sum()) != accepted:
+        raise RuntimeError("verdicts changed between runs")
+    pinned.free()
     if dist:
         import torch
         import torch.distributed as td

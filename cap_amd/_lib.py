@@ -19,7 +19,7 @@ CURVE_IDS = {"P-256": 1, "P-384": 2, "P-521": 3}
 
 # every symbol include/jg.h declares
 EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_last_error",
-           "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_sync",
+           "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_enqueue", "jg_batch_sync",
            "jg_batch_free", "jg_batch_kernel_times", "jg_version"]
 
 
@@ -64,6 +64,7 @@ def lib():
         L.jg_host_free.argtypes = [vp]
         L.jg_batch_stage.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.POINTER(JgTok), sz, ctypes.POINTER(vp)]
         L.jg_batch_run.argtypes = [vp, vp, vp]
+        L.jg_batch_enqueue.argtypes = [vp, vp, vp]
         L.jg_batch_sync.argtypes = [vp, vp]
         L.jg_batch_free.argtypes = [vp, vp]
         L.jg_batch_kernel_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
@@ -181,6 +182,30 @@ class Context:
         return Batch(self, h, len(arena.toks))
 
 
+class PinnedBuffer:
+    """Page-locked host memory from jg_host_alloc (hipHostMalloc)."""
+
+    def __init__(self, nbytes):
+        self.n = nbytes
+        self.ptr = lib().jg_host_alloc(max(1, nbytes))
+        if not self.ptr:
+            raise JgError("jg_host_alloc failed")
+
+    def bytes(self):
+        return ctypes.string_at(self.ptr, self.n)
+
+    def free(self):
+        if self.ptr:
+            lib().jg_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Batch:
     def __init__(self, ctx, h, n):
         self.ctx, self.h, self.n = ctx, h, n
@@ -191,6 +216,14 @@ class Batch:
         if rc != 0:
             raise JgError(f"jg_batch_run rc={rc}: {self.ctx.error()}")
         return bytes(out[:self.n]) if want_verdicts else None
+
+    def enqueue(self, pinned_verdicts=None):
+        """Enqueue one run without waiting; verdicts land in `pinned_verdicts`
+        (a PinnedBuffer) once sync() returns."""
+        ptr = pinned_verdicts.ptr if pinned_verdicts is not None else None
+        rc = lib().jg_batch_enqueue(self.ctx.h, self.h, ptr)
+        if rc != 0:
+            raise JgError(f"jg_batch_enqueue rc={rc}: {self.ctx.error()}")
 
     def sync(self):
         rc = lib().jg_batch_sync(self.ctx.h, self.h)

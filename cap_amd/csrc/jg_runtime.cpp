@@ -129,8 +129,11 @@ struct jg_batch {
   ClassRange ranges[NCLS] = {};
   uint64_t epoch = 0;
   bool timing = true;
+  // timing marks of the most recent run: events are created once and
+  // re-recorded every run (no per-run event churn)
   std::vector<std::string> mark_names;
   std::vector<hipEvent_t> mark_events;
+  size_t marks_used = 0;
   std::vector<std::string> tnames;
   std::vector<float> tms;
   ~jg_batch() {
@@ -195,11 +198,15 @@ int classify(const jg_ctx* ctx, const jg_tok& t) {
 
 void mark(jg_batch* b, const char* name) {
   if (!b->timing) return;
-  hipEvent_t e;
-  HIPCHK(hipEventCreate(&e));
-  HIPCHK(hipEventRecord(e, b->dev->stream));
-  b->mark_names.emplace_back(name);
-  b->mark_events.push_back(e);
+  if (b->marks_used == b->mark_events.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    b->mark_events.push_back(e);
+    b->mark_names.emplace_back();
+  }
+  HIPCHK(hipEventRecord(b->mark_events[b->marks_used], b->dev->stream));
+  b->mark_names[b->marks_used] = name;
+  ++b->marks_used;
 }
 
 const char* cls_name(int c) {
@@ -309,9 +316,7 @@ void run(jg_ctx* ctx, jg_batch* b) {
   if (b->epoch != ctx->epoch) throw std::runtime_error("key table reloaded since this batch was staged");
   Bufs* B = b->b;
   hipStream_t s = d->stream;
-  for (auto e : b->mark_events) (void)hipEventDestroy(e);
-  b->mark_events.clear();
-  b->mark_names.clear();
+  b->marks_used = 0;
   const int64_t np = b->npad;
   mark(b, "begin");
   HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, s));
@@ -380,7 +385,7 @@ void run(jg_ctx* ctx, jg_batch* b) {
 void collect_times(jg_batch* b) {
   b->tnames.clear();
   b->tms.clear();
-  for (size_t i = 1; i < b->mark_events.size(); ++i) {
+  for (size_t i = 1; i < b->marks_used; ++i) {
     float ms = 0;
     if (hipEventElapsedTime(&ms, b->mark_events[i - 1], b->mark_events[i]) == hipSuccess) {
       b->tnames.push_back(b->mark_names[i]);
@@ -638,6 +643,20 @@ int jg_batch_run(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out) {
       HIPCHK(hipStreamSynchronize(b->dev->stream));
       collect_times(b);
     }
+    return 0;
+  } catch (const std::exception& e) {
+    ctx->set_err(e.what());
+    return -2;
+  }
+}
+
+int jg_batch_enqueue(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out) {
+  if (!ctx || !b) return -1;
+  try {
+    std::lock_guard<std::mutex> g(b->dev->mu);
+    run(ctx, b);
+    if (verdict_out && b->ntok > 0)
+      HIPCHK(hipMemcpyAsync(verdict_out, b->b->verdict.p, (size_t)b->ntok, hipMemcpyDeviceToHost, b->dev->stream));
     return 0;
   } catch (const std::exception& e) {
     ctx->set_err(e.what());

@@ -14,6 +14,8 @@
 //                 recomputed with complete case handling; rare
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "common.hpp"
 #include "ecdsa.hpp"
 #include "mp.hpp"
@@ -50,6 +52,136 @@ __device__ __forceinline__ bool zero_limbs(const uint32_t* a) {
 }
 
 // ------------------------------------------------------------------ scalar
+// Per-token checks and inputs of the scalar stage.  Returns ok; r, s, e as
+// plain 28-bit limbs (s replaced by 1 when the token is rejected, so the batch
+// product stays invertible).
+template <class CV>
+__device__ __forceinline__ bool ec_scalar_inputs(const EcArgs& a, int64_t p, uint32_t* r, uint32_t* s, uint32_t* e) {
+  using Fn = typename CV::Fn;
+  constexpr int L = Fn::L;
+  constexpr int CB = CV::C::BYTES;
+  const int64_t np = a.npad;
+  const int32_t t = a.perm[p];
+  if (t < 0) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) { r[j] = 0; e[j] = 0; s[j] = j == 0 ? 1u : 0u; }
+    return false;
+  }
+  const int kidx = a.wave_key[p / WAVE];
+  bool ok = a.status[p] == ST_OK && a.keys[kidx].valid;
+  const int alg = a.toks[t].alg;
+  uint32_t rw[17], sw[17];
+#pragma unroll
+  for (int q = 0; q < 17; ++q) {
+    rw[q] = a.sigw[(int64_t)q * np + p];
+    sw[q] = a.sigw[(int64_t)(EC_S_ROW + q) * np + p];
+  }
+#pragma unroll
+  for (int q = 0; q < 17; ++q) {
+    if (4 * q >= CB) ok = ok && rw[q] == 0 && sw[q] == 0;
+    else if (4 * q + 4 > CB) {
+      const uint32_t hi = ~0u << (8 * (CB - 4 * q));
+      ok = ok && (rw[q] & hi) == 0 && (sw[q] & hi) == 0;
+    }
+  }
+  mp::words_to_limbs<L, 17>(r, rw);
+  mp::words_to_limbs<L, 17>(s, sw);
+  uint32_t nl[L];
+  mp::set_const<Fn>(nl, Fn::M);
+  ok = ok && !zero_limbs<L>(r) && !zero_limbs<L>(s) && lt_limbs<L>(r, nl) && lt_limbs<L>(s, nl);
+  {
+    const int hl = es_hash_bytes(alg) < CB ? es_hash_bytes(alg) : CB;   // multiple of 4
+    uint32_t ew[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int src = hl / 4 - 1 - q;
+      ew[q] = src >= 0 ? a.dig[(int64_t)(src < 0 ? 0 : src) * np + p] : 0u;
+    }
+    mp::words_to_limbs<L, 16>(e, ew);
+    mp::csub<Fn>(e);
+  }
+  if (!ok) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) s[j] = j == 0 ? 1u : 0u;
+  }
+  return ok;
+}
+
+// Batched scalar stage (Montgomery's trick): thread i owns the B tokens
+// p_j = begin + i + j*S and pays ONE Fermat inversion for all of them:
+//   pass 1: c_j = s_0 ... s_j (Montgomery), c_j and s_j parked in the u1/u2 rows
+//   inv = c_{B-1}^-1
+//   pass 2 (j descending): w_j = inv * c_{j-1}, inv *= s_j;
+//           u1 = e w_j, u2 = r w_j (mod n), signed 8-bit digits
+template <class CV>
+__global__ void __launch_bounds__(64) k_ec_scalar_batch(EcArgs a, int B) {
+  using Fn = typename CV::Fn;
+  constexpr int L = Fn::L;
+  constexpr int NWIN = ec_windows(CV::CLS);
+  const int64_t np = a.npad;
+  const int64_t n = a.end - a.begin;
+  const int64_t S = (n + B - 1) / B;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S) return;
+  uint32_t acc[L];
+  mp::set_const<Fn>(acc, Fn::ONE);
+  int nb = 0;
+  for (int j = 0; j < B; ++j) {
+    const int64_t p = a.begin + i + (int64_t)j * S;
+    if (p >= a.end) break;
+    uint32_t r[L], s[L], e[L], sm[L];
+    const bool ok = ec_scalar_inputs<CV>(a, p, r, s, e);
+    if (!ok && a.perm[p] >= 0) a.status[p] = ST_REJECT;
+    mp::to_mont<Fn>(sm, s);
+    mp::mul<Fn>(acc, acc, sm);
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      a.u1w[(int64_t)k * np + p] = acc[k];
+      a.u2w[(int64_t)k * np + p] = sm[k];
+    }
+    ++nb;
+  }
+  uint32_t inv[L];
+  mp::inv<Fn>(inv, acc);
+  for (int j = nb - 1; j >= 0; --j) {
+    const int64_t p = a.begin + i + (int64_t)j * S;
+    uint32_t cprev[L], sm[L], w[L];
+    if (j > 0) {
+      const int64_t pp = p - S;
+#pragma unroll
+      for (int k = 0; k < L; ++k) cprev[k] = a.u1w[(int64_t)k * np + pp];
+    } else {
+      mp::set_const<Fn>(cprev, Fn::ONE);
+    }
+#pragma unroll
+    for (int k = 0; k < L; ++k) sm[k] = a.u2w[(int64_t)k * np + p];
+    mp::mul<Fn>(w, inv, cprev);                  // s_j^-1 R
+    mp::mul<Fn>(inv, inv, sm);
+    uint32_t r[L], s[L], e[L], u1[L], u2[L];
+    (void)ec_scalar_inputs<CV>(a, p, r, s, e);
+    mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
+    mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      a.u1w[(int64_t)k * np + p] = u1[k];
+      a.u2w[(int64_t)k * np + p] = u2[k];
+    }
+    // signed 8-bit windows: u = sum d_w 2^(8w), d_w in [-128, 127] (fits the
+    // packed int8; |d| <= 128 indexes the 128-entry tables)
+    int c1 = 0, c2 = 0;
+#pragma unroll
+    for (int w8 = 0; w8 < NWIN; ++w8) {
+      const int bit = 8 * w8, q = bit / MP_W, sh = bit % MP_W;
+      uint32_t b1 = q < L ? (u1[q] >> sh) : 0u, b2 = q < L ? (u2[q] >> sh) : 0u;
+      if (sh > MP_W - 8 && q + 1 < L) { b1 |= u1[q + 1] << (MP_W - sh); b2 |= u2[q + 1] << (MP_W - sh); }
+      int v1 = (int)(b1 & 0xffu) + c1, v2 = (int)(b2 & 0xffu) + c2;
+      c1 = v1 >= 128; c2 = v2 >= 128;
+      v1 -= c1 << 8; v2 -= c2 << 8;
+      a.digs[(int64_t)w8 * np + p] = ((uint32_t)v1 & 0xffu) | (((uint32_t)v2 & 0xffu) << 8);
+    }
+  }
+}
+
 template <class CV>
 __global__ void __launch_bounds__(64) k_ec_scalar(EcArgs a) {
   using Fn = typename CV::Fn;
@@ -472,7 +604,11 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   dim3 g((unsigned)waves), b(WAVE);
   (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
-  hipLaunchKernelGGL(k_ec_scalar<CV>, g, b, 0, s, a);
+  // tokens per thread for the batched inversion: keep >= ~8 waves per CU
+  const int64_t n = a.end - a.begin;
+  int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * 8 * WAVE)));
+  const int64_t S = (n + B - 1) / B;
+  hipLaunchKernelGGL(k_ec_scalar_batch<CV>, dim3((unsigned)((S + WAVE - 1) / WAVE)), b, 0, s, a, B);
   mk("scalar");
   hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
   mk("point");

@@ -196,31 +196,34 @@ MPD void from_mont(uint32_t* r, const uint32_t* a) {
 // r = x^E for an exponent held in a constexpr array of 28-bit limbs (read with
 // wave-uniform indices -> scalar loads).  `minus2` subtracts 2 from limb 0
 // (E = m - 2 for Fermat inversion; every modulus here has limb 0 >= 2).
-// Left-to-right 4-bit fixed window; the window value is uniform across the
-// wave, so the table select is a uniform compare chain, not a divergent branch.
+// Left-to-right fixed window of WB bits (4 for 10-limb fields, 2 above, so the
+// 2^WB-entry table fits the register file); the window value is uniform across
+// the wave, so the table select is a uniform compare chain, not a divergent branch.
 template <class F>
 MPD void pow_e(uint32_t* r, const uint32_t* x, const uint32_t* E, int ebits, bool minus2) {
   constexpr int L = F::L;
-  uint32_t tab[16][L];
+  constexpr int WB = L <= 10 ? 4 : 2, NT = 1 << WB;
+  uint32_t tab[NT][L];
   set_const<F>(tab[0], F::ONE);
   copy<F>(tab[1], x);
 #pragma unroll
-  for (int i = 2; i < 16; ++i) mul<F>(tab[i], tab[i - 1], x);
+  for (int i = 2; i < NT; ++i) mul<F>(tab[i], tab[i - 1], x);
   uint32_t acc[L];
   set_const<F>(acc, F::ONE);
-  const int top = (ebits + 3) & ~3;
-  for (int b = top - 4; b >= 0; b -= 4) {
-    sqr<F>(acc, acc); sqr<F>(acc, acc); sqr<F>(acc, acc); sqr<F>(acc, acc);
+  const int top = (ebits + WB - 1) / WB * WB;
+  for (int b = top - WB; b >= 0; b -= WB) {
+#pragma unroll
+    for (int k = 0; k < WB; ++k) sqr<F>(acc, acc);
     const int w = b / MP_W, o = b % MP_W;
     const uint32_t lo = E[w] - ((minus2 && w == 0) ? 2u : 0u);
     uint32_t nib = lo >> o;
-    if (o > MP_W - 4 && w + 1 < L) nib |= E[w + 1] << (MP_W - o);
-    nib &= 15u;
+    if (o > MP_W - WB && w + 1 < L) nib |= E[w + 1] << (MP_W - o);
+    nib &= (uint32_t)(NT - 1);
     uint32_t sel[L];
 #pragma unroll
     for (int j = 0; j < L; ++j) sel[j] = tab[0][j];
 #pragma unroll
-    for (int i = 1; i < 16; ++i)
+    for (int i = 1; i < NT; ++i)
       if (nib == (uint32_t)i) {
 #pragma unroll
         for (int j = 0; j < L; ++j) sel[j] = tab[i][j];

@@ -66,12 +66,19 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   // zero the rows this token may leave partially written
   for (int r = 0; r < a.zrows; ++r) sigw[(int64_t)r * np + p] = 0u;
 
-  const uint8_t* sp = a.arena + tk.off + tk.sig_rel_off;
+  // characters are fetched as aligned dwords (4 per load) from the arena
+  const uint64_t sbyte = tk.off + tk.sig_rel_off;
+  const uint32_t* sw32 = reinterpret_cast<const uint32_t*>(a.arena + (sbyte & ~3ull));
+  const uint32_t first = (uint32_t)(sbyte & 3ull);
   uint32_t acc = 0, bitsn = 0, outi = 0;
   uint32_t cur_row = 0xffffffffu, cur_word = 0;
   uint32_t R_le[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // Ed25519: first 32 bytes (R)
-  for (uint32_t i = 0; i < (D ? n : 0u); ++i) {
-    const int v = b64val(sp[i]);
+  const uint32_t nchars = D ? n : 0u;
+  uint32_t word = 0;
+  for (uint32_t i = 0; i < nchars; ++i) {
+    const uint32_t pos = first + i;
+    if (i == 0 || (pos & 3u) == 0) word = sw32[pos >> 2];
+    const int v = b64val((word >> ((pos & 3u) * 8)) & 0xffu);
     if (v < 0) { st = ST_REJECT; break; }
     acc = (acc << 6) | (uint32_t)v;
     bitsn += 6;

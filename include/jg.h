@@ -111,6 +111,10 @@ void jg_host_free(void* p);
 int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t arena_len,
                    const jg_tok* toks, size_t ntok, jg_batch** out);
 int jg_batch_run(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out);
+/* Enqueue one run (kernels + verdict copy into verdict_out, which must be
+ * pinned -- jg_host_alloc -- and stay valid until jg_batch_sync) and return
+ * without waiting: consecutive runs stream back to back on the device. */
+int jg_batch_enqueue(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out);
 int jg_batch_sync(jg_ctx* ctx, jg_batch* b);
 void jg_batch_free(jg_ctx* ctx, jg_batch* b);
 
