@@ -302,7 +302,7 @@ void stage(jg_ctx* ctx, jg_batch* b, const uint8_t* arena, size_t arena_len, con
   B->vpad.get(npad);
   B->verdict.get(std::max<size_t>(ntok, 1));
   B->rows.get(sizeof(uint32_t) * (size_t)b->scratch_rows * npad);
-  B->pss.get((size_t)std::max<int64_t>(b->pss_tokens, 1) * 1024);
+  B->pss.get((size_t)std::max<int64_t>(b->pss_tokens, 1) * 2048);
   B->exc.get(sizeof(int32_t) * npad);
   B->exc_cnt.get(sizeof(uint32_t) * 4);
   // the host vectors die here: the copies above must complete first

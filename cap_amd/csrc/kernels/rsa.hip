@@ -338,20 +338,33 @@ __global__ void __launch_bounds__(64) k_rsa_pad(RsaArgs a) {
     const int hlen = hb / 8;
     if (alg <= 3) {
       // PKCS#1 v1.5: EM == 00 01 FF..FF 00 || DigestInfo || H   (R15)
+      // Compared word by word on the little-endian integer y: LE byte j holds
+      // EM[k-1-j]; H occupies j < hlen (whole words: y word q == digest word
+      // hlen/4-1-q), DigestInfo hlen <= j < tlen, then 00, FF.., 01, 00.
       const int tlen = 19 + hlen;
       const uint8_t* DI = hb == 256 ? DI256 : hb == 384 ? DI384 : DI512;
       bool ok = k >= tlen + 11;
-      for (int pos = 0; pos < k && ok; ++pos) {
-        uint32_t ex;
-        if (pos == 0) ex = 0;
-        else if (pos == 1) ex = 1;
-        else if (pos < k - tlen - 1) ex = 0xff;
-        else if (pos == k - tlen - 1) ex = 0;
-        else if (pos < k - hlen) ex = DI[pos - (k - tlen)];
-        else ex = dbyte(a.dig, np, p, pos - (k - hlen));
-        ok = ybyte(a.yw, np, p, k, pos) == ex;
+      uint32_t diff = 0;
+      for (int q = 0; q < hlen / 4; ++q)
+        diff |= a.yw[(int64_t)q * np + p] ^ a.dig[(int64_t)(hlen / 4 - 1 - q) * np + p];
+      const int nw = (k + 3) / 4;
+      for (int q = hlen / 4; q < nw; ++q) {
+        const uint32_t yv = a.yw[(int64_t)q * np + p];
+        uint32_t ev = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const int j = 4 * q + bb;
+          uint32_t ex;
+          if (j < tlen) ex = DI[tlen - 1 - j];
+          else if (j == tlen) ex = 0;
+          else if (j < k - 2) ex = 0xff;
+          else if (j == k - 2) ex = 1;
+          else ex = 0;                      // j == k-1, and j >= k (y < n < 2^(8k))
+          ev |= ex << (8 * bb);
+        }
+        diff |= yv ^ ev;
       }
-      verdict = ok;
+      verdict = ok && diff == 0;
     } else {
       // EMSA-PSS-VERIFY with auto salt length (R16)
       const int embits = K.embits;
@@ -364,7 +377,9 @@ __global__ void __launch_bounds__(64) k_rsa_pad(RsaArgs a) {
       const uint32_t bitmask = 0xffu >> (8 * emlen - embits);
       ok = ok && (ybyte(a.yw, np, p, k, lead) & ~bitmask) == 0;
       if (ok) {
-        uint8_t* buf = a.pss_scratch + (p - a.begin) * 1024;   // [0,512): DB ; [512,1024): work
+        // [0,512): DB ; [512,2048): work (H||ctr, then M' = 0^8||mHash||salt <= 584 B,
+        // plus the SHA reader's over-read of one block)
+        uint8_t* buf = a.pss_scratch + (p - a.begin) * 2048;
         uint8_t* wk = buf + 512;
         const int dblen = emlen - hlen - 1;
         // H = EM[dblen .. dblen+hlen)

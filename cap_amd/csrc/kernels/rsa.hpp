@@ -20,7 +20,7 @@ struct RsaArgs {
   uint8_t* status;
   const uint16_t* siglen;
   uint8_t* verdict_pad;
-  uint8_t* pss_scratch;       // 1 KiB per token of the class range
+  uint8_t* pss_scratch;       // 2 KiB per token of the class range
   int64_t npad, begin, end;
 };
 

@@ -56,9 +56,28 @@ struct MemString {
   uint32_t len;
 
   SHD uint32_t raw_be(uint32_t i) const {        // bytes [4i, 4i+4) of m, big-endian
-    const uint32_t lo = __builtin_nontemporal_load(aligned + i);
-    const uint32_t hi = __builtin_nontemporal_load(aligned + i + 1);
+    const uint32_t lo = aligned[i];
+    const uint32_t hi = aligned[i + 1];
     return bswap32(__builtin_amdgcn_alignbyte(hi, lo, shift));
+  }
+
+  // N consecutive big-endian words starting at word w0, padded (SHA padding
+  // 0x80 / zeros; the length words are the caller's).  All N+1 aligned loads
+  // are issued unconditionally, back to back: reads may run past the string
+  // (the arena carries slack), bytes at or beyond len are masked.
+  template <int N>
+  SHD void padded_words(uint32_t w0, uint32_t* out) const {
+    uint32_t u[N + 1];
+#pragma unroll
+    for (int k = 0; k <= N; ++k) u[k] = aligned[w0 + k];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const uint32_t raw = bswap32(__builtin_amdgcn_alignbyte(u[k + 1], u[k], shift));
+      const int rem = (int)len - (int)(4u * (w0 + k));
+      const uint32_t keep = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : (0xffffffffu << (32 - 8 * rem)));
+      const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80u << (24 - 8 * rem)) : 0u;
+      out[k] = (raw & keep) | pad;
+    }
   }
 };
 
@@ -108,16 +127,14 @@ SHD void sha256_mem(uint32_t h[8], const MemString& m) {
   const uint32_t nwords = nblk * 16;
   for (uint32_t blk = 0; blk < nblk; ++blk) {
     uint32_t w[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t i = blk * 16 + k;
-      uint32_t v = pad_word(4u * i < m.len ? m.raw_be(i) : 0u, i, m.len);
-      if (i == nwords - 1) v = m.len << 3;
-      if (i == nwords - 2) v = m.len >> 29;
-      w[k] = v;
+    m.padded_words<16>(blk * 16, w);
+    if (blk == nblk - 1) {
+      w[14] = m.len >> 29;
+      w[15] = m.len << 3;
     }
     sha256_compress(h, w);
   }
+  (void)nwords;
 }
 
 // ---------------------------------------------------------------- SHA-512/384
@@ -166,29 +183,24 @@ SHD void sha512_mem(uint64_t h[8], bool is384, const MemString& m, const uint32_
   const uint32_t nw32 = nblk * 32;                   // 32-bit words in the padded stream
   const uint32_t pw = plen / 4;                      // prefix words (0 or 16)
   for (uint32_t blk = 0; blk < nblk; ++blk) {
+    uint32_t v[32];
+    if (pw != 0 && blk == 0) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = prefix[k];
+      m.padded_words<16>(0, v + 16);
+    } else {
+      m.padded_words<32>(blk * 32 - pw, v);
+    }
+    if (blk == nblk - 1) {                           // 128-bit length, high 64 bits zero
+      v[30] = tot >> 29;
+      v[31] = tot << 3;
+    }
     uint64_t w[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      uint32_t v2[2];
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl) {
-        const uint32_t i = blk * 32 + 2 * k + hl;    // 32-bit word index in the stream
-        uint32_t v;
-        if (i < pw) {
-          // prefix words only ever occupy block 0, whose k is compile-time
-          v = prefix[(2 * k + hl) & 15];
-        } else {
-          const uint32_t j = i - pw;                 // word index within m
-          v = pad_word(4u * j < m.len ? m.raw_be(j) : 0u, j, m.len);
-        }
-        if (i == nw32 - 1) v = tot << 3;
-        if (i == nw32 - 2) v = tot >> 29;
-        v2[hl] = v;
-      }
-      w[k] = ((uint64_t)v2[0] << 32) | v2[1];
-    }
+    for (int k = 0; k < 16; ++k) w[k] = ((uint64_t)v[2 * k] << 32) | v[2 * k + 1];
     sha512_compress(h, w);
   }
+  (void)nw32;
 }
 
 }  // namespace sha2
