@@ -42,13 +42,15 @@ assert JG_TOK.itemsize == 24
 def p256_point_mads_per_token():
     """32x32->64 multiply-accumulates the P-256 comb kernel (k_ec_point) issues per
     token: 28-bit limbs, L = 10; Montgomery product = L^2 (mul) or L(L+1)/2 (sqr)
-    + L * (non-zero limbs of p = 6) for the reduction; mixed addition = 8 mul + 3 sqr
-    + 3 value folds (6 non-zero limbs of 2^256 mod p); 2 x 32.4 expected non-zero
-    signed 8-bit digits, the first an assignment; final check 1 sqr + 2 mul."""
-    L, red, fold = 10, 10 * 6, 6
+    + L * 4 for the reduction (p + 1 has 4 non-zero limbs above limb 0, mp.hpp);
+    mixed addition = 8 mul + 3 sqr + 3 value folds (6 non-zero limbs of
+    2^256 mod p); signed 16-bit comb digits (ecdsa.hpp ec_comb_w): 16 windows
+    non-zero w.p. 1 - 2^-16 plus a carry window non-zero w.p. ~1/2, for u1 and
+    u2, the first addition an assignment; final check 1 sqr + 2 mul."""
+    L, red, fold = 10, 10 * 4, 6
     mul, sqr = L * L + red, L * (L + 1) // 2 + red
     madd = 8 * mul + 3 * sqr + 3 * fold
-    adds = 2 * (32 * 255 / 256 + 0.5) - 1
+    adds = 2 * (16 * (1 - 2.0 ** -16) + 0.5) - 1
     return adds * madd + sqr + 2 * mul
 
 

@@ -397,9 +397,19 @@ void collect_times(jg_batch* b) {
 // ---------------------------------------------------------------- keys
 struct StagedKeys {
   std::vector<DevKey> dk;
-  std::vector<uint32_t> blob;
-  std::vector<int32_t> rsa_idx, ec_idx[NCLS], ed_idx;
+  std::vector<uint32_t> blob;      // host-initialised part of the device key blob
+  uint64_t tab_words = 0;          // device-only tail: comb tables (built on the GPU)
+  std::vector<int32_t> rsa_idx, ec_idx[NCLS], ed_idx, tab_keys;
 };
+
+// comb tables never exist on the host: offsets are relative to the device-only
+// tail until build_keys rebases them past the host part
+uint64_t tab_alloc(StagedKeys& S, int key, uint64_t words) {
+  const uint64_t off = S.tab_words;
+  S.tab_words += (words + 3) & ~uint64_t(3);
+  S.tab_keys.push_back(key);
+  return off;
+}
 
 uint64_t blob_alloc(std::vector<uint32_t>& blob, size_t words) {
   const uint64_t off = (blob.size() + 3) & ~size_t(3);          // 16-byte aligned
@@ -453,7 +463,7 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       K.cls = cls;
       K.kbytes = cb;
       K.aux_off = blob_alloc(S.blob, 2 * L);
-      K.tab_off = blob_alloc(S.blob, (size_t)ec_table_words(cls));
+      K.tab_off = tab_alloc(S, i, (uint64_t)ec_table_words(cls));
       const size_t cl = k.coord_len > 0 ? (size_t)k.coord_len : 0;
       // crypto/ecdsa pointFromAffine: coordinates must fit the curve's bit size
       bool ok = k.x && k.y && cl > 0 && bitlen_be(k.x, cl) <= (cls == CLS_P521 ? 521 : cb * 8) &&
@@ -470,7 +480,7 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       K.cls = CLS_ED25519;
       K.kbytes = 32;
       K.aux_off = blob_alloc(S.blob, 8 + 2 * ED_L);
-      K.tab_off = blob_alloc(S.blob, (size_t)ED_TABLE_WORDS);
+      K.tab_off = tab_alloc(S, i, (uint64_t)ED_TABLE_WORDS);
       // crypto/ed25519.Verify panics on len(pub) != 32; go-jose never hands it one
       const bool ok = k.x && k.coord_len == 32;
       if (ok) std::memcpy(S.blob.data() + K.aux_off, k.x, 32);
@@ -482,6 +492,8 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       hk.valid = 0;
     }
   }
+  blob_alloc(S.blob, 0);                                      // align the host part
+  for (int k : S.tab_keys) S.dk[k].tab_off += S.blob.size();
 }
 
 void ensure_tables(Device* d, const StagedKeys& S) {
@@ -507,7 +519,7 @@ void load_keys_device(Device* d, const StagedKeys& S) {
   d->dkeys = nullptr; d->dblob = nullptr; d->didx = nullptr;
   const size_t nk = std::max<size_t>(S.dk.size(), 1);
   HIPCHK(hipMalloc(&d->dkeys, sizeof(DevKey) * nk));
-  HIPCHK(hipMalloc(&d->dblob, sizeof(uint32_t) * std::max<size_t>(S.blob.size(), 4)));
+  HIPCHK(hipMalloc(&d->dblob, sizeof(uint32_t) * std::max<uint64_t>(S.blob.size() + S.tab_words, 4)));
   if (!S.dk.empty()) HIPCHK(hipMemcpyAsync(d->dkeys, S.dk.data(), sizeof(DevKey) * S.dk.size(), hipMemcpyHostToDevice, s));
   if (!S.blob.empty())
     HIPCHK(hipMemcpyAsync(d->dblob, S.blob.data(), sizeof(uint32_t) * S.blob.size(), hipMemcpyHostToDevice, s));

@@ -2,13 +2,14 @@
 //
 // Replaces go-jose ecEncrypterVerifier.verifyPayload -> crypto/ecdsa.Verify
 // (rules R18-R22).  Per token:
-//   k_ec_scalar : r, s in [1, n-1] (sizes from the alg, curve from the key),
-//                 e = leftmost bits of H, w = s^-1, u1 = e w, u2 = r w (mod n),
-//                 u1/u2 recoded to signed 8-bit windows
+//   k_ec_scalar_batch : r, s in [1, n-1] (sizes from the alg, curve from the
+//                 key), e = leftmost bits of H, w = s^-1 (one inversion per B
+//                 tokens), u1 = e w, u2 = r w (mod n), recoded to signed W-bit
+//                 digits (W = ec_comb_w: 16 for P-256, 12 for P-384/P-521)
 //   k_ec_point  : R = u1 G + u2 Q as a sum of one precomputed affine multiple of
-//                 G and one of Q per window (comb tables in HBM / L2: entries
-//                 d * 2^(8w) * P, d = 1..128), mixed Jacobian+affine additions,
-//                 no doublings; accept iff X == r Z^2 or (r+n) Z^2 (no inversion)
+//                 G and one of Q per window (comb tables in HBM: entries
+//                 d * 2^(W w) * P, d = 1..2^(W-1)), mixed Jacobian+affine
+//                 additions, no doublings; accept iff X == r Z^2 or (r+n) Z^2
 //   k_ec_exact  : tokens whose fast sum hit an exceptional case of the group
 //                 law (Z == 0: a doubling, an inverse pair, or R = infinity) --
 //                 recomputed with complete case handling; rare
@@ -107,17 +108,36 @@ __device__ __forceinline__ bool ec_scalar_inputs(const EcArgs& a, int64_t p, uin
   return ok;
 }
 
+// Signed W-bit recoding: u = sum_w d_w 2^(W w), d_w in [-2^(W-1), 2^(W-1)),
+// stored as two int16 per window row (u1 digit low, u2 digit high).
+template <class CV>
+__device__ __forceinline__ void store_digits(const EcArgs& a, int64_t p, const uint32_t* u1, const uint32_t* u2) {
+  constexpr int L = CV::Fn::L;
+  constexpr int W = ec_comb_w(CV::CLS), NWIN = ec_windows(CV::CLS);
+  constexpr uint32_t DM = (1u << W) - 1u;
+  int c1 = 0, c2 = 0;
+#pragma unroll
+  for (int w = 0; w < NWIN; ++w) {
+    const int bit = W * w, q = bit / MP_W, sh = bit % MP_W;
+    uint32_t b1 = q < L ? (u1[q] >> sh) : 0u, b2 = q < L ? (u2[q] >> sh) : 0u;
+    if (sh > MP_W - W && q + 1 < L) { b1 |= u1[q + 1] << (MP_W - sh); b2 |= u2[q + 1] << (MP_W - sh); }
+    int v1 = (int)(b1 & DM) + c1, v2 = (int)(b2 & DM) + c2;
+    c1 = v1 >= (1 << (W - 1)); c2 = v2 >= (1 << (W - 1));
+    v1 -= c1 << W; v2 -= c2 << W;
+    a.digs[(int64_t)w * a.npad + p] = ((uint32_t)v1 & 0xffffu) | ((uint32_t)v2 << 16);
+  }
+}
+
 // Batched scalar stage (Montgomery's trick): thread i owns the B tokens
 // p_j = begin + i + j*S and pays ONE Fermat inversion for all of them:
 //   pass 1: c_j = s_0 ... s_j (Montgomery), c_j and s_j parked in the u1/u2 rows
 //   inv = c_{B-1}^-1
 //   pass 2 (j descending): w_j = inv * c_{j-1}, inv *= s_j;
-//           u1 = e w_j, u2 = r w_j (mod n), signed 8-bit digits
+//           u1 = e w_j, u2 = r w_j (mod n), signed W-bit digits
 template <class CV>
 __global__ void __launch_bounds__(64) k_ec_scalar_batch(EcArgs a, int B) {
   using Fn = typename CV::Fn;
   constexpr int L = Fn::L;
-  constexpr int NWIN = ec_windows(CV::CLS);
   const int64_t np = a.npad;
   const int64_t n = a.end - a.begin;
   const int64_t S = (n + B - 1) / B;
@@ -166,96 +186,8 @@ __global__ void __launch_bounds__(64) k_ec_scalar_batch(EcArgs a, int B) {
       a.u1w[(int64_t)k * np + p] = u1[k];
       a.u2w[(int64_t)k * np + p] = u2[k];
     }
-    // signed 8-bit windows: u = sum d_w 2^(8w), d_w in [-128, 127] (fits the
-    // packed int8; |d| <= 128 indexes the 128-entry tables)
-    int c1 = 0, c2 = 0;
-#pragma unroll
-    for (int w8 = 0; w8 < NWIN; ++w8) {
-      const int bit = 8 * w8, q = bit / MP_W, sh = bit % MP_W;
-      uint32_t b1 = q < L ? (u1[q] >> sh) : 0u, b2 = q < L ? (u2[q] >> sh) : 0u;
-      if (sh > MP_W - 8 && q + 1 < L) { b1 |= u1[q + 1] << (MP_W - sh); b2 |= u2[q + 1] << (MP_W - sh); }
-      int v1 = (int)(b1 & 0xffu) + c1, v2 = (int)(b2 & 0xffu) + c2;
-      c1 = v1 >= 128; c2 = v2 >= 128;
-      v1 -= c1 << 8; v2 -= c2 << 8;
-      a.digs[(int64_t)w8 * np + p] = ((uint32_t)v1 & 0xffu) | (((uint32_t)v2 & 0xffu) << 8);
-    }
+    store_digits<CV>(a, p, u1, u2);
   }
-}
-
-template <class CV>
-__global__ void __launch_bounds__(64) k_ec_scalar(EcArgs a) {
-  using Fn = typename CV::Fn;
-  constexpr int L = Fn::L;
-  constexpr int CB = CV::C::BYTES;
-  constexpr int NWIN = ec_windows(CV::CLS);
-  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
-  const int64_t np = a.npad;
-  const int32_t t = a.perm[p];
-  if (t < 0) return;
-  const int kidx = __builtin_amdgcn_readfirstlane(a.wave_key[p / WAVE]);
-  bool ok = a.status[p] == ST_OK && a.keys[kidx].valid;
-  const int alg = a.toks[t].alg;
-
-  // r, s: big-endian ks-byte integers decoded into LE words by k_prep; any bit
-  // beyond the curve's byte size makes them >= n
-  uint32_t rw[17], sw[17];
-#pragma unroll
-  for (int q = 0; q < 17; ++q) {
-    rw[q] = a.sigw[(int64_t)q * np + p];
-    sw[q] = a.sigw[(int64_t)(EC_S_ROW + q) * np + p];
-  }
-#pragma unroll
-  for (int q = 0; q < 17; ++q) {
-    if (4 * q >= CB) ok = ok && rw[q] == 0 && sw[q] == 0;
-    else if (4 * q + 4 > CB) {
-      const uint32_t hi = ~0u << (8 * (CB - 4 * q));
-      ok = ok && (rw[q] & hi) == 0 && (sw[q] & hi) == 0;
-    }
-  }
-  uint32_t r[L], s[L], e[L];
-  mp::words_to_limbs<L, 17>(r, rw);
-  mp::words_to_limbs<L, 17>(s, sw);
-  uint32_t nl[L];
-  mp::set_const<Fn>(nl, Fn::M);
-  ok = ok && !zero_limbs<L>(r) && !zero_limbs<L>(s) && lt_limbs<L>(r, nl) && lt_limbs<L>(s, nl);
-  // e = leftmost min(hlen, orderBytes) bytes of H (every order here is byte-aligned
-  // except P-521's, whose 66 bytes exceed every hash: no shift needed)  [R21]
-  {
-    const int hl = es_hash_bytes(alg) < CB ? es_hash_bytes(alg) : CB;   // multiple of 4
-    uint32_t ew[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int src = hl / 4 - 1 - q;
-      ew[q] = src >= 0 ? a.dig[(int64_t)(src < 0 ? 0 : src) * np + p] : 0u;
-    }
-    mp::words_to_limbs<L, 16>(e, ew);
-    mp::csub<Fn>(e);                       // e < 2n for every curve/hash pairing
-  }
-  // w = s^-1 (Fermat), u1 = e w, u2 = r w
-  uint32_t sm[L], wm[L], u1[L], u2[L];
-  mp::to_mont<Fn>(sm, s);
-  mp::inv<Fn>(wm, sm);
-  mp::mul<Fn>(u1, e, wm); mp::csub<Fn>(u1);
-  mp::mul<Fn>(u2, r, wm); mp::csub<Fn>(u2);
-#pragma unroll
-  for (int j = 0; j < L; ++j) {
-    a.u1w[(int64_t)j * np + p] = u1[j];
-    a.u2w[(int64_t)j * np + p] = u2[j];
-  }
-  // signed 8-bit windows: u = sum d_w 2^(8w), d_w in [-128, 127] (fits the
-  // packed int8; |d| <= 128 indexes the 128-entry tables)
-  int c1 = 0, c2 = 0;
-#pragma unroll
-  for (int w = 0; w < NWIN; ++w) {
-    const int bit = 8 * w, q = bit / MP_W, sh = bit % MP_W;
-    uint32_t b1 = q < L ? (u1[q] >> sh) : 0u, b2 = q < L ? (u2[q] >> sh) : 0u;
-    if (sh > MP_W - 8 && q + 1 < L) { b1 |= u1[q + 1] << (MP_W - sh); b2 |= u2[q + 1] << (MP_W - sh); }
-    int v1 = (int)(b1 & 0xffu) + c1, v2 = (int)(b2 & 0xffu) + c2;
-    c1 = v1 >= 128; c2 = v2 >= 128;
-    v1 -= c1 << 8; v2 -= c2 << 8;
-    a.digs[(int64_t)w * np + p] = ((uint32_t)v1 & 0xffu) | (((uint32_t)v2 & 0xffu) << 8);
-  }
-  if (!ok) a.status[p] = ST_REJECT;
 }
 
 // ------------------------------------------------------------------ point ops
@@ -295,10 +227,10 @@ template <class CV>
 __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z, bool& empty,
                                            const uint32_t* __restrict__ tab, int w, int d) {
   using Fp = typename CV::Fp;
-  constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS);
+  constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS), NE = ec_entries(CV::CLS);
   if (d == 0) return;
   const int ad = d < 0 ? -d : d;
-  const uint32_t* ent = tab + ((int64_t)w * COMB_ENTRIES + (ad - 1)) * STRIDE;
+  const uint32_t* ent = tab + ((int64_t)w * NE + (ad - 1)) * STRIDE;
   uint32_t x2[L], y2[L];
 #pragma unroll
   for (int j = 0; j < L; ++j) { x2[j] = ent[j]; y2[j] = ent[L + j]; }
@@ -332,8 +264,8 @@ __global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
   bool empty = true;
   for (int w = 0; w < NWIN; ++w) {
     const uint32_t dd = a.digs[(int64_t)w * np + p];
-    const int d1 = (int)(int8_t)(dd & 0xffu);
-    const int d2 = (int)(int8_t)((dd >> 8) & 0xffu);
+    const int d1 = (int)(int16_t)(dd & 0xffffu);
+    const int d2 = (int)(int16_t)(dd >> 16);
     add_window<CV>(X, Y, Z, empty, gtab, w, d1);
     add_window<CV>(X, Y, Z, empty, qtab, w, d2);
   }
@@ -551,52 +483,89 @@ __global__ void k_ec_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, i
   K.valid = ok ? 1 : 0;
 }
 
-// thread per (window w, digit d): entry = d * 2^(8w) * B in affine Montgomery form
 template <class CV>
-__device__ void table_entry(uint32_t* out, const uint32_t* bx, const uint32_t* by, int w, int d) {
+__device__ void store_affine(uint32_t* out, const JPt<typename CV::Fp>& P) {
   using Fp = typename CV::Fp;
   constexpr int L = Fp::L;
-  JPt<Fp> P, acc;
-  affine_point<CV>(P, bx, by);
-  for (int i = 0; i < 8 * w; ++i) jdbl<CV>(P, P);
-  acc.inf = true;
-  for (int bit = 7; bit >= 0; --bit) {
-    jdbl<CV>(acc, acc);
-    if ((d >> bit) & 1) jadd<CV>(acc, acc, P);
-  }
   uint32_t zi[L], zi2[L], zi3[L], x[L], y[L];
-  mp::inv<Fp>(zi, acc.Z);
+  mp::inv<Fp>(zi, P.Z);
   mp::sqr<Fp>(zi2, zi);
   mp::mul<Fp>(zi3, zi2, zi);
-  mp::mul<Fp>(x, acc.X, zi2);
-  mp::mul<Fp>(y, acc.Y, zi3);
+  mp::mul<Fp>(x, P.X, zi2);
+  mp::mul<Fp>(y, P.Y, zi3);
   mp::canon<Fp>(x); mp::canon<Fp>(y);
 #pragma unroll
   for (int j = 0; j < L; ++j) { out[j] = x[j]; out[L + j] = y[j]; }
 }
 
+// window base 2^(W w) * B (= entry d = 1 of window w), affine Montgomery form
 template <class CV>
-__global__ void k_ec_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
-  constexpr int NWIN = ec_windows(CV::CLS), STRIDE = ec_stride(CV::CLS);
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void window_base(uint32_t* out, const uint32_t* bx, const uint32_t* by, int w) {
+  using Fp = typename CV::Fp;
+  JPt<Fp> P;
+  affine_point<CV>(P, bx, by);
+  for (int i = 0; i < ec_comb_w(CV::CLS) * w; ++i) jdbl<CV>(P, P);
+  store_affine<CV>(out, P);
+}
+
+// entry d * base (d < 2^W), affine Montgomery form
+template <class CV>
+__device__ void table_entry(uint32_t* out, const uint32_t* base, int d) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  JPt<Fp> P, acc;
+  affine_point<CV>(P, base, base + L);
+  acc.inf = true;
+  for (int bit = ec_comb_w(CV::CLS) - 1; bit >= 0; --bit) {
+    jdbl<CV>(acc, acc);
+    if ((d >> bit) & 1) jadd<CV>(acc, acc, P);
+  }
+  store_affine<CV>(out, acc);
+}
+
+// Tables are built in two launches: thread per (key, window) for the window
+// bases (entry 1), then thread per (key, entry >= 2) from its window's base.
+template <class CV>
+__global__ void k_ec_table_base_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS), STRIDE = ec_stride(CV::CLS);
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
-  if (k >= n || e >= NWIN * COMB_ENTRIES) return;
+  if (k >= n || w >= NWIN) return;
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
   const uint32_t* aux = blob + K.aux_off;
-  const int w = e / COMB_ENTRIES, d = e % COMB_ENTRIES + 1;
-  table_entry<CV>(blob + K.tab_off + (int64_t)e * STRIDE, aux, aux + CV::Fp::L, w, d);
+  window_base<CV>(blob + K.tab_off + (int64_t)w * NE * STRIDE, aux, aux + CV::Fp::L, w);
+}
+
+template <class CV>
+__global__ void k_ec_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS), STRIDE = ec_stride(CV::CLS);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (k >= n || e >= NWIN * NE || e % NE == 0) return;
+  const DevKey& K = keys[idx[k]];
+  if (!K.valid) return;
+  uint32_t* tab = blob + K.tab_off;
+  table_entry<CV>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
+}
+
+template <class CV>
+__global__ void k_ec_table_base_g(uint32_t* tab) {
+  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS), STRIDE = ec_stride(CV::CLS);
+  using Fp = typename CV::Fp;
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= NWIN) return;
+  uint32_t gx[Fp::L], gy[Fp::L];
+  mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
+  window_base<CV>(tab + (int64_t)w * NE * STRIDE, gx, gy, w);
 }
 
 template <class CV>
 __global__ void k_ec_table_g(uint32_t* tab) {
-  constexpr int NWIN = ec_windows(CV::CLS), STRIDE = ec_stride(CV::CLS);
-  using Fp = typename CV::Fp;
+  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS), STRIDE = ec_stride(CV::CLS);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= NWIN * COMB_ENTRIES) return;
-  uint32_t gx[Fp::L], gy[Fp::L];
-  mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
-  table_entry<CV>(tab + (int64_t)e * STRIDE, gx, gy, e / COMB_ENTRIES, e % COMB_ENTRIES + 1);
+  if (e >= NWIN * NE || e % NE == 0) return;
+  table_entry<CV>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
 }
 
 template <class CV>
@@ -616,6 +585,22 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   mk("exact");
 }
 
+template <class CV>
+void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
+  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS);
+  dim3 b(64);
+  hipLaunchKernelGGL(k_ec_keyprep<CV>, dim3((n + 63) / 64), b, 0, s, keys, blob, idx, n);
+  hipLaunchKernelGGL(k_ec_table_base_keys<CV>, dim3((NWIN + 63) / 64, n), b, 0, s, keys, blob, idx, n);
+  hipLaunchKernelGGL(k_ec_table_keys<CV>, dim3((NWIN * NE + 63) / 64, n), b, 0, s, keys, blob, idx, n);
+}
+
+template <class CV>
+void gtable_chain(uint32_t* tab, hipStream_t s) {
+  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS);
+  hipLaunchKernelGGL(k_ec_table_base_g<CV>, dim3((NWIN + 63) / 64), dim3(64), 0, s, tab);
+  hipLaunchKernelGGL(k_ec_table_g<CV>, dim3((NWIN * NE + 63) / 64), dim3(64), 0, s, tab);
+}
+
 }  // namespace
 
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const Marker& mk) {
@@ -630,33 +615,19 @@ void launch_ec(int cls, const EcArgs& a, hipStream_t s, const Marker& mk) {
 
 void launch_ec_keyprep(int cls, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
   if (n <= 0) return;
-  dim3 g1((n + 63) / 64), b(64);
-  const int nwin = ec_windows(cls);
-  dim3 g2((nwin * COMB_ENTRIES + 63) / 64, n);
   switch (cls) {
-    case CLS_P256:
-      hipLaunchKernelGGL(k_ec_keyprep<CurveP256>, g1, b, 0, s, keys, blob, idx, n);
-      hipLaunchKernelGGL(k_ec_table_keys<CurveP256>, g2, b, 0, s, keys, blob, idx, n);
-      break;
-    case CLS_P384:
-      hipLaunchKernelGGL(k_ec_keyprep<CurveP384>, g1, b, 0, s, keys, blob, idx, n);
-      hipLaunchKernelGGL(k_ec_table_keys<CurveP384>, g2, b, 0, s, keys, blob, idx, n);
-      break;
-    case CLS_P521:
-      hipLaunchKernelGGL(k_ec_keyprep<CurveP521>, g1, b, 0, s, keys, blob, idx, n);
-      hipLaunchKernelGGL(k_ec_table_keys<CurveP521>, g2, b, 0, s, keys, blob, idx, n);
-      break;
+    case CLS_P256: keyprep_chain<CurveP256>(keys, blob, idx, n, s); break;
+    case CLS_P384: keyprep_chain<CurveP384>(keys, blob, idx, n, s); break;
+    case CLS_P521: keyprep_chain<CurveP521>(keys, blob, idx, n, s); break;
     default: break;
   }
 }
 
 void launch_ec_gtable(int cls, uint32_t* tab, hipStream_t s) {
-  const int nwin = ec_windows(cls);
-  dim3 g((nwin * COMB_ENTRIES + 63) / 64), b(64);
   switch (cls) {
-    case CLS_P256: hipLaunchKernelGGL(k_ec_table_g<CurveP256>, g, b, 0, s, tab); break;
-    case CLS_P384: hipLaunchKernelGGL(k_ec_table_g<CurveP384>, g, b, 0, s, tab); break;
-    case CLS_P521: hipLaunchKernelGGL(k_ec_table_g<CurveP521>, g, b, 0, s, tab); break;
+    case CLS_P256: gtable_chain<CurveP256>(tab, s); break;
+    case CLS_P384: gtable_chain<CurveP384>(tab, s); break;
+    case CLS_P521: gtable_chain<CurveP521>(tab, s); break;
     default: break;
   }
 }

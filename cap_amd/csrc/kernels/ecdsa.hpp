@@ -16,7 +16,7 @@ struct EcArgs {
   const uint32_t* dig;        // digest rows (big-endian words)
   uint8_t* status;
   uint8_t* verdict_pad;
-  uint32_t* digs;             // per window: packed signed digits (d1 | d2 << 8)
+  uint32_t* digs;             // per window: packed signed digits (d1 | d2 << 16), int16 each
   uint32_t* u1w;              // u1, u2 canonical 28-bit limb rows (exact path)
   uint32_t* u2w;
   const uint32_t* gtab;       // comb table of the generator for this curve
@@ -28,9 +28,17 @@ struct EcArgs {
 // table geometry per curve: words per entry (x,y Montgomery limbs, 16-B aligned)
 constexpr int ec_limbs(int cls) { return cls == jgk::CLS_P256 ? 10 : cls == jgk::CLS_P384 ? 15 : 20; }
 constexpr int ec_stride(int cls) { return (2 * ec_limbs(cls) + 3) & ~3; }
-constexpr int ec_windows(int cls) { return cls == jgk::CLS_P256 ? 33 : cls == jgk::CLS_P384 ? 49 : 66; }
+constexpr int ec_order_bits(int cls) { return cls == jgk::CLS_P256 ? 256 : cls == jgk::CLS_P384 ? 384 : 521; }
+// Fixed-base comb over signed w-bit digits: u = sum_w d_w 2^(W w), d_w in
+// [-2^(W-1), 2^(W-1)), so a token costs ceil((bits+1)/W) mixed additions per
+// scalar and each (key, window) holds 2^(W-1) affine multiples d 2^(W w) P.
+// Wider W trades HBM (P-256, W=16: 44.6 MB per key, 288 GB per GPU) for fewer
+// additions; digits are packed as two int16 per word, so W <= 16.
+constexpr int ec_comb_w(int cls) { return cls == jgk::CLS_P256 ? 16 : 12; }
+constexpr int ec_entries(int cls) { return 1 << (ec_comb_w(cls) - 1); }
+constexpr int ec_windows(int cls) { return (ec_order_bits(cls) + 1 + ec_comb_w(cls) - 1) / ec_comb_w(cls); }
 constexpr int64_t ec_table_words(int cls) {
-  return (int64_t)ec_windows(cls) * jgk::COMB_ENTRIES * ec_stride(cls);
+  return (int64_t)ec_windows(cls) * ec_entries(cls) * ec_stride(cls);
 }
 
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);

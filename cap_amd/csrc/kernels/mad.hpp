@@ -15,6 +15,12 @@ __device__ __forceinline__ void mad64(uint64_t& acc, uint32_t a, uint32_t b) {
   asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
 }
 
+// acc = a * b (first partial product of a column: no zero-initialised accumulator)
+__device__ __forceinline__ void mul64(uint64_t& acc, uint32_t a, uint32_t b) {
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(acc), "=s"(cc) : "v"(a), "v"(b));
+}
+
 // b wave-uniform (SGPR operand)
 __device__ __forceinline__ void mad64s(uint64_t& acc, uint32_t a, uint32_t b) {
   uint64_t cc;

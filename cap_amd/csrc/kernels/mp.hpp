@@ -32,10 +32,20 @@ MPD void mont_reduce(uint32_t* r, uint64_t* t) {
   constexpr int L = F::L;
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    const uint32_t m = ((uint32_t)t[i] * F::NP) & MP_MASK;
+    if constexpr (F::NP1) {
+      // m = -1 mod 2^28 => NP = 1, q = t[i] mod 2^28 and q*m = q*(m+1) - q:
+      // the "- q" is exactly the low limb the carry shift drops, and m+1 is
+      // sparse (P-256: 4 non-zero limbs of 10, P-521: 1 of 20).
+      const uint32_t q = (uint32_t)t[i] & MP_MASK;
 #pragma unroll
-    for (int j = 0; j < L; ++j)
-      if (F::M[j] != 0) mad64s(t[i + j], m, F::M[j]);
+      for (int j = 1; j < L; ++j)
+        if (F::M1[j] != 0) mad64s(t[i + j], q, F::M1[j]);
+    } else {
+      const uint32_t q = ((uint32_t)t[i] * F::NP) & MP_MASK;
+#pragma unroll
+      for (int j = 0; j < L; ++j)
+        if (F::M[j] != 0) mad64s(t[i + j], q, F::M[j]);
+    }
     t[i + 1] += t[i] >> MP_W;
   }
   uint64_t c = 0;
@@ -52,12 +62,15 @@ template <class F>
 MPD void mul(uint32_t* r, const uint32_t* a, const uint32_t* b) {
   constexpr int L = F::L;
   uint64_t t[2 * L];
-#pragma unroll
-  for (int k = 0; k < 2 * L; ++k) t[k] = 0;
+  t[2 * L - 1] = 0;
 #pragma unroll
   for (int i = 0; i < L; ++i)
 #pragma unroll
-    for (int j = 0; j < L; ++j) mad64(t[i + j], a[i], b[j]);
+    for (int j = 0; j < L; ++j) {
+      // first product of column i+j in this loop order writes, not accumulates
+      if (i == 0 || j == L - 1) mul64(t[i + j], a[i], b[j]);
+      else mad64(t[i + j], a[i], b[j]);
+    }
   mont_reduce<F>(r, t);
 }
 
@@ -69,13 +82,16 @@ MPD void sqr(uint32_t* r, const uint32_t* a) {
   uint32_t a2[L];
 #pragma unroll
   for (int i = 0; i < L; ++i) a2[i] = a[i] << 1;
-#pragma unroll
-  for (int k = 0; k < 2 * L; ++k) t[k] = 0;
+  t[2 * L - 1] = 0;
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    mad64(t[2 * i], a[i], a[i]);
+    if (i == 0 || i == L - 1) mul64(t[2 * i], a[i], a[i]);
+    else mad64(t[2 * i], a[i], a[i]);
 #pragma unroll
-    for (int j = i + 1; j < L; ++j) mad64(t[i + j], a2[i], a[j]);
+    for (int j = i + 1; j < L; ++j) {
+      if (i == 0 || j == L - 1) mul64(t[i + j], a2[i], a[j]);
+      else mad64(t[i + j], a2[i], a[j]);
+    }
   }
   mont_reduce<F>(r, t);
 }

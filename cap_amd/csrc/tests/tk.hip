@@ -115,7 +115,9 @@ __global__ void k_tk_entry(const int* wd, uint32_t* out, int n) {
   if (i >= n) return;
   uint32_t gx[L], gy[L];
   mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
-  table_entry<CV>(out + (size_t)i * 2 * L, gx, gy, wd[2 * i], wd[2 * i + 1]);
+  uint32_t base[2 * L];
+  window_base<CV>(base, gx, gy, wd[2 * i]);
+  table_entry<CV>(out + (size_t)i * 2 * L, base, wd[2 * i + 1]);
 }
 
 template <class CV>

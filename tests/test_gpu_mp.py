@@ -187,13 +187,15 @@ def test_generator_table_entries(tk, cid):
     p, L = c["p"], c["L"]
     R = 1 << (W * L)
     G = (c["gx"], c["gy"])
-    nwin = {1: 33, 2: 49, 3: 66}[cid]
-    wd = [(0, 1), (0, 2), (0, 128), (1, 1), (1, 127), (5, 64), (nwin - 1, 1), (nwin - 1, 128), (nwin // 2, 77)]
+    cw = {1: 16, 2: 12, 3: 12}[cid]                 # ecdsa.hpp ec_comb_w
+    nwin = -(-(c["n"].bit_length() + 1) // cw)
+    ne = 1 << (cw - 1)
+    wd = [(0, 1), (0, 2), (0, ne), (1, 1), (1, ne - 1), (5, 64), (nwin - 1, 1), (nwin - 1, ne), (nwin // 2, 77)]
     A = (ctypes.c_int * (2 * len(wd)))(*[v for t in wd for v in t])
     O = (ctypes.c_uint32 * (len(wd) * 2 * L))()
     assert tk.tk_ec(cid, 1, A, ctypes.sizeof(A), O, ctypes.sizeof(O), len(wd)) == 0
     for i, (w, d) in enumerate(wd):
-        want = ec_mul(c, d << (8 * w), G)
+        want = ec_mul(c, d << (cw * w), G)
         x = from_limbs(O[2 * i * L:(2 * i + 1) * L])
         y = from_limbs(O[(2 * i + 1) * L:(2 * i + 2) * L])
         assert (x, y) == (want[0] * R % p, want[1] * R % p), (w, d)
