@@ -5,24 +5,45 @@
 // aligned 64-bit register pairs, wasting one VGPR per operand: a 37-limb x
 // 37-limb CIOS step needed 225 VGPRs that way and 154 with this wrapper
 // (gfx950 requires 64-bit VGPR tuples to be even-aligned).  The carry-out
-// SGPR pair of the VOP3b encoding is a dead output the allocator may reuse.
+// SGPR pair of the VOP3b encoding is dead.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
-__device__ __forceinline__ void mad64(uint64_t& acc, uint32_t a, uint32_t b) {
-  uint64_t cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
+// The carry-out goes to a hard-wired SGPR pair chosen by `slot`.  LLVM's
+// gfx950 hazard recognizer assumes an inline asm statement may carry a dst-forwarding hazard and pads an s_nop before the next
+// instruction that touches any register the asm defined -- with the carry-out
+// as an allocated operand every MAD landed on the same dead SGPR pair, so
+// every MAD paid an s_nop (4 issue cycles): 36.0 vs 29.1 T MAD/s at 4
+// waves/SIMD (profiles/r01_int_rates2.json).  Callers pass a compile-time
+// slot (after unrolling) selecting one of 4 pairs: products alternate slots
+// 0/1 and reductions 2/3, so interleaved product and reduction streams
+// rarely put the same pair back to back.
+#define JG_MAD_ACC(PAIR, LO, HI, SRC_B) \
+  asm("v_mad_u64_u32 %0, " PAIR ", %1, %2, %0" : "+v"(acc) : "v"(a), SRC_B(b) : LO, HI)
+#define JG_MAD_SET(PAIR, LO, HI, SRC_B) \
+  asm("v_mad_u64_u32 %0, " PAIR ", %1, %2, 0" : "=v"(acc) : "v"(a), SRC_B(b) : LO, HI)
+#define JG_MAD_ASM(ONE, SRC_B)                                  \
+  switch (slot & 3) {                                           \
+    case 0: ONE("s[88:89]", "s88", "s89", SRC_B); break;        \
+    case 1: ONE("s[90:91]", "s90", "s91", SRC_B); break;        \
+    case 2: ONE("s[92:93]", "s92", "s93", SRC_B); break;        \
+    default: ONE("s[94:95]", "s94", "s95", SRC_B); break;       \
+  }
+#define JG_V(x) "v"(x)
+#define JG_S(x) "s"(x)
+
+// acc += a * b
+__device__ __forceinline__ void mad64(uint64_t& acc, uint32_t a, uint32_t b, int slot = 0) {
+  JG_MAD_ASM(JG_MAD_ACC, JG_V);
 }
 
 // acc = a * b (first partial product of a column: no zero-initialised accumulator)
-__device__ __forceinline__ void mul64(uint64_t& acc, uint32_t a, uint32_t b) {
-  uint64_t cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(acc), "=s"(cc) : "v"(a), "v"(b));
+__device__ __forceinline__ void mul64(uint64_t& acc, uint32_t a, uint32_t b, int slot = 0) {
+  JG_MAD_ASM(JG_MAD_SET, JG_V);
 }
 
-// b wave-uniform (SGPR operand)
-__device__ __forceinline__ void mad64s(uint64_t& acc, uint32_t a, uint32_t b) {
-  uint64_t cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "s"(b));
+// acc += a * b, b wave-uniform (SGPR operand)
+__device__ __forceinline__ void mad64s(uint64_t& acc, uint32_t a, uint32_t b, int slot = 0) {
+  JG_MAD_ASM(JG_MAD_ACC, JG_S);
 }

@@ -39,12 +39,12 @@ MPD void mont_reduce(uint32_t* r, uint64_t* t) {
       const uint32_t q = (uint32_t)t[i] & MP_MASK;
 #pragma unroll
       for (int j = 1; j < L; ++j)
-        if (F::M1[j] != 0) mad64s(t[i + j], q, F::M1[j]);
+        if (F::M1[j] != 0) mad64s(t[i + j], q, F::M1[j], 2 + (j & 1));
     } else {
       const uint32_t q = ((uint32_t)t[i] * F::NP) & MP_MASK;
 #pragma unroll
       for (int j = 0; j < L; ++j)
-        if (F::M[j] != 0) mad64s(t[i + j], q, F::M[j]);
+        if (F::M[j] != 0) mad64s(t[i + j], q, F::M[j], 2 + (j & 1));
     }
     t[i + 1] += t[i] >> MP_W;
   }
@@ -68,8 +68,8 @@ MPD void mul(uint32_t* r, const uint32_t* a, const uint32_t* b) {
 #pragma unroll
     for (int j = 0; j < L; ++j) {
       // first product of column i+j in this loop order writes, not accumulates
-      if (i == 0 || j == L - 1) mul64(t[i + j], a[i], b[j]);
-      else mad64(t[i + j], a[i], b[j]);
+      if (i == 0 || j == L - 1) mul64(t[i + j], a[i], b[j], j & 1);
+      else mad64(t[i + j], a[i], b[j], j & 1);
     }
   mont_reduce<F>(r, t);
 }
@@ -85,12 +85,12 @@ MPD void sqr(uint32_t* r, const uint32_t* a) {
   t[2 * L - 1] = 0;
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    if (i == 0 || i == L - 1) mul64(t[2 * i], a[i], a[i]);
-    else mad64(t[2 * i], a[i], a[i]);
+    if (i == 0 || i == L - 1) mul64(t[2 * i], a[i], a[i], 1);
+    else mad64(t[2 * i], a[i], a[i], 1);
 #pragma unroll
     for (int j = i + 1; j < L; ++j) {
-      if (i == 0 || j == L - 1) mul64(t[i + j], a2[i], a[j]);
-      else mad64(t[i + j], a2[i], a[j]);
+      if (i == 0 || j == L - 1) mul64(t[i + j], a2[i], a[j], (j - i + 1) & 1);
+      else mad64(t[i + j], a2[i], a[j], (j - i + 1) & 1);
     }
   }
   mont_reduce<F>(r, t);
@@ -148,7 +148,7 @@ MPD void freduce(uint32_t* r) {
 #pragma unroll
   for (int j = 0; j < L; ++j) {
     uint64_t v = (uint64_t)r[j] + c;
-    if (F::FOLDC[j] != 0) mad64s(v, h, F::FOLDC[j]);
+    if (F::FOLDC[j] != 0) mad64s(v, h, F::FOLDC[j], 2 + (j & 1));
     r[j] = (uint32_t)v & MP_MASK;
     c = v >> MP_W;
   }

@@ -59,10 +59,10 @@ template <int H, int G>
 __device__ __forceinline__ void cios_step(uint64_t* T, uint32_t ai, const uint32_t* v, const uint32_t* n,
                                           uint32_t np, bool lane0, bool lastl) {
 #pragma unroll
-  for (int j = 0; j < H; ++j) mad64(T[j], ai, v[j]);
+  for (int j = 0; j < H; ++j) mad64(T[j], ai, v[j], j & 1);
   const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
 #pragma unroll
-  for (int j = 0; j < H; ++j) mad64(T[j], m, n[j]);
+  for (int j = 0; j < H; ++j) mad64(T[j], m, n[j], 2 + (j & 1));
   const uint64_t c = lane0 ? (T[0] >> W28) : 0ull;
   T[1] += c;
   const uint32_t lo = from_next<G>((uint32_t)T[0]);

@@ -49,12 +49,27 @@ DEF_KERNEL(k_lshl_add_u64,
 DEF_KERNEL(k_mad_u64_u32_dep,
   asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c[0]) : "v"(a[k]), "v"(b) : "vcc"))
 
+// 8 MADs per asm statement: the compiler's conservative s_nop between inline
+// asm statements is paid once per 8 instead of once per MAD
+#define MAD8(c, a, b) asm volatile(                                     \
+  "v_mad_u64_u32 %0, s[100:101], %8, %9, %0\n"                          \
+  "v_mad_u64_u32 %1, s[100:101], %8, %9, %1\n"                          \
+  "v_mad_u64_u32 %2, s[100:101], %8, %9, %2\n"                          \
+  "v_mad_u64_u32 %3, s[100:101], %8, %9, %3\n"                          \
+  "v_mad_u64_u32 %4, s[100:101], %8, %9, %4\n"                          \
+  "v_mad_u64_u32 %5, s[100:101], %8, %9, %5\n"                          \
+  "v_mad_u64_u32 %6, s[100:101], %8, %9, %6\n"                          \
+  "v_mad_u64_u32 %7, s[100:101], %8, %9, %7"                             \
+  : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(c[4]), "+v"(c[5]), "+v"(c[6]), "+v"(c[7]) \
+  : "v"(a), "v"(b) : "s100", "s101")
+DEF_KERNEL(k_mad_block8, if (k == 0) { MAD8(c, a[1], b); })
+
 struct K { const char* name; void (*fn)(uint32_t*, uint32_t); };
 
 int main() {
   K ks[] = {
     {"v_mad_u64_u32", k_mad_u64_u32}, {"v_mad_u64_u32(sgpr)", k_mad_u64_u32_sgpr},
-    {"v_mad_u64_u32(dep chain)", k_mad_u64_u32_dep},
+    {"v_mad_u64_u32(dep chain)", k_mad_u64_u32_dep}, {"v_mad_u64_u32(8 per asm)", k_mad_block8},
     {"v_mul_lo_u32", k_mul_lo_u32}, {"v_mul_hi_u32", k_mul_hi_u32},
     {"v_mad_u32_u24", k_mad_u32_u24}, {"v_mul_hi_u32_u24", k_mul_hi_u32_u24},
     {"v_add_co_u32", k_add_co_u32}, {"v_addc_co_u32", k_addc_co_u32},
