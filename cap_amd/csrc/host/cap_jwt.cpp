@@ -1,0 +1,815 @@
+// cap_jwt.cpp -- see cap_jwt.hpp.
+//
+// Batch flow of KeySet::verify_batch:
+//   1. host threads parse every token (go-jose ParseSigned, R1-R8); compact
+//      tokens take a fast path whose protected-header decode is memoised per
+//      header segment (tokens signed by one issuer share it byte for byte);
+//   2. each token becomes one arena entry  signing-input '.' base64url(sig):
+//      canonical tokens are copied as they are, anything else is re-encoded
+//      (R6), so the device always sees go-jose's computeAuthData bytes;
+//   3. candidate keys per token -- static set: every key of the alg's family,
+//      in order (R33); JWKS: keys whose kid matches, all keys when the token
+//      has none (R34) -- become jg_tok jobs, verified in ONE jg_verify_batch;
+//   4. host threads turn verdicts into (claims, error) exactly as the
+//      reference's per-token loop would (first verifying key wins; the claims
+//      do not depend on which key verified).
+#include "cap_jwt.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+#include <unordered_map>
+
+#include "../../../include/jg.h"
+
+namespace capjwt {
+
+const char* const kSupportedAlgorithms[10] = {"RS256", "RS384", "RS512", "ES256", "ES384",
+                                              "ES512", "PS256", "PS384", "PS512", "EdDSA"};
+
+std::string SupportedSigningAlgorithm(const std::vector<std::string>& algs) {
+  for (const auto& a : algs)
+    if (!alg_id(a)) return "unsupported signing algorithm \"" + a + "\"";
+  return "";
+}
+
+int host_threads() {
+  static const int n = [] {
+    if (const char* e = std::getenv("CAPJWT_HOST_THREADS")) {
+      const int v = std::atoi(e);
+      if (v > 0) return v;
+    }
+    const int hw = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(hw > 0 ? hw : 1, 16));
+  }();
+  return n;
+}
+
+namespace {
+
+template <class F>
+void parallel_for(size_t n, int threads, F&& fn) {
+  // fn(begin, end): contiguous chunks; small batches stay on the caller's thread
+  const size_t min_chunk = 512;
+  const size_t nt = std::min<size_t>((size_t)std::max(1, threads), (n + min_chunk - 1) / min_chunk);
+  if (nt <= 1) {
+    if (n) fn((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (size_t t = 0; t < nt; ++t) {
+    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    th.emplace_back([&fn, lo, hi] { fn(lo, hi); });
+  }
+  for (auto& t : th) t.join();
+}
+
+int64_t wall_now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+// ---------------------------------------------------------------- per-token parse
+struct HdrInfo {                 // one decoded protected-header segment (compact form)
+  bool b64_ok = false;
+  std::string b64_err;
+  bool ok = false;               // JSON + sanitize
+  std::string err;
+  Signature sig;                 // protected_raw / protected_hdr / alg / kid
+  bool seg_canonical = false;
+  bool verifiable = false;       // crit understood, non-empty protected bytes
+  bool needs_b64 = true;
+  int alg = 0;
+};
+
+std::shared_ptr<const HdrInfo> make_hdr(std::string_view seg) {
+  auto h = std::make_shared<HdrInfo>();
+  h->b64_ok = b64url_decode(seg, &h->sig.protected_raw, &h->b64_err);
+  if (!h->b64_ok) return h;
+  // parse the header exactly as parse_signed does, on a minimal token
+  JWS j;
+  std::string tok = b64url_encode(h->sig.protected_raw) + "..";
+  if (!parse_signed(tok, &j, &h->err)) return h;
+  h->ok = true;
+  h->sig = j.sigs[0];
+  h->seg_canonical = b64url_canonical(seg);
+  std::string si;
+  h->verifiable = signing_input(j, &si);       // payload "" -> crit / protected checks only
+  if (const json::Value* b = h->sig.protected_hdr.get("b64"); b && b->kind == json::Value::Bool) h->needs_b64 = b->b;
+  h->alg = alg_id(h->sig.alg);
+  return h;
+}
+
+struct HdrCache {
+  std::unordered_map<std::string, std::shared_ptr<const HdrInfo>> m;
+  std::shared_ptr<const HdrInfo> get(std::string_view seg) {
+    auto it = m.find(std::string(seg));
+    if (it != m.end()) return it->second;
+    if (m.size() > 4096) m.clear();
+    auto h = make_hdr(seg);
+    m.emplace(std::string(seg), h);
+    return h;
+  }
+};
+
+struct Tok {
+  TokenInfo info;
+  std::string payload;
+  std::string kid;
+  int alg = 0;
+  bool verifiable = false;     // DetachedVerify gets as far as verifyPayload
+  // arena entry: literal token span, or owned bytes
+  const char* lit = nullptr;
+  size_t lit_len = 0;
+  std::string owned;
+  uint32_t si_len = 0, sig_b64_len = 0;
+  uint64_t arena_off = 0;
+};
+
+void parse_one(std::string_view token, HdrCache& cache, Tok* t) {
+  // compact fast path: no whitespace / non-ASCII, exactly three segments
+  if (!token.empty() && token[0] != '{' && !has_go_space_or_nonascii(token)) {
+    const size_t d1 = token.find('.');
+    const size_t d2 = d1 == std::string_view::npos ? d1 : token.find('.', d1 + 1);
+    if (d1 == std::string_view::npos || d2 == std::string_view::npos ||
+        token.find('.', d2 + 1) != std::string_view::npos) {
+      t->info.parse_err = "square/go-jose: compact JWS format must have three parts";
+      return;
+    }
+    const std::string_view hs = token.substr(0, d1), ps = token.substr(d1 + 1, d2 - d1 - 1),
+                           ss = token.substr(d2 + 1);
+    auto h = cache.get(hs);
+    // parseSignedCompact order: protected, payload, signature decodes, then sanitize
+    if (!h->b64_ok) { t->info.parse_err = h->b64_err; return; }
+    if (!b64url_decode(ps, &t->payload, &t->info.parse_err)) return;
+    std::string sig;
+    if (!b64url_decode(ss, &sig, &t->info.parse_err)) return;
+    if (!h->ok) { t->info.parse_err = h->err; return; }
+    t->info.parsed = true;
+    t->info.nsigs = 1;
+    t->info.sig0_len = sig.size();
+    t->info.alg = h->sig.alg;
+    t->kid = h->sig.kid;
+    t->alg = h->alg;
+    t->verifiable = h->verifiable && t->alg != 0;
+    if (!t->verifiable) return;
+    const bool sig_canon = b64url_canonical(ss);
+    if (h->seg_canonical && h->needs_b64 && b64url_canonical(ps) && sig_canon) {
+      t->lit = token.data();
+      t->lit_len = token.size();
+      t->si_len = (uint32_t)d2;
+      t->sig_b64_len = (uint32_t)ss.size();
+      return;
+    }
+    JWS j;
+    j.payload = t->payload;
+    j.sigs.push_back(h->sig);
+    std::string si;
+    signing_input(j, &si);
+    t->si_len = (uint32_t)si.size();
+    t->owned = std::move(si);
+    t->owned.push_back('.');
+    const std::string sb = b64url_encode(sig);
+    t->sig_b64_len = (uint32_t)sb.size();
+    t->owned += sb;
+    return;
+  }
+  // general path: jose.ParseSigned
+  JWS j;
+  if (!parse_signed(token, &j, &t->info.parse_err)) return;
+  t->info.parsed = true;
+  t->info.nsigs = j.sigs.size();
+  t->info.sig0_len = j.sigs.empty() ? 0 : j.sigs[0].signature.size();
+  t->info.alg = j.sigs.empty() ? "" : j.sigs[0].alg;
+  t->kid = j.sigs.empty() ? "" : j.sigs[0].kid;      // go-oidc: the first signature's kid
+  t->payload = j.payload;
+  std::string si;
+  if (!signing_input(j, &si)) return;
+  t->alg = alg_id(j.sigs[0].alg);
+  t->verifiable = t->alg != 0;
+  if (!t->verifiable) return;
+  t->si_len = (uint32_t)si.size();
+  t->owned = std::move(si);
+  t->owned.push_back('.');
+  const std::string sb = b64url_encode(j.sigs[0].signature);
+  t->sig_b64_len = (uint32_t)sb.size();
+  t->owned += sb;
+}
+
+// json.Unmarshal(payload, &map[string]interface{})  [R33, R35, R40]
+bool claims_map(const std::string& payload, json::Value* out, std::string* err) {
+  if (!json::parse(payload, out, err)) return false;
+  if (out->is_null()) return true;
+  if (out->kind != json::Value::Object) {
+    static const char* names[] = {"null", "bool", "number", "string", "array", "object"};
+    *err = std::string("json: cannot unmarshal ") + names[out->kind] + " into Go value of type map[string]interface {}";
+    return false;
+  }
+  if (json::has_range_error(*out)) {
+    *err = "json: cannot unmarshal number into Go value of type float64";
+    return false;
+  }
+  return true;
+}
+
+jg_key to_jg(const PublicKey& k) {
+  jg_key o{};
+  switch (k.kind) {
+    case PublicKey::RSA:
+      o.kind = JG_KEY_RSA;
+      o.n = (const uint8_t*)k.n.data();
+      o.n_len = (int32_t)k.n.size();
+      o.e = k.e;
+      break;
+    case PublicKey::EC:
+      o.kind = JG_KEY_EC;
+      o.curve = k.curve;
+      o.x = (const uint8_t*)k.x.data();
+      o.y = (const uint8_t*)k.y.data();
+      o.coord_len = (int32_t)k.x.size();
+      break;
+    case PublicKey::Ed25519:
+      o.kind = JG_KEY_ED25519;
+      o.x = (const uint8_t*)k.x.data();
+      o.coord_len = (int32_t)k.x.size();
+      break;
+    default:
+      o.kind = 0;         // HMAC secret / private key / nothing: verifies no token on this path
+  }
+  return o;
+}
+
+int key_family(const PublicKey& k) {
+  switch (k.kind) {
+    case PublicKey::RSA: return JG_KEY_RSA;
+    case PublicKey::EC: return JG_KEY_EC;
+    case PublicKey::Ed25519: return k.x.size() == 32 ? JG_KEY_ED25519 : 0;
+    default: return 0;
+  }
+}
+
+// The GPU half shared by both key sets: parse, pack, verify.  `cand(t, push)`
+// pushes the key indices to try for token t.
+struct Verified {
+  std::vector<Tok> toks;
+  std::vector<uint8_t> any;      // some candidate key verified
+};
+
+template <class Cand>
+void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verified* V, Cand&& cand,
+                const std::vector<size_t>* subset = nullptr) {
+  const size_t n = subset ? subset->size() : tokens.size();
+  auto tok_index = [&](size_t i) { return subset ? (*subset)[i] : i; };
+  if (!subset) {
+    V->toks.assign(tokens.size(), Tok());
+    parallel_for(n, eng.threads(), [&](size_t lo, size_t hi) {
+      HdrCache cache;
+      for (size_t i = lo; i < hi; ++i) parse_one(tokens[i], cache, &V->toks[i]);
+    });
+  }
+  V->any.resize(tokens.size(), 0);
+  // arena layout: prefix sums of entry sizes
+  std::vector<uint64_t> off(n + 1, 0);
+  std::vector<uint32_t> njob(n + 1, 0);
+  std::vector<std::vector<uint16_t>> keys_of(n);
+  for (size_t i = 0; i < n; ++i) {
+    Tok& t = V->toks[tok_index(i)];
+    uint64_t sz = 0;
+    if (t.verifiable) {
+      cand(t, keys_of[i]);
+      if (!keys_of[i].empty()) sz = t.lit ? t.lit_len : t.owned.size();
+    }
+    t.arena_off = off[i];
+    off[i + 1] = off[i] + sz;
+    njob[i + 1] = njob[i] + (uint32_t)keys_of[i].size();
+  }
+  const size_t total_jobs = njob[n];
+  if (total_jobs == 0) return;
+  const uint64_t arena_len = off[n];
+  uint8_t* arena = eng.arena_buffer(arena_len);
+  std::vector<jg_tok> jobs(total_jobs);
+  std::vector<uint32_t> job_tok(total_jobs);
+  parallel_for(n, eng.threads(), [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      if (keys_of[i].empty()) continue;
+      const Tok& t = V->toks[tok_index(i)];
+      if (t.lit) std::memcpy(arena + off[i], t.lit, t.lit_len);
+      else std::memcpy(arena + off[i], t.owned.data(), t.owned.size());
+      for (size_t k = 0; k < keys_of[i].size(); ++k) {
+        jg_tok& j = jobs[njob[i] + k];
+        j.off = off[i];
+        j.sig_in_len = t.si_len;
+        j.sig_rel_off = t.si_len + 1;
+        j.sig_b64_len = t.sig_b64_len;
+        j.key_idx = keys_of[i][k];
+        j.alg = (uint8_t)t.alg;
+        j.flags = 0;
+        job_tok[njob[i] + k] = (uint32_t)tok_index(i);
+      }
+    }
+  });
+  std::vector<uint8_t> verdict(total_jobs, 0);
+  eng.verify(arena, arena_len, jobs.data(), total_jobs, verdict.data());
+  for (size_t j = 0; j < total_jobs; ++j)
+    if (verdict[j] == JG_ACCEPT) V->any[job_tok[j]] = 1;
+}
+
+// ---------------------------------------------------------------- static key set
+class StaticKeySet final : public KeySet {
+ public:
+  StaticKeySet(const std::vector<PublicKey>& keys, const std::vector<int>& devices) : keys_(keys), eng_(devices) {
+    eng_.load(keys_);
+    for (const auto& k : keys_) fam_.push_back(key_family(k));
+  }
+  std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, std::vector<TokenInfo>* info) override {
+    std::lock_guard<std::mutex> g(mu_);
+    Verified V;
+    gpu_verify(eng_, tokens, &V, [&](const Tok& t, std::vector<uint16_t>& out) {
+      // staticKeySet: every key in order (jwt/keyset.go:162-168); a key of
+      // another family fails newVerifier/verifyPayload without arithmetic (R10)
+      const int fam = alg_key_kind(t.alg);
+      for (size_t k = 0; k < keys_.size(); ++k)
+        if (fam_[k] == fam) out.push_back((uint16_t)k);
+    });
+    std::vector<Result> res(tokens.size());
+    parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        const Tok& t = V.toks[i];
+        Result& r = res[i];
+        if (!t.info.parsed) { r.err = t.info.parse_err; continue; }     // jwt.ParseSigned error
+        std::string jerr;
+        // parsedJWT.Claims(key, &allClaims): verify, then unmarshal; a JSON
+        // error moves on to the next key, so it ends as "no known key"
+        if (V.any[i] && claims_map(t.payload, &r.claims, &jerr)) {
+          r.ok = true;
+        } else {
+          r.claims = json::Value();
+          r.err = "no known key successfully validated the token signature";
+        }
+      }
+    });
+    if (info) {
+      info->resize(tokens.size());
+      for (size_t i = 0; i < tokens.size(); ++i) (*info)[i] = std::move(V.toks[i].info);
+    }
+    return res;
+  }
+
+ private:
+  std::vector<PublicKey> keys_;
+  std::vector<int> fam_;
+  Engine eng_;
+  std::mutex mu_;
+};
+
+// ---------------------------------------------------------------- JWKS key set (go-oidc v2.2.1 remoteKeySet)
+bool ca_pem_ok(const std::string& pem) {
+  // x509.CertPool.AppendCertsFromPEM: true iff at least one CERTIFICATE block parses
+  std::string_view rest = pem;
+  bool any = false;
+  while (true) {
+    const size_t b = rest.find("-----BEGIN CERTIFICATE-----");
+    if (b == std::string_view::npos) break;
+    const size_t e = rest.find("-----END CERTIFICATE-----", b);
+    if (e == std::string_view::npos) break;
+    const std::string_view block = rest.substr(b, e + 25 - b);
+    std::string body;
+    const size_t hs = block.find('\n');
+    for (char c : block.substr(hs == std::string_view::npos ? 0 : hs, block.size() - 25 - (hs == std::string_view::npos ? 0 : hs)))
+      if (c != ' ' && c != '\t' && c != '\r' && c != '\n') body.push_back(c);
+    std::string der, err;
+    PublicKey pk;
+    if (b64std_decode(body, &der) && parse_certificate_public_key(der, &pk, &err)) any = true;
+    rest = rest.substr(e + 25);
+  }
+  return any;
+}
+
+class JSONWebKeySet final : public KeySet {
+ public:
+  JSONWebKeySet(std::string url, std::string ca, Fetcher f, const std::vector<int>& devices)
+      : url_(std::move(url)), ca_(std::move(ca)), fetch_(std::move(f)), eng_(devices) {}
+
+  std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, std::vector<TokenInfo>* info) override {
+    std::lock_guard<std::mutex> g(mu_);
+    Verified V;
+    auto cand = [&](const Tok& t, std::vector<uint16_t>& out) {
+      // remoteKeySet.verify: keyID == "" || key.KeyID == keyID   [R31, R34]
+      const int fam = alg_key_kind(t.alg);
+      for (size_t k = 0; k < keys_.size(); ++k)
+        if ((t.kid.empty() || keys_[k].kid == t.kid) && fam_[k] == fam) out.push_back((uint16_t)k);
+    };
+    std::vector<Result> res(tokens.size());
+    if (have_keys_) {
+      gpu_verify(eng_, tokens, &V, cand);
+    } else {
+      gpu_verify(eng_, tokens, &V, [](const Tok&, std::vector<uint16_t>&) {});
+    }
+    // tokens that parsed but did not verify: refresh once if the cache has
+    // expired (now + keysExpiryDelta(30s) after expiry), then retry them
+    std::vector<size_t> miss;
+    for (size_t i = 0; i < tokens.size(); ++i)
+      if (V.toks[i].info.parsed && !V.any[i]) miss.push_back(i);
+    std::string fetch_err;
+    bool refreshed = false;
+    if (!miss.empty() && (!have_keys_ || wall_now_ns() + 30 * kSecond > expiry_ns_)) {
+      refreshed = true;
+      if (refresh(&fetch_err)) gpu_verify(eng_, tokens, &V, cand, &miss);
+    }
+    parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        const Tok& t = V.toks[i];
+        Result& r = res[i];
+        if (!t.info.parsed) { r.err = "oidc: malformed jwt: " + t.info.parse_err; continue; }
+        if (!V.any[i]) {
+          r.err = refreshed && !fetch_err.empty() ? "fetching keys " + fetch_err
+                                                  : "failed to verify id token signature";
+          continue;
+        }
+        std::string jerr;       // jsonWebKeySet.VerifySignature: json.Unmarshal(payload)
+        if (claims_map(t.payload, &r.claims, &jerr)) r.ok = true;
+        else { r.claims = json::Value(); r.err = jerr; }
+      }
+    });
+    if (info) {
+      info->resize(tokens.size());
+      for (size_t i = 0; i < tokens.size(); ++i) (*info)[i] = std::move(V.toks[i].info);
+    }
+    return res;
+  }
+
+ private:
+  bool refresh(std::string* err) {
+    // go-oidc updateKeys
+    FetchResponse resp;
+    try {
+      resp = fetch_(url_, ca_);
+    } catch (const std::exception& e) {
+      *err = std::string("oidc: get keys failed ") + e.what();
+      return false;
+    }
+    if (resp.status != 200) {
+      *err = "oidc: get keys failed: " + resp.status_text + " " + resp.body;
+      return false;
+    }
+    std::vector<JSONWebKey> keys;
+    std::string derr;
+    if (!jwks_decode(resp.body, &keys, &derr)) {
+      *err = "oidc: failed to decode keys: " + derr + " " + resp.body;
+      return false;
+    }
+    if (keys.size() > 65535) { *err = "oidc: too many keys"; return false; }
+    std::vector<PublicKey> pk;
+    fam_.clear();
+    for (const auto& k : keys) {
+      pk.push_back(k.key);
+      fam_.push_back(key_family(k.key));
+    }
+    eng_.load(pk);
+    keys_ = std::move(keys);
+    have_keys_ = true;
+    expiry_ns_ = wall_now_ns() + (resp.max_age_s > 0 ? resp.max_age_s * kSecond : 0);
+    return true;
+  }
+
+  std::string url_, ca_;
+  Fetcher fetch_;
+  Engine eng_;
+  std::mutex mu_;
+  std::vector<JSONWebKey> keys_;
+  std::vector<int> fam_;
+  bool have_keys_ = false;
+  int64_t expiry_ns_ = 0;
+};
+
+// ---------------------------------------------------------------- Go time arithmetic
+constexpr int64_t kUnixToInternal = 62135596800LL;   // time.unixToInternal
+struct GoTime {
+  int64_t sec;     // seconds since year 1 (Time.ext without monotonic)
+  int64_t nsec;    // [0, 1e9)
+};
+GoTime go_now(int64_t unix_ns) {
+  int64_t s = unix_ns / kSecond, ns = unix_ns % kSecond;
+  if (ns < 0) { ns += kSecond; --s; }
+  return {s + kUnixToInternal, ns};
+}
+GoTime go_add(GoTime t, int64_t d) {                  // Time.Add
+  int64_t dsec = d / kSecond;
+  int64_t nsec = t.nsec + d % kSecond;
+  if (nsec >= kSecond) { ++dsec; nsec -= kSecond; }
+  else if (nsec < 0) { --dsec; nsec += kSecond; }
+  const int64_t sum = (int64_t)((uint64_t)t.sec + (uint64_t)dsec);
+  if ((sum > t.sec) == (dsec > 0)) t.sec = sum;
+  else if (dsec > 0) t.sec = INT64_MAX;
+  else t.sec = -INT64_MAX;
+  t.nsec = nsec;
+  return t;
+}
+GoTime go_unix(int64_t sec) { return {(int64_t)((uint64_t)sec + (uint64_t)kUnixToInternal), 0}; }   // time.Unix(sec, 0)
+bool go_before(GoTime a, GoTime b) { return a.sec < b.sec || (a.sec == b.sec && a.nsec < b.nsec); }
+bool go_after(GoTime a, GoTime b) { return a.sec > b.sec || (a.sec == b.sec && a.nsec > b.nsec); }
+
+double dur_seconds(int64_t d) {                       // time.Duration.Seconds
+  const int64_t s = d / kSecond, ns = d % kSecond;
+  return (double)s + (double)ns / 1e9;
+}
+int64_t go_f64_to_i64(double f) {                     // int64(f) on amd64 (CVTTSD2SQ)
+  if (std::isnan(f) || f >= 9223372036854775808.0 || f < -9223372036854775808.0) return INT64_MIN;
+  return (int64_t)f;
+}
+
+// encoding/json field matching: fold(key) == fold(field name) (Go 1.21 foldName)
+bool fold_eq(const std::string& key, const char* upper_field) {
+  const unsigned char* p = (const unsigned char*)key.data();
+  size_t i = 0, j = 0;
+  const size_t n = key.size(), m = std::strlen(upper_field);
+  while (i < n) {
+    if (j >= m) return false;
+    uint32_t r;
+    size_t w;
+    r = json::decode_rune(p + i, n - i, &w);
+    if (r >= 'a' && r <= 'z') r -= 32;
+    else if (r == 0x17F) r = 'S';          // LATIN SMALL LETTER LONG S folds to S
+    else if (r == 0x212A) r = 'K';         // KELVIN SIGN folds to K
+    if (r != (unsigned char)upper_field[j]) return false;
+    i += w;
+    ++j;
+  }
+  return j == m;
+}
+
+}  // namespace
+
+// ====================================================================== Engine
+Engine::Engine(const std::vector<int>& devices) {
+  ctx_ = jg_create(devices.empty() ? nullptr : devices.data(), (int)devices.size());
+  if (!ctx_) throw std::runtime_error(std::string("capjwt: no GPU verifier: ") + jg_last_error(nullptr));
+  threads_ = host_threads();
+}
+
+Engine::~Engine() {
+  if (pinned_) jg_host_free(pinned_);
+  if (ctx_) jg_destroy(ctx_);
+}
+
+void Engine::load(const std::vector<PublicKey>& keys) {
+  std::vector<jg_key> jk;
+  jk.reserve(keys.size());
+  for (const auto& k : keys) jk.push_back(to_jg(k));
+  if (jg_keys_load(ctx_, jk.data(), (int)jk.size()) != 0)
+    throw std::runtime_error(std::string("capjwt: jg_keys_load: ") + jg_last_error(ctx_));
+}
+
+uint8_t* Engine::arena_buffer(size_t bytes) {
+  if (bytes > pinned_cap_) {
+    if (pinned_) jg_host_free(pinned_);
+    pinned_cap_ = std::max(bytes, pinned_cap_ * 3 / 2);
+    pinned_ = (uint8_t*)jg_host_alloc(pinned_cap_);
+    if (!pinned_) throw std::runtime_error("capjwt: pinned host allocation failed");
+  }
+  return pinned_;
+}
+
+void Engine::verify(const uint8_t* arena, size_t arena_len, const void* jobs, size_t njobs, uint8_t* verdicts) {
+  std::lock_guard<std::mutex> g(mu_);
+  const int rc = jg_verify_batch(ctx_, arena, arena_len, (const jg_tok*)jobs, njobs, verdicts);
+  if (rc != 0) throw std::runtime_error(std::string("capjwt: jg_verify_batch: ") + jg_last_error(ctx_));
+}
+
+// ====================================================================== KeySet
+Result KeySet::VerifySignature(std::string_view token) {
+  return verify_batch({token}, nullptr)[0];
+}
+
+std::vector<Result> KeySet::VerifySignatureBatch(const std::vector<std::string_view>& tokens) {
+  return verify_batch(tokens, nullptr);
+}
+
+std::unique_ptr<KeySet> NewStaticKeySet(const std::vector<PublicKey>& keys, std::string* err,
+                                        const std::vector<int>& devices) {
+  if (keys.empty()) { *err = "publicKeys must not be empty"; return nullptr; }
+  if (keys.size() > 65535) { *err = "at most 65535 keys"; return nullptr; }
+  return std::make_unique<StaticKeySet>(keys, devices);
+}
+
+std::unique_ptr<KeySet> NewJSONWebKeySet(const std::string& jwks_url, const std::string& jwks_ca_pem, Fetcher fetch,
+                                         std::string* err, const std::vector<int>& devices) {
+  if (jwks_url.empty()) { *err = "jwksURL must not be empty"; return nullptr; }
+  if (!jwks_ca_pem.empty() && !ca_pem_ok(jwks_ca_pem)) { *err = "could not parse CA PEM value successfully"; return nullptr; }
+  return std::make_unique<JSONWebKeySet>(jwks_url, jwks_ca_pem, std::move(fetch), devices);
+}
+
+std::unique_ptr<KeySet> NewOIDCDiscoveryKeySet(const std::string& issuer, const std::string& issuer_ca_pem,
+                                               Fetcher fetch, std::string* err, const std::vector<int>& devices) {
+  // jwt/keyset.go:49-104
+  if (issuer.empty()) { *err = "issuer must not be empty"; return nullptr; }
+  if (!issuer_ca_pem.empty() && !ca_pem_ok(issuer_ca_pem)) { *err = "could not parse CA PEM value successfully"; return nullptr; }
+  std::string base = issuer;
+  if (!base.empty() && base.back() == '/') base.pop_back();          // strings.TrimSuffix(issuer, "/")
+  FetchResponse resp;
+  try {
+    resp = fetch(base + "/.well-known/openid-configuration", issuer_ca_pem);
+  } catch (const std::exception& e) {
+    *err = e.what();
+    return nullptr;
+  }
+  if (resp.status != 200) { *err = resp.status_text + ": " + resp.body; return nullptr; }
+  json::Value doc;
+  std::string jerr;
+  std::string iss, jwks;
+  bool ok = json::parse(resp.body, &doc, &jerr);
+  if (ok && !doc.is_null() && doc.kind != json::Value::Object) { ok = false; jerr = "json: cannot unmarshal into struct"; }
+  if (ok && doc.kind == json::Value::Object) {
+    // encoding/json into struct { Issuer `json:"issuer"`; JWKSURL `json:"jwks_uri"` }
+    for (const auto& m : doc.obj) {
+      std::string* dst = fold_eq(m.first, "ISSUER") ? &iss : fold_eq(m.first, "JWKS_URI") ? &jwks : nullptr;
+      if (!dst || m.second.is_null()) continue;
+      if (m.second.kind != json::Value::String) { ok = false; jerr = "json: cannot unmarshal into string"; break; }
+      *dst = m.second.str;
+    }
+  }
+  if (!ok) {
+    // unmarshalResp (jwt/keyset.go:229-241)
+    std::string media = resp.content_type.substr(0, resp.content_type.find(';'));
+    while (!media.empty() && media.back() == ' ') media.pop_back();
+    for (auto& c : media) c = (char)std::tolower((unsigned char)c);
+    if (media == "application/json")
+      *err = "failed to decode OIDC discovery document: got Content-Type = application/json, but could not unmarshal as JSON: " + jerr;
+    else
+      *err = "failed to decode OIDC discovery document: expected Content-Type = application/json, got \"" +
+             resp.content_type + "\": " + jerr;
+    return nullptr;
+  }
+  if (iss != issuer) {
+    *err = "issuer did not match the returned issuer, expected \"" + issuer + "\" got \"" + iss + "\"";
+    return nullptr;
+  }
+  return std::make_unique<JSONWebKeySet>(jwks, issuer_ca_pem, std::move(fetch), devices);
+}
+
+bool ParsePublicKeyPEM(std::string_view data, PublicKey* out, std::string* err) {
+  return parse_public_key_pem(data, out, err);
+}
+
+// ====================================================================== Validator
+std::unique_ptr<Validator> NewValidator(KeySet* ks, std::string* err) {
+  if (!ks) { *err = "keySet must not be nil"; return nullptr; }
+  return std::make_unique<Validator>(ks);
+}
+
+Result validate_claims(const json::Value& all_claims, const TokenInfo& info, const Expected& expected,
+                       int64_t now_unix_ns) {
+  Result r;
+  // validateSigningAlgorithm (jwt/jwt.go:207-239)  [R36]
+  {
+    std::string e = SupportedSigningAlgorithm(expected.SigningAlgorithms);
+    if (e.empty() && !info.parsed) e = info.parse_err;
+    if (e.empty() && (info.nsigs == 0 || (info.nsigs == 1 && info.sig0_len == 0))) e = "token must be signed";
+    if (e.empty() && info.nsigs > 1) e = "token with multiple signatures not supported";
+    if (e.empty()) {
+      bool found = false;
+      if (expected.SigningAlgorithms.empty()) found = info.alg == "RS256";
+      for (const auto& a : expected.SigningAlgorithms) found = found || a == info.alg;
+      if (!found) e = "token signed with unexpected algorithm";
+    }
+    if (!e.empty()) {
+      r.err = "invalid algorithm (alg) header parameter: " + e;
+      return r;
+    }
+  }
+  // json.Marshal(allClaims) -> json.Unmarshal(&jwt.Claims{})  [R37]: members in
+  // sorted key order, each assigned to the case-insensitively matching field
+  std::string iss, sub, jti;
+  std::vector<std::string> aud;
+  bool has_iat = false, has_exp = false, has_nbf = false;
+  int64_t iat = 0, exp = 0, nbf = 0;
+  if (all_claims.kind == json::Value::Object) {
+    std::vector<const json::Member*> ms;
+    for (const auto& m : all_claims.obj) ms.push_back(&m);
+    std::sort(ms.begin(), ms.end(), [](const json::Member* a, const json::Member* b) { return a->first < b->first; });
+    for (const json::Member* m : ms) {
+      const json::Value& v = m->second;
+      std::string* sfield = fold_eq(m->first, "ISS") ? &iss : fold_eq(m->first, "SUB") ? &sub
+                            : fold_eq(m->first, "JTI") ? &jti : nullptr;
+      if (sfield) {
+        if (v.is_null()) continue;
+        if (v.kind != json::Value::String) {
+          r.err = "json: cannot unmarshal into Go struct field Claims." + m->first + " of type string";
+          return r;
+        }
+        *sfield = v.str;
+        continue;
+      }
+      if (fold_eq(m->first, "AUD")) {
+        // jwt.Audience.UnmarshalJSON: string or array of strings; null included
+        if (v.kind == json::Value::String) {
+          aud.assign(1, v.str);
+          continue;
+        }
+        bool ok = v.kind == json::Value::Array;
+        std::vector<std::string> a;
+        if (ok)
+          for (const auto& e : v.arr) {
+            if (e.kind != json::Value::String) { ok = false; break; }
+            a.push_back(e.str);
+          }
+        if (!ok) {
+          r.err = "square/go-jose/jwt: expected string or array value to unmarshal to Audience";
+          return r;
+        }
+        aud = std::move(a);
+        continue;
+      }
+      bool* has = fold_eq(m->first, "EXP") ? &has_exp : fold_eq(m->first, "NBF") ? &has_nbf
+                  : fold_eq(m->first, "IAT") ? &has_iat : nullptr;
+      if (has) {
+        int64_t* dst = has == &has_exp ? &exp : has == &has_nbf ? &nbf : &iat;
+        if (v.is_null()) { *has = false; *dst = 0; continue; }       // *NumericDate = nil
+        if (v.kind != json::Value::Number) {
+          r.err = "square/go-jose/jwt: expected number value to unmarshal NumericDate";
+          return r;
+        }
+        *has = true;
+        *dst = go_f64_to_i64(v.num);                                 // NumericDate(f)
+      }
+    }
+  }
+  // time defaulting (jwt/jwt.go:117-170)  [R38]
+  if (!has_iat) iat = 0;
+  if (!has_exp) exp = 0;
+  if (!has_nbf) nbf = 0;
+  if (iat == 0 && exp == 0 && nbf == 0) {
+    r.err = "no issued at (iat), not before (nbf), or expiration time (exp) claims in token";
+    return r;
+  }
+  if (exp == 0) {
+    const int64_t latest = nbf > iat ? nbf : iat;
+    double lw = dur_seconds(expected.ExpirationLeeway);
+    if (lw < 0) lw = 0;
+    else if (lw == 0) lw = DefaultLeewaySeconds;
+    exp = (int64_t)((uint64_t)latest + (uint64_t)go_f64_to_i64(lw));
+  }
+  if (nbf == 0) {
+    if (iat != 0) {
+      nbf = iat;
+    } else {
+      double lw = dur_seconds(expected.NotBeforeLeeway);
+      if (lw < 0) lw = 0;
+      else if (lw == 0) lw = DefaultLeewaySeconds;
+      nbf = (int64_t)((uint64_t)exp - (uint64_t)go_f64_to_i64(lw));
+    }
+  }
+  int64_t cks = expected.ClockSkewLeeway;
+  if (dur_seconds(cks) < 0) cks = 0;
+  else if (dur_seconds(cks) == 0) cks = 60 * kSecond;           // jwt.DefaultLeeway = 1 minute
+  // registered claims (jwt/jwt.go:172-184)  [R39]
+  if (!expected.Issuer.empty() && expected.Issuer != iss) { r.err = "invalid issuer (iss) claim"; return r; }
+  if (!expected.Subject.empty() && expected.Subject != sub) { r.err = "invalid subject (sub) claim"; return r; }
+  if (!expected.ID.empty() && expected.ID != jti) { r.err = "invalid ID (jti) claim"; return r; }
+  if (!expected.Audiences.empty()) {
+    bool found = false;
+    for (const auto& e : expected.Audiences)
+      for (const auto& a : aud) found = found || a == e;
+    if (!found) {
+      r.err = "invalid audience (aud) claim: audience claim does not match any expected audience";
+      return r;
+    }
+  }
+  // time window (jwt/jwt.go:186-199)
+  const GoTime now = go_now(now_unix_ns);
+  if (go_before(go_add(now, cks), go_unix(nbf))) { r.err = "invalid not before (nbf) claim: token not yet valid"; return r; }
+  if (go_after(go_add(now, -cks), go_unix(exp))) { r.err = "invalid expiration time (exp) claim: token is expired"; return r; }
+  if (go_before(go_add(now, cks), go_unix(iat))) { r.err = "invalid issued at (iat) claim: token issued in the future"; return r; }
+  r.ok = true;                 // the caller attaches all_claims (returned unchanged)
+  return r;
+}
+
+Result Validator::Validate(std::string_view token, const Expected& expected) {
+  return ValidateBatch({token}, expected)[0];
+}
+
+std::vector<Result> Validator::ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected) {
+  std::vector<TokenInfo> info;
+  std::vector<Result> sig = ks_->verify_batch(tokens, &info);
+  const int64_t now = expected.has_now ? expected.now_unix_ns : wall_now_ns();
+  std::vector<Result> out(tokens.size());
+  parallel_for(tokens.size(), host_threads(), [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      if (!sig[i].ok) {
+        out[i].err = "error verifying token signature: " + sig[i].err;
+        continue;
+      }
+      out[i] = validate_claims(sig[i].claims, info[i], expected, now);
+      if (out[i].ok) out[i].claims = std::move(sig[i].claims);
+    }
+  });
+  return out;
+}
+
+}  // namespace capjwt

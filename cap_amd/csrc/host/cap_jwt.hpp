@@ -1,0 +1,151 @@
+// cap_jwt.hpp -- C++ mirror of cap's jwt package API (jwt/keyset.go, jwt/jwt.go,
+// jwt/algs.go) on top of the GPU verifier's C ABI (include/jg.h).
+//
+// Go is absent from this image, so this layer stands where the Go host code of
+// BASELINE.json's north star would: it keeps base64url/JSON header parsing,
+// kid -> key lookup and claims validation on the host and hands every
+// signature check to libcapjwt.so in one batch.  Names, argument meaning and
+// error strings follow the reference:
+//
+//   Go (reference)                                   here
+//   KeySet.VerifySignature    jwt/keyset.go:27-32     KeySet::VerifySignature / VerifySignatureBatch
+//   NewStaticKeySet           jwt/keyset.go:142-150   NewStaticKeySet
+//   NewJSONWebKeySet          jwt/keyset.go:109-123   NewJSONWebKeySet (HTTP GET via a Fetcher)
+//   NewOIDCDiscoveryKeySet    jwt/keyset.go:49-104    NewOIDCDiscoveryKeySet
+//   ParsePublicKeyPEM         jwt/keyset.go:178-200   ParsePublicKeyPEM
+//   NewValidator / Validate   jwt/jwt.go:25-202       NewValidator / Validator::Validate
+//   (north star) ValidateBatch                        Validator::ValidateBatch
+//   SupportedSigningAlgorithm jwt/algs.go:38-46       SupportedSigningAlgorithm
+//
+// There is no CPU verification path: a KeySet whose GPU context cannot be
+// created fails at construction.
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "jose.hpp"
+#include "json.hpp"
+
+struct jg_ctx;
+
+namespace capjwt {
+
+// ---------------------------------------------------------------- algs (jwt/algs.go)
+extern const char* const kSupportedAlgorithms[10];
+// "" if every alg is supported, else `unsupported signing algorithm "X"`
+std::string SupportedSigningAlgorithm(const std::vector<std::string>& algs);
+
+// ---------------------------------------------------------------- results
+// (claims, error): ok == true <=> Go's err == nil.  claims is the
+// map[string]interface{} (Object) or nil (Null, for a `null` payload).
+struct Result {
+  bool ok = false;
+  json::Value claims;
+  std::string err;
+};
+
+// ---------------------------------------------------------------- HTTP
+// The JWKS / discovery GET.  The reference uses net/http with a TLS client
+// built from the CA PEM (createCAContext, jwt/keyset.go:204-227); here the
+// caller supplies the transport.  Throw std::runtime_error for a transport
+// error (Go: client.Do error).
+struct FetchResponse {
+  int status = 200;
+  std::string status_text = "200 OK";   // resp.Status
+  std::string body;
+  std::string content_type = "application/json";
+  int64_t max_age_s = -1;               // Cache-Control max-age; -1 = none (go-oidc: expire at once)
+};
+using Fetcher = std::function<FetchResponse(const std::string& url, const std::string& ca_pem)>;
+
+// ---------------------------------------------------------------- GPU engine
+// One jg_ctx (HIP devices + staged key table) and the host buffers of a batch.
+class Engine {
+ public:
+  explicit Engine(const std::vector<int>& devices);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+  void load(const std::vector<PublicKey>& keys);      // jg_keys_load
+  // verify (arena entry, key, alg) jobs; verdicts[i] = 1 accept, 0 reject
+  void verify(const uint8_t* arena, size_t arena_len, const void* jobs, size_t njobs, uint8_t* verdicts);
+  uint8_t* arena_buffer(size_t bytes);                 // pinned, grow-only
+  int threads() const { return threads_; }
+ private:
+  jg_ctx* ctx_ = nullptr;
+  uint8_t* pinned_ = nullptr;
+  size_t pinned_cap_ = 0;
+  int threads_ = 1;
+  std::mutex mu_;
+};
+
+// ---------------------------------------------------------------- KeySet
+struct TokenInfo {          // what validateSigningAlgorithm needs from ParseSigned
+  bool parsed = false;
+  std::string parse_err;
+  size_t nsigs = 0;
+  size_t sig0_len = 0;
+  std::string alg;
+};
+
+class KeySet {
+ public:
+  virtual ~KeySet() = default;
+  // jwt/keyset.go:27-32
+  Result VerifySignature(std::string_view token);
+  std::vector<Result> VerifySignatureBatch(const std::vector<std::string_view>& tokens);
+  // batch verify that also returns what the parse learned (Validator reuses it)
+  virtual std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens,
+                                           std::vector<TokenInfo>* info) = 0;
+};
+
+std::unique_ptr<KeySet> NewStaticKeySet(const std::vector<PublicKey>& keys, std::string* err,
+                                        const std::vector<int>& devices = {});
+std::unique_ptr<KeySet> NewJSONWebKeySet(const std::string& jwks_url, const std::string& jwks_ca_pem, Fetcher fetch,
+                                         std::string* err, const std::vector<int>& devices = {});
+std::unique_ptr<KeySet> NewOIDCDiscoveryKeySet(const std::string& issuer, const std::string& issuer_ca_pem,
+                                               Fetcher fetch, std::string* err, const std::vector<int>& devices = {});
+
+// ---------------------------------------------------------------- Validator
+constexpr int64_t kSecond = 1000000000LL;
+constexpr int64_t DefaultLeewaySeconds = 150;          // jwt/jwt.go:16
+
+struct Expected {                                      // jwt/jwt.go:38-83
+  std::string Issuer, Subject, ID;
+  std::vector<std::string> Audiences;
+  std::vector<std::string> SigningAlgorithms;
+  int64_t NotBeforeLeeway = 0;                         // time.Duration (ns)
+  int64_t ExpirationLeeway = 0;
+  int64_t ClockSkewLeeway = 0;
+  bool has_now = false;                                // Now == nil -> time.Now()
+  int64_t now_unix_ns = 0;
+};
+
+class Validator {
+ public:
+  explicit Validator(KeySet* ks) : ks_(ks) {}
+  Result Validate(std::string_view token, const Expected& expected);
+  std::vector<Result> ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected);
+ private:
+  KeySet* ks_;
+};
+// nil keySet -> error "keySet must not be nil"
+std::unique_ptr<Validator> NewValidator(KeySet* ks, std::string* err);
+
+// The claim checks of Validate after the signature (jwt/jwt.go:103-201), on a
+// verified claims map and the token's parse info.  Exposed for tests.
+Result validate_claims(const json::Value& all_claims, const TokenInfo& info, const Expected& expected,
+                       int64_t now_unix_ns);
+
+bool ParsePublicKeyPEM(std::string_view data, PublicKey* out, std::string* err);
+
+// Host threads used by batch parsing / claims (CAPJWT_HOST_THREADS, default
+// min(hardware threads, 16)).
+int host_threads();
+
+}  // namespace capjwt

@@ -1,0 +1,344 @@
+// py_capjwt.cpp -- Python binding of the C++ cap jwt mirror (cap_jwt.hpp), so
+// the parity tests can drive KeySet / Validator the way the reference's Go
+// tests do (jwt/keyset_test.go, jwt/jwt_test.go).  Values cross as Go would
+// hand them out: claims map -> dict with float64 numbers; error -> str or None.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "cap_jwt.hpp"
+
+namespace py = pybind11;
+using namespace capjwt;
+
+namespace {
+
+py::object to_py(const json::Value& v) {
+  switch (v.kind) {
+    case json::Value::Null: return py::none();
+    case json::Value::Bool: return py::bool_(v.b);
+    case json::Value::Number: return py::float_(v.num);
+    case json::Value::String: return py::str(v.str);
+    case json::Value::Array: {
+      py::list l;
+      for (const auto& e : v.arr) l.append(to_py(e));
+      return std::move(l);
+    }
+    case json::Value::Object: {
+      py::dict d;
+      for (const auto& m : v.obj) d[py::str(m.first)] = to_py(m.second);
+      return std::move(d);
+    }
+  }
+  return py::none();
+}
+
+py::tuple result_py(const Result& r) {
+  if (r.ok) return py::make_tuple(to_py(r.claims), py::none());
+  return py::make_tuple(py::none(), py::str(r.err));
+}
+
+py::list results_py(const std::vector<Result>& rs) {
+  py::list l;
+  for (const auto& r : rs) l.append(result_py(r));
+  return l;
+}
+
+std::vector<std::string> as_strings(const py::sequence& toks) {
+  std::vector<std::string> v;
+  v.reserve(py::len(toks));
+  for (auto t : toks) {
+    if (py::isinstance<py::bytes>(t)) v.push_back(t.cast<std::string>());
+    else v.push_back(t.cast<std::string>());
+  }
+  return v;
+}
+
+std::vector<std::string_view> views(const std::vector<std::string>& s) {
+  return std::vector<std::string_view>(s.begin(), s.end());
+}
+
+// newline-separated token blob -> views (end-to-end benchmark input, no
+// per-token Python objects)
+std::vector<std::string_view> split_lines(const std::string& blob) {
+  std::vector<std::string_view> v;
+  size_t s = 0;
+  for (size_t i = 0; i <= blob.size(); ++i)
+    if (i == blob.size() || blob[i] == '\n') {
+      if (i > s) v.emplace_back(blob.data() + s, i - s);
+      s = i + 1;
+    }
+  return v;
+}
+
+Fetcher wrap_fetch(py::object fn) {
+  // fn(url, ca_pem) -> dict(status=, status_text=, body=, content_type=, max_age=); raise = transport error
+  auto holder = std::make_shared<py::object>(std::move(fn));
+  return [holder](const std::string& url, const std::string& ca) -> FetchResponse {
+    py::gil_scoped_acquire g;
+    FetchResponse r;
+    py::object res;
+    try {
+      res = (*holder)(url, ca);
+    } catch (py::error_already_set& e) {
+      throw std::runtime_error(std::string("Get \"") + url + "\": " + e.what());
+    }
+    py::dict d = res.cast<py::dict>();
+    if (d.contains("status")) r.status = d["status"].cast<int>();
+    r.status_text = d.contains("status_text") ? d["status_text"].cast<std::string>()
+                                              : std::to_string(r.status) + (r.status == 200 ? " OK" : "");
+    if (d.contains("body")) {
+      py::object b = d["body"];
+      r.body = py::isinstance<py::bytes>(b) ? b.cast<std::string>() : b.cast<std::string>();
+    }
+    if (d.contains("content_type")) r.content_type = d["content_type"].cast<std::string>();
+    if (d.contains("max_age")) r.max_age_s = d["max_age"].cast<int64_t>();
+    return r;
+  };
+}
+
+struct PyKeySet {
+  std::shared_ptr<KeySet> ks;
+};
+
+PyKeySet must(std::unique_ptr<KeySet> p, const std::string& err) {
+  if (!p) throw py::value_error(err);
+  return PyKeySet{std::shared_ptr<KeySet>(std::move(p))};
+}
+
+py::dict key_dict(const PublicKey& k) {
+  py::dict d;
+  static const char* kinds[] = {"none", "RSA", "EC", "Ed25519", "oct"};
+  d["kind"] = kinds[k.kind];
+  if (k.kind == PublicKey::RSA) {
+    d["n"] = py::bytes(k.n);
+    d["e"] = k.e;
+  } else if (k.kind == PublicKey::EC) {
+    static const char* crv[] = {"", "P-256", "P-384", "P-521"};
+    d["crv"] = crv[k.curve];
+    d["x"] = py::bytes(k.x);
+    d["y"] = py::bytes(k.y);
+  } else if (k.kind == PublicKey::Ed25519) {
+    d["x"] = py::bytes(k.x);
+  } else if (k.kind == PublicKey::Symmetric) {
+    d["k"] = py::bytes(k.k);
+  }
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_capjwt_host, m) {
+  m.doc() = "C++ host mirror of cap's jwt package over the MI355X verifier (libcapjwt.so)";
+
+  py::class_<PublicKey>(m, "PublicKey")
+      .def_static("rsa", [](py::bytes n, uint64_t e) {
+        PublicKey k;
+        k.kind = PublicKey::RSA;
+        std::string s = n;
+        size_t i = 0;
+        while (i < s.size() && s[i] == 0) ++i;
+        k.n = s.substr(i);
+        k.e = e;
+        return k;
+      })
+      .def_static("ec", [](const std::string& crv, py::bytes x, py::bytes y) {
+        PublicKey k;
+        k.kind = PublicKey::EC;
+        k.curve = crv == "P-256" ? 1 : crv == "P-384" ? 2 : crv == "P-521" ? 3 : 0;
+        if (!k.curve) throw py::value_error("unsupported curve " + crv);
+        k.x = x;
+        k.y = y;
+        return k;
+      })
+      .def_static("ed25519", [](py::bytes pub) {
+        PublicKey k;
+        k.kind = PublicKey::Ed25519;
+        k.x = pub;
+        return k;
+      })
+      .def_static("symmetric", [](py::bytes secret) {
+        PublicKey k;
+        k.kind = PublicKey::Symmetric;
+        k.k = secret;
+        return k;
+      })
+      .def("as_dict", &key_dict)
+      .def("__eq__", [](const PublicKey& a, const PublicKey& b) { return a == b; });
+
+  py::class_<Expected>(m, "Expected")
+      .def(py::init<>())
+      .def_readwrite("Issuer", &Expected::Issuer)
+      .def_readwrite("Subject", &Expected::Subject)
+      .def_readwrite("ID", &Expected::ID)
+      .def_readwrite("Audiences", &Expected::Audiences)
+      .def_readwrite("SigningAlgorithms", &Expected::SigningAlgorithms)
+      .def_readwrite("NotBeforeLeeway", &Expected::NotBeforeLeeway)
+      .def_readwrite("ExpirationLeeway", &Expected::ExpirationLeeway)
+      .def_readwrite("ClockSkewLeeway", &Expected::ClockSkewLeeway)
+      .def_readwrite("has_now", &Expected::has_now)
+      .def_readwrite("now_unix_ns", &Expected::now_unix_ns);
+
+  // ---- CPU-side pieces (no GPU needed)
+  m.def("supported_signing_algorithm", [](const std::vector<std::string>& algs) -> py::object {
+    const std::string e = SupportedSigningAlgorithm(algs);
+    if (e.empty()) return py::none();
+    return py::str(e);
+  });
+  m.def("json_loads", [](py::bytes b) -> py::tuple {
+    json::Value v;
+    std::string err;
+    std::string s = b;
+    if (!json::parse(s, &v, &err)) return py::make_tuple(py::none(), py::str(err));
+    if (json::has_range_error(v)) return py::make_tuple(py::none(), py::str("number out of range"));
+    return py::make_tuple(to_py(v), py::none());
+  });
+  m.def("b64url_decode", [](const std::string& s) -> py::object {
+    std::string out, err;
+    if (!b64url_decode(s, &out, &err)) return py::none();
+    return py::bytes(out);
+  });
+  m.def("strip_whitespace", [](py::bytes s) { return py::bytes(strip_whitespace(std::string(s))); });
+  m.def("parse_signed", [](py::bytes tok) -> py::dict {
+    JWS j;
+    std::string err;
+    py::dict d;
+    std::string t = tok;
+    if (!parse_signed(t, &j, &err)) {
+      d["error"] = err;
+      return d;
+    }
+    d["error"] = py::none();
+    d["payload"] = py::bytes(j.payload);
+    d["nsigs"] = j.sigs.size();
+    if (!j.sigs.empty()) {
+      d["alg"] = j.sigs[0].alg;
+      d["kid"] = j.sigs[0].kid;
+      d["signature"] = py::bytes(j.sigs[0].signature);
+      d["protected"] = py::bytes(j.sigs[0].protected_raw);
+    }
+    std::string si;
+    if (signing_input(j, &si)) d["signing_input"] = py::bytes(si);
+    else d["signing_input"] = py::none();
+    return d;
+  });
+  m.def("parse_public_key_pem", [](py::bytes pem) {
+    PublicKey k;
+    std::string err;
+    if (!ParsePublicKeyPEM(std::string(pem), &k, &err)) throw py::value_error(err);
+    return k;
+  });
+  m.def("jwks_decode", [](py::bytes doc) {
+    std::vector<JSONWebKey> keys;
+    std::string err;
+    if (!jwks_decode(std::string(doc), &keys, &err)) throw py::value_error(err);
+    py::list l;
+    for (const auto& k : keys) l.append(py::make_tuple(k.kid, k.key));
+    return l;
+  });
+  m.def("ec_on_curve", [](const std::string& crv, py::bytes x, py::bytes y) {
+    const int c = crv == "P-256" ? 1 : crv == "P-384" ? 2 : crv == "P-521" ? 3 : 0;
+    return ec_on_curve(c, std::string(x), std::string(y));
+  });
+  m.def("validate_claims", [](py::bytes payload, const std::string& alg, size_t sig_len, const Expected& exp,
+                              int64_t now_ns) {
+    // the post-signature half of Validate on a payload whose signature verified
+    json::Value v;
+    std::string err;
+    if (!json::parse(std::string(payload), &v, &err)) return py::tuple(py::make_tuple(py::none(), py::str(err)));
+    TokenInfo info;
+    info.parsed = true;
+    info.nsigs = 1;
+    info.sig0_len = sig_len;
+    info.alg = alg;
+    Result r = validate_claims(v, info, exp, now_ns);
+    if (r.ok) r.claims = v;
+    return result_py(r);
+  });
+  m.def("host_threads", &host_threads);
+
+  // ---- GPU-backed key sets and validator
+  py::class_<PyKeySet>(m, "KeySet")
+      .def("verify_signature", [](PyKeySet& s, py::object tok) {
+        std::string t = tok.cast<std::string>();
+        Result r;
+        {
+          py::gil_scoped_release rel;
+          r = s.ks->VerifySignature(t);
+        }
+        return result_py(r);
+      })
+      .def("verify_signature_batch", [](PyKeySet& s, py::sequence toks) {
+        auto v = as_strings(toks);
+        std::vector<Result> rs;
+        {
+          py::gil_scoped_release rel;
+          rs = s.ks->VerifySignatureBatch(views(v));
+        }
+        return results_py(rs);
+      });
+
+  m.def("new_static_keyset", [](const std::vector<PublicKey>& keys, const std::vector<int>& devices) {
+    std::string err;
+    return must(NewStaticKeySet(keys, &err, devices), err);
+  }, py::arg("keys"), py::arg("devices") = std::vector<int>{});
+  m.def("new_json_web_keyset", [](const std::string& url, const std::string& ca, py::object fetch,
+                                  const std::vector<int>& devices) {
+    std::string err;
+    return must(NewJSONWebKeySet(url, ca, wrap_fetch(std::move(fetch)), &err, devices), err);
+  }, py::arg("url"), py::arg("ca_pem"), py::arg("fetch"), py::arg("devices") = std::vector<int>{});
+  m.def("new_oidc_discovery_keyset", [](const std::string& issuer, const std::string& ca, py::object fetch,
+                                        const std::vector<int>& devices) {
+    std::string err;
+    std::unique_ptr<KeySet> ks;
+    {
+      ks = NewOIDCDiscoveryKeySet(issuer, ca, wrap_fetch(std::move(fetch)), &err, devices);
+    }
+    return must(std::move(ks), err);
+  }, py::arg("issuer"), py::arg("ca_pem"), py::arg("fetch"), py::arg("devices") = std::vector<int>{});
+
+  struct PyValidator {
+    std::shared_ptr<KeySet> ks;
+    std::unique_ptr<Validator> v;
+  };
+  py::class_<PyValidator>(m, "Validator")
+      .def(py::init([](PyKeySet* ks) {
+        if (!ks) throw py::value_error("keySet must not be nil");
+        auto p = std::make_unique<PyValidator>();
+        p->ks = ks->ks;
+        p->v = std::make_unique<Validator>(ks->ks.get());
+        return p;
+      }))
+      .def("validate", [](PyValidator& s, py::object tok, const Expected& e) {
+        std::string t = tok.cast<std::string>();
+        Result r;
+        {
+          py::gil_scoped_release rel;
+          r = s.v->Validate(t, e);
+        }
+        return result_py(r);
+      })
+      .def("validate_batch", [](PyValidator& s, py::sequence toks, const Expected& e) {
+        auto v = as_strings(toks);
+        std::vector<Result> rs;
+        {
+          py::gil_scoped_release rel;
+          rs = s.v->ValidateBatch(views(v), e);
+        }
+        return results_py(rs);
+      })
+      .def("validate_blob", [](PyValidator& s, py::bytes blob, const Expected& e) {
+        // end-to-end throughput entry: newline-separated tokens in, per-token
+        // accept bytes out (claims stay on the C++ side)
+        std::string b = blob;
+        std::string ok;
+        {
+          py::gil_scoped_release rel;
+          auto toks = split_lines(b);
+          auto rs = s.v->ValidateBatch(toks, e);
+          ok.resize(rs.size());
+          for (size_t i = 0; i < rs.size(); ++i) ok[i] = rs[i].ok ? 1 : 0;
+        }
+        return py::bytes(ok);
+      });
+}

@@ -56,7 +56,10 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   uint32_t D;
   if ((n & 3u) == 1u) { st = ST_REJECT; D = 0; }
   else D = (n >> 2) * 3u + ((n & 3u) == 2u ? 1u : (n & 3u) == 3u ? 2u : 0u);
-  if (D > 4u * SIGW_ROWS) { st = ST_REJECT; D = 0; }
+  // a signature longer than the rows this class reads cannot have the key's
+  // length (R13/R18/R23); rejecting it here also keeps every write below in
+  // bounds of the zrows x npad scratch the runtime allocated for the batch
+  if (D > 4u * (uint32_t)a.zrows) { st = ST_REJECT; D = 0; }
   const int layout = (CLS == CLS_ED25519) ? LAY_LE : (CLS >= CLS_P256 ? LAY_SPLIT_BE : LAY_BE);
   uint32_t ks = 0;
   if (layout == LAY_SPLIT_BE) {

@@ -28,3 +28,27 @@ def test_golden_vectors(ctx):
         if got != t["verdict"]:
             bad.append((t["name"], got, t["verdict"], t["source"]))
     assert not bad, bad
+
+
+def test_cross_product_every_token_every_key(ctx):
+    """Every golden token against every loaded key in ONE batch (mixed classes,
+    signatures longer than the key, wrong families): each verdict equals the
+    oracle's.  Pins the per-class scratch bounds and the class bucketing."""
+    from oracle import jws
+    keys, toks = H.golden()
+    okeys = [jws.Key.from_fixture(k) for k in keys]
+    from cap_amd import _lib
+    arena = _lib.Arena()
+    want = []
+    for t in toks:
+        p = jws.parse_jws(t["token"])
+        if p is None or not p.crit_ok:
+            continue
+        sig_b64 = jws.b64url_encode(p.signature).encode()
+        for ki, k in enumerate(okeys):
+            arena.add(p.signing_input, sig_b64, p.alg, ki)
+            want.append(int(jws.verify_sig(p, k)))
+    out = ctx.verify(arena)
+    bad = [i for i, w in enumerate(want) if out[i] != w]
+    assert not bad, (len(bad), bad[:20])
+    assert sum(want) > 150
