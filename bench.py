@@ -7,8 +7,11 @@ host) over one batch of synthetic signed tokens already resident in HBM.
 
 Headline workload (BASELINE.json configs[1]): ES256, P-256 JWKS with 4 kids,
 1,048,576 tokens per GPU.  Second half of the metric: RS256 RSA-2048 on the same
-batch size (reported under "rs256").  Tokens are signed by OpenSSL (tools/tokgen)
-from a unique pool replicated to the batch size; verdicts are never cached.
+batch size (reported under "rs256").  The other BASELINE configs are reported
+under "configs" (per-GPU share of each, same timing rules), the end-to-end
+Validator.ValidateBatch rate (host parse + GPU + claims) under "e2e".  Tokens
+are signed by OpenSSL (tools/tokgen) from a unique pool replicated to the batch
+size; verdicts are never cached, and every line checks its accept count.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, weak scaling)
@@ -27,7 +30,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 KEYDIR = os.path.join(ROOT, "tests", "golden", "keys")
+BENCHKEYS = os.path.join(ROOT, "tools", "benchkeys")
 TOKGEN = os.path.join(ROOT, "tools", "tokgen", "tokgen")
+TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 
 # measured v_mad_u64_u32 issue rate, chip-wide (profiles/r01_int_rates.json,
 # 8 waves/SIMD, SGPR operand): the integer multiply-add roofline denominator
@@ -36,6 +41,8 @@ MAD_PEAK_T = 32.27
 JG_TOK = np.dtype([("off", "<u8"), ("sig_in_len", "<u4"), ("sig_rel_off", "<u4"), ("sig_b64_len", "<u4"),
                    ("key_idx", "<u2"), ("alg", "u1"), ("flags", "u1")])
 assert JG_TOK.itemsize == 24
+ALG_IDS = {"RS256": 1, "RS384": 2, "RS512": 3, "PS256": 4, "PS384": 5, "PS512": 6,
+           "ES256": 7, "ES384": 8, "ES512": 9, "EdDSA": 10}
 
 
 # ---------------------------------------------------------------- algorithmic work
@@ -54,11 +61,11 @@ def p256_point_mads_per_token():
     return adds * madd + sqr + 2 * mul
 
 
-def rsa2048_modexp_mads_per_token():
-    """k_rsa_modexp<37,2,8>: R = 2^(28*74); 18 Montgomery products (to-Montgomery,
-    16 squarings, final multiply) of 2 * 74^2 multiply-accumulates each."""
-    L = 74
-    return 18 * 2 * L * L
+def rsa_modexp_mads_per_token(limbs):
+    """k_rsa_modexp: 18 Montgomery products (to-Montgomery, 16 squarings, final
+    multiply) of 2 * L^2 multiply-accumulates each (L 28-bit limbs: 74 for
+    RSA-2048, 148 for RSA-4096)."""
+    return 18 * 2 * limbs * limbs
 
 
 # ---------------------------------------------------------------- inputs
@@ -67,19 +74,24 @@ def ensure_tokgen():
         subprocess.run(["make", "-s", "-C", os.path.dirname(TOKGEN)], check=True)
 
 
-def gen_tokens(alg, count, keys, threads, tag):
+def gen_tokens(alg, count, keypaths, threads, tag, kid_base=0):
     ensure_tokgen()
-    out = os.path.join("/tmp", f"capjwt_{tag}_{alg}_{count}_{os.getpid()}.txt")
-    subprocess.run([TOKGEN, alg, str(count), str(threads), out] + [os.path.join(KEYDIR, k + ".pem") for k in keys],
-                   check=True)
+    out = os.path.join("/tmp", f"capjwt_{tag}_{alg}_{count}_{kid_base}_{os.getpid()}.txt")
+    env = dict(os.environ, TOKGEN_KID_BASE=str(kid_base))
+    subprocess.run([TOKGEN, alg, str(count), str(threads), out] + list(keypaths), check=True, env=env)
     with open(out, "rb") as f:
         toks = f.read().split(b"\n")[:count]
     os.unlink(out)
     return toks
 
 
-def build_arena(pool, alg_id, nkeys, total):
-    """Pack a token pool into (arena bytes, jg_tok array), replicated to `total`."""
+def golden_keypaths(kids):
+    return [os.path.join(KEYDIR, k + ".pem") for k in kids]
+
+
+def pack(pool, algs, keyidx, total):
+    """Pack a unique token pool (with per-token alg id and key index) into
+    (arena bytes, jg_tok array), replicated to `total` jobs."""
     lens = np.fromiter((len(t) for t in pool), dtype=np.int64, count=len(pool))
     dots = np.fromiter((t.rfind(b".") for t in pool), dtype=np.int64, count=len(pool))
     offs = np.zeros(len(pool), dtype=np.int64)
@@ -87,30 +99,47 @@ def build_arena(pool, alg_id, nkeys, total):
     blob = b"".join(pool)
     reps = (total + len(pool) - 1) // len(pool)
     arena = blob * reps
-    toks = np.zeros(reps * len(pool), dtype=JG_TOK)
-    for r in range(reps):
-        sl = slice(r * len(pool), (r + 1) * len(pool))
-        toks["off"][sl] = offs + r * len(blob)
     idx = np.arange(reps * len(pool)) % len(pool)
+    toks = np.zeros(reps * len(pool), dtype=JG_TOK)
+    toks["off"] = offs[idx] + (np.arange(reps * len(pool)) // len(pool)) * len(blob)
     toks["sig_in_len"] = dots[idx]
     toks["sig_rel_off"] = dots[idx] + 1
     toks["sig_b64_len"] = (lens - dots - 1)[idx]
-    toks["key_idx"] = np.arange(reps * len(pool)) % len(pool) % nkeys
-    toks["alg"] = alg_id
+    toks["key_idx"] = np.asarray(keyidx)[idx]
+    toks["alg"] = np.asarray(algs)[idx]
     return arena, toks[:total]
 
 
 def abi_keys(names):
-    from cap_amd import _lib
     from tests import gpu_helpers as H
     keys, _ = H.golden()
     by = {k["kid"]: k for k in keys}
     return [H.abi_key(by[n]) for n in names]
 
 
+def bench_keys():
+    """tools/benchkeys/kids.json -> [(kid, alg, pem path, _lib.Key, jwk)]"""
+    import base64
+    from cap_amd import _lib
+    def d(s):
+        return base64.urlsafe_b64decode(s + "=" * (-len(s) % 4))
+    out = []
+    for k in json.load(open(os.path.join(BENCHKEYS, "kids.json"))):
+        j = k["jwk"]
+        if j["kty"] == "RSA":
+            key = _lib.Key.rsa(d(j["n"]), int.from_bytes(d(j["e"]), "big"))
+        elif j["kty"] == "EC":
+            key = _lib.Key.ec(j["crv"], d(j["x"]), d(j["y"]))
+        else:
+            key = _lib.Key.ed25519(d(j["x"]))
+        out.append((k["kid"], k["alg"], os.path.join(BENCHKEYS, k["pem"]), key, j))
+    return out
+
+
 # ---------------------------------------------------------------- measurement
 def measure(ctx, arena, toks, steps, warmup, dist):
     from cap_amd import _lib
+    from cap_amd.shard import max_over_ranks
     h = ctypes.c_void_p()
     L = _lib.lib()
     rc = L.jg_batch_stage(ctx.h, 0, arena, len(arena), toks.ctypes.data_as(ctypes.POINTER(_lib.JgTok)), len(toks),
@@ -147,14 +176,11 @@ def measure(ctx, arena, toks, steps, warmup, dist):
     pinned.free()
     if dist:
         import torch
-        import torch.distributed as td
         torch.cuda.synchronize()
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        td.all_reduce(t, op=td.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, device="cuda")
     b.free()
-    kms = {k: float(np.mean(v)) for k, v in times.items()}
-    return elapsed, accepted, kms
+    kms = {k: float(np.mean(x)) for k, x in times.items()}
+    return elapsed, accepted, kms, v
 
 
 def measure_pcie(ctx, arena, toks, iters=3):
@@ -169,8 +195,7 @@ def measure_pcie(ctx, arena, toks, iters=3):
     best = float("inf")
     for _ in range(iters):
         t0 = time.perf_counter()
-        if L.jg_verify_batch(ctx.h, pa.ptr, len(arena), tp, len(toks),
-                             out) != 0:
+        if L.jg_verify_batch(ctx.h, pa.ptr, len(arena), tp, len(toks), out) != 0:
             raise RuntimeError(ctx.error())
         best = min(best, time.perf_counter() - t0)
     pa.free()
@@ -180,7 +205,37 @@ def measure_pcie(ctx, arena, toks, iters=3):
                     f"{iters}; not the headline value"}
 
 
-def cpu_baseline(pool, alg, keyname, threads, seconds):
+def measure_e2e(pool, kids_jwk, total, threads):
+    """Validator.ValidateBatch through the C++ host mirror (JWKS key set, host
+    parse + kid routing + one GPU batch + claims validation), tokens handed
+    over as one newline-separated host blob.  Not the headline value."""
+    from cap_amd import jwt
+    jwks = json.dumps({"keys": kids_jwk}).encode()
+    ks, err = jwt.NewJSONWebKeySet(None, "https://bench.example/jwks", "",
+                                   lambda url, ca: {"status": 200, "body": jwks, "max_age": 3600})
+    assert err is None, err
+    v, _ = jwt.NewValidator(ks)
+    e = jwt.Expected(Issuer="https://example.com/", Audiences=["www.example.com"], SigningAlgorithms=["ES256"],
+                     Now=lambda: 1611699344 + 60)
+    reps = (total + len(pool) - 1) // len(pool)
+    blob = b"\n".join((pool * reps)[:total])
+    v.ValidateBlob(b"\n".join(pool[:4096]), e)          # warm: JWKS fetch + key staging
+    best, acc = float("inf"), 0
+    for _ in range(2):
+        t0 = time.perf_counter()
+        ok = v.ValidateBlob(blob, e)
+        best = min(best, time.perf_counter() - t0)
+        acc = sum(ok)
+    if acc != total:
+        raise RuntimeError(f"e2e accepted {acc}/{total}")
+    from cap_amd import _capjwt_host
+    return {"value": total / best, "unit": "validated JWTs/s", "ms_per_batch": best * 1e3, "tokens": total,
+            "host_threads": _capjwt_host.host_threads(),
+            "note": "Validator.ValidateBatch (jwt/jwt.go:95 semantics) end to end: host parse/kid routing/claims "
+                    "on host_threads cores + one jg_verify_batch (H2D included); not the headline value"}
+
+
+def cpu_baseline(pool, alg, okeys, threads, seconds, keyidx=None):
     """The C oracle (oracle/jws_oracle.c) on the host's cores over a bounded sample."""
     from oracle import jws
     L = jws.lib()
@@ -192,9 +247,6 @@ def cpu_baseline(pool, alg, keyname, threads, seconds):
                     ("msg", ctypes.c_void_p), ("mlen", ctypes.c_size_t), ("sig", ctypes.c_void_p),
                     ("slen", ctypes.c_size_t)]
     L.or_verify_many.argtypes = [ctypes.POINTER(Job), ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
-    from tests import gpu_helpers as H
-    kd = {k["kid"]: k for k in H.golden()[0]}
-    keys = [jws.Key.from_fixture(kd[k]) for k in (keyname if isinstance(keyname, list) else [keyname])]
     keep = []
 
     def buf(b):
@@ -202,16 +254,15 @@ def cpu_baseline(pool, alg, keyname, threads, seconds):
         keep.append(c)
         return ctypes.cast(c, ctypes.c_void_p)
 
-    # calibrate: 0.25 s single-thread, then size the sample for `seconds` of wall time
     def make_jobs(n):
         jobs = (Job * n)()
         for i in range(n):
             t = pool[i % len(pool)]
             d = t.rfind(b".")
             sig = jws.b64url_decode(t[d + 1:].decode())
-            k = keys[i % len(keys)]
+            k = okeys[(keyidx[i % len(pool)] if keyidx is not None else i % len(okeys))]
             j = jobs[i]
-            j.alg = jws.ALGS[alg]
+            j.alg = jws.ALGS[alg if isinstance(alg, str) else alg[i % len(pool)]]
             j.msg, j.mlen = buf(t[:d]), d
             j.sig, j.slen = buf(sig), len(sig)
             if k.kty == "RSA":
@@ -222,6 +273,7 @@ def cpu_baseline(pool, alg, keyname, threads, seconds):
             else:
                 j.key_kind, j.x = 2, buf(k.x)
         return jobs
+    # calibrate on 64 tokens single-threaded, then size the sample for `seconds` of wall time
     probe = make_jobs(64)
     out = (ctypes.c_uint8 * 64)()
     t0 = time.perf_counter()
@@ -234,10 +286,119 @@ def cpu_baseline(pool, alg, keyname, threads, seconds):
     L.or_verify_many(jobs, n, threads, out)
     el = time.perf_counter() - t0
     ok = sum(out)
+    name = alg if isinstance(alg, str) else "mixed"
     return {"value": n / el, "unit": "verified JWTs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} {alg} tokens from the benchmark pool verified by the C oracle "
+            "sample": f"{n} {name} tokens from the benchmark pool verified by the C oracle "
                       f"(oracle/jws_oracle.c, a restatement of Go crypto/*, not Go itself) "
                       f"on {threads} host threads; {ok}/{n} accepted; {el:.2f} s wall"}
+
+
+def golden_oracle_keys(kids):
+    from oracle import jws
+    from tests import gpu_helpers as H
+    kd = {k["kid"]: k for k in H.golden()[0]}
+    return [jws.Key.from_fixture(kd[k]) for k in kids]
+
+
+# ---------------------------------------------------------------- other BASELINE configs
+def tamper(pool, algs, keyidx, keys_meta, frac, seed=1):
+    """5 % tampered tokens: sig bit-flip, payload char flip, kid
+    swap, alg swap in equal parts.  Returns new (pool, algs, keyidx, expected)."""
+    rng = np.random.default_rng(seed)
+    pool, algs, keyidx = list(pool), np.array(algs), np.array(keyidx)
+    good = np.ones(len(pool), dtype=bool)
+    sel = rng.choice(len(pool), int(len(pool) * frac), replace=False)
+    b64 = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_"
+    fam = {a: a[:2] if a != "EdDSA" else "Ed" for a in ALG_IDS}
+    by_id = {v: k for k, v in ALG_IDS.items()}
+    for j, i in enumerate(sel):
+        t = bytearray(pool[i])
+        mode = j % 4
+        if mode == 0:                                   # signature bit flip (first sig char)
+            d = t.rfind(b".") + 1
+            t[d] = b64[(b64.index(t[d]) ^ 1)]
+        elif mode == 1:                                 # payload character flip
+            d = t.index(b".") + 5
+            t[d] = b64[(b64.index(t[d]) ^ 2)]
+        elif mode == 2:                                 # kid swap: routed to another kid's key
+            keyidx[i] = (keyidx[i] + 1) % len(keys_meta)
+        else:                                           # alg swap within the family (RS<->PS ...)
+            a = by_id[int(algs[i])]
+            alts = [x for x in ALG_IDS if fam[x] == fam[a] and x != a] or [a]
+            algs[i] = ALG_IDS[alts[j % len(alts)]]
+            if alts == [a]:
+                keyidx[i] = (keyidx[i] + 1) % len(keys_meta)
+        pool[i] = bytes(t)
+        good[i] = False
+    return pool, algs, keyidx, good
+
+
+def config_line(ctx, name, workload, pool, algs, keyidx, expected_good, per_gpu, steps, warmup, dist, world,
+                kernel_key=None, mads=None):
+    arena, toks = pack(pool, algs, keyidx, per_gpu)
+    el, acc, kms, v = measure(ctx, arena, toks, steps, warmup, dist)
+    reps = (per_gpu + len(pool) - 1) // len(pool)
+    want = int(np.tile(expected_good, reps)[:per_gpu].sum())
+    line = {"workload": workload, "value": world * per_gpu * steps / el, "unit": "verified JWTs/s",
+            "ms_per_step": el * 1000.0 / steps, "tokens_per_gpu": per_gpu, "unique_pool": len(pool),
+            "accepted": acc, "expected_accepted": want, "kernel_ms": kms}
+    if acc != want:
+        line["error"] = f"accepted {acc} != expected {want}"
+    if kernel_key and mads and kernel_key in kms:
+        ach = mads * per_gpu / (kms[kernel_key] * 1e-3) / 1e12
+        line["roofline"] = {"bound": "valu", "kernel": kernel_key, "achieved": ach, "peak": MAD_PEAK_T,
+                            "unit": "TMAD/s", "frac": ach / MAD_PEAK_T}
+    return line
+
+
+def run_configs(ctx, args, threads, rank, world, dist):
+    out = {}
+    # configs[2]: PS512 RSA-4096, 1M tokens sharded across 8 GPUs -> 131072 per GPU
+    ctx.load_keys(abi_keys(["rsa4096-a"]))
+    pool = gen_tokens("PS512", 4096, golden_keypaths(["rsa4096-a"]), threads, f"c2r{rank}")
+    out["ps512_rsa4096"] = config_line(
+        ctx, "ps512_rsa4096", "PS512 RSA-4096 (PSS/MGF1-SHA512), 1M tokens / 8 GPUs = 131072 per GPU (configs[2])",
+        pool, [ALG_IDS["PS512"]] * len(pool), [0] * len(pool), np.ones(len(pool), bool), 131072,
+        max(1, args.steps // 2), 1, dist, world, "rsa4096_modexp", rsa_modexp_mads_per_token(148))
+    # configs[3]: EdDSA Ed25519 + ES384 P-384 mixed, 1M tokens per GPU
+    ctx.load_keys(abi_keys(["ed-a", "p384-a"]))
+    pe = gen_tokens("EdDSA", 8192, golden_keypaths(["ed-a"]), threads, f"c3r{rank}")
+    p3 = gen_tokens("ES384", 8192, golden_keypaths(["p384-a"]), threads, f"c3r{rank}", kid_base=1)
+    pool = [t for pair in zip(pe, p3) for t in pair]
+    algs = [ALG_IDS["EdDSA"], ALG_IDS["ES384"]] * len(pe)
+    out["eddsa_es384_mixed"] = config_line(
+        ctx, "eddsa_es384_mixed", "EdDSA Ed25519 + ES384 P-384 50/50 mixed batch, 1M tokens per GPU (configs[3])",
+        pool, algs, [0, 1] * len(pe), np.ones(len(pool), bool), 1 << 20, max(1, args.steps // 2), 1, dist, world)
+    # configs[4]: all 10 algs, 32 kids, ~5 % tampered; the 10M stream in 256k-token chunks (one chunk per step)
+    meta = bench_keys()
+    ctx.load_keys([m[3] for m in meta])
+    pool, algs, keyidx = [], [], []
+    for ki, (kid, alg, pem, _, _) in enumerate(meta):
+        n = 512 if alg in ("RS512", "PS512") else 1024
+        toks = gen_tokens(alg, n, [pem], threads, f"c4r{rank}", kid_base=ki)
+        pool += toks
+        algs += [ALG_IDS[alg]] * n
+        keyidx += [ki] * n
+    order = np.random.default_rng(1).permutation(len(pool))
+    pool = [pool[i] for i in order]
+    algs = [algs[i] for i in order]
+    keyidx = [keyidx[i] for i in order]
+    pool, algs, keyidx, good = tamper(pool, algs, keyidx, meta, 0.05)
+    out["mixed_10alg_32kid"] = config_line(
+        ctx, "mixed_10alg_32kid", "all 10 algs, 32 kids, 5% tampered, 10M stream on 8 GPUs in 262144-token chunks "
+        "(configs[4]); one chunk per step per GPU", pool, algs, keyidx, good, 262144, max(1, args.steps // 2), 1,
+        dist, world)
+    return out
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc pass
+    (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), or None."""
+    try:
+        d = json.load(open(TRAFFIC))
+        return d["kernels"][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def main():
@@ -248,6 +409,8 @@ def main():
     ap.add_argument("--tokens", type=int, default=1 << 20, help="tokens per GPU per step")
     ap.add_argument("--pool", type=int, default=1 << 17, help="unique signed tokens (replicated)")
     ap.add_argument("--no-rs256", action="store_true")
+    ap.add_argument("--no-configs", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     args = ap.parse_args()
@@ -269,9 +432,10 @@ def main():
     # ---- ES256, P-256 JWKS with 4 kids (configs[1])
     kids = ["p256-a", "p256-b", "p256-c", "p256-d"]
     ctx.load_keys(abi_keys(kids))
-    pool = gen_tokens("ES256", min(args.pool, args.tokens), kids, host_threads, f"r{rank}")
-    arena, toks = build_arena(pool, 7, len(kids), args.tokens)
-    el, acc, kms = measure(ctx, arena, toks, args.steps, args.warmup, dist)
+    pool = gen_tokens("ES256", min(args.pool, args.tokens), golden_keypaths(kids), host_threads, f"r{rank}")
+    npool = len(pool)
+    arena, toks = pack(pool, [ALG_IDS["ES256"]] * npool, np.arange(npool) % len(kids), args.tokens)
+    el, acc, kms, _ = measure(ctx, arena, toks, args.steps, args.warmup, dist)
     ntok = len(toks)
     value = world * ntok * args.steps / el
     ms_step = el * 1000.0 / args.steps
@@ -290,51 +454,80 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32 (28-bit limbs, 64-bit v_mad_u64_u32 accumulators)",
-        "data": f"synthetic: OpenSSL-signed ES256 JWTs (testJWTClaims shape), {len(pool)}-token unique pool "
+        "data": f"synthetic: OpenSSL-signed ES256 JWTs (testJWTClaims shape), {npool}-token unique pool "
                 f"replicated to {ntok} per GPU, no verdict caching",
         "config": {"workload": "ES256 P-256 JWKS with 4 kids, 1M tokens batch-verified per MI355X (BASELINE configs[1])",
                    "tokens_per_gpu": ntok, "kids": 4, "parallelism": f"independent shards x{world}"},
         "accepted": acc,
         "roofline": {"bound": "valu", "kernel": "k_ec_point<P256>",
                      "achieved": achieved, "peak": MAD_PEAK_T, "unit": "TMAD/s",
-                     "frac": achieved / MAD_PEAK_T, "traffic": None,
+                     "frac": achieved / MAD_PEAK_T, "traffic": load_traffic("p256_point"),
                      "note": "integer multiply-add roofline (SURVEY §8d): algorithmic 32x32->64 MADs "
                              f"per token {p256_point_mads_per_token():.0f} x tokens / HIP-event kernel time; "
-                             "peak = measured v_mad_u64_u32 rate"},
+                             "peak = measured v_mad_u64_u32 rate; traffic = HBM bytes per launch from the "
+                             "rocprofv3 --pmc pass in profiles/r01_pmc_traffic.json"},
         "kernel_ms": kms,
     }
     if acc != ntok:
         result["error"] = f"only {acc}/{ntok} valid tokens accepted"
     if rank == 0 and world == 1:
         result["pcie"] = measure_pcie(ctx, arena, toks)
+    del arena, toks
 
     # ---- RS256 RSA-2048 (second half of the metric)
     if not args.no_rs256:
         ctx.load_keys(abi_keys(["rsa2048-a"]))
-        rpool = gen_tokens("RS256", min(1 << 15, args.tokens), ["rsa2048-a"], host_threads, f"r{rank}")
-        rarena, rtoks = build_arena(rpool, 1, 1, args.tokens)
-        rel, racc, rkms = measure(ctx, rarena, rtoks, max(1, args.steps // 2), 1, dist)
+        rpool = gen_tokens("RS256", min(1 << 15, args.tokens), golden_keypaths(["rsa2048-a"]), host_threads,
+                           f"r{rank}")
+        rarena, rtoks = pack(rpool, [ALG_IDS["RS256"]] * len(rpool), [0] * len(rpool), args.tokens)
         rsteps = max(1, args.steps // 2)
+        rel, racc, rkms, _ = measure(ctx, rarena, rtoks, rsteps, 1, dist)
         mexp = rkms.get("rsa2048_modexp", float("nan"))
-        rach = rsa2048_modexp_mads_per_token() * len(rtoks) / (mexp * 1e-3) / 1e12
+        rach = rsa_modexp_mads_per_token(74) * len(rtoks) / (mexp * 1e-3) / 1e12
         result["rs256"] = {"value": world * len(rtoks) * rsteps / rel, "unit": "verified JWTs/s",
                            "ms_per_step": rel * 1000.0 / rsteps, "tokens_per_gpu": len(rtoks),
                            "accepted": racc, "kernel_ms": rkms,
                            "roofline": {"bound": "valu", "kernel": "k_rsa_modexp<37,2,8>", "achieved": rach,
                                         "peak": MAD_PEAK_T, "unit": "TMAD/s", "frac": rach / MAD_PEAK_T,
-                                        "mads_per_token": rsa2048_modexp_mads_per_token()}}
+                                        "mads_per_token": rsa_modexp_mads_per_token(74),
+                                        "traffic": load_traffic("rsa2048_modexp")}}
+        if racc != len(rtoks):
+            result["rs256"]["error"] = f"only {racc}/{len(rtoks)} valid tokens accepted"
+        del rarena, rtoks
+
+    # ---- the other BASELINE configs (per-GPU share, same timing rules)
+    if not args.no_configs:
+        result["configs"] = run_configs(ctx, args, host_threads, rank, world, dist)
+    ctx.close()
+
+    # ---- end-to-end Validator.ValidateBatch (host + GPU), rank 0 only
+    if rank == 0 and not args.no_e2e:
+        jwk = [{"kty": "EC", "kid": f"kid-{i:02d}", "crv": "P-256", **xy} for i, xy in enumerate(p256_jwk_xy(kids))]
+        result["e2e"] = measure_e2e(pool, jwk, args.tokens, host_threads)
+
     # ---- CPU baseline (rank 0, N = 1 only)
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(pool, "ES256", kids, host_threads, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(pool, "ES256", golden_oracle_keys(kids), host_threads, args.cpu_seconds)
         if not args.no_rs256:
-            result["cpu_baseline_rs256"] = cpu_baseline(rpool, "RS256", "rsa2048-a", host_threads,
-                                                        args.cpu_seconds / 2)
-    ctx.close()
+            result["cpu_baseline_rs256"] = cpu_baseline(rpool, "RS256", golden_oracle_keys(["rsa2048-a"]),
+                                                        host_threads, args.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps(result))
     if dist:
         import torch.distributed as td
         td.destroy_process_group()
+
+
+def p256_jwk_xy(kids):
+    import base64
+    from tests import gpu_helpers as H
+    kd = {k["kid"]: k for k in H.golden()[0]}
+    out = []
+    for k in kids:
+        d = kd[k]
+        out.append({"x": base64.urlsafe_b64encode(int(d["x"], 16).to_bytes(32, "big")).rstrip(b"=").decode(),
+                    "y": base64.urlsafe_b64encode(int(d["y"], 16).to_bytes(32, "big")).rstrip(b"=").decode()})
+    return out
 
 
 if __name__ == "__main__":

@@ -44,6 +44,7 @@ typedef struct {
   int nkeys;
   long lo, hi;
   char** out;
+  int kid_base;           /* TOKGEN_KID_BASE: first kid number ("kid-NN") */
 } job;
 
 static const EVP_MD* alg_md(const char* alg) {
@@ -64,7 +65,7 @@ static void* worker(void* arg) {
   unsigned char sig[1024], raw[200];
   for (long i = j->lo; i < j->hi; ++i) {
     const int k = (int)(i % j->nkeys);
-    snprintf(hdr, sizeof hdr, "{\"alg\":\"%s\",\"kid\":\"kid-%02d\",\"typ\":\"JWT\"}", j->alg, k);
+    snprintf(hdr, sizeof hdr, "{\"alg\":\"%s\",\"kid\":\"kid-%02d\",\"typ\":\"JWT\"}", j->alg, j->kid_base + k);
     snprintf(pay, sizeof pay,
              "{\"aud\":[\"www.example.com\"],\"exp\":1611699944,\"iat\":1611699344,"
              "\"iss\":\"https://example.com/\",\"jti\":\"%ld\",\"nbf\":1611699344,\"sub\":\"alice@example.com\"}", i);
@@ -129,7 +130,8 @@ int main(int argc, char** argv) {
   pthread_t* th = calloc((size_t)threads, sizeof(pthread_t));
   job* js = calloc((size_t)threads, sizeof(job));
   for (int t = 0; t < threads; ++t) {
-    js[t] = (job){alg, keys, nkeys, count * t / threads, count * (t + 1) / threads, out};
+    const char* kb = getenv("TOKGEN_KID_BASE");
+    js[t] = (job){alg, keys, nkeys, count * t / threads, count * (t + 1) / threads, out, kb ? atoi(kb) : 0};
     pthread_create(&th[t], NULL, worker, &js[t]);
   }
   for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
