@@ -47,3 +47,16 @@ __device__ __forceinline__ void mul64(uint64_t& acc, uint32_t a, uint32_t b, int
 __device__ __forceinline__ void mad64s(uint64_t& acc, uint32_t a, uint32_t b, int slot = 0) {
   JG_MAD_ASM(JG_MAD_ACC, JG_S);
 }
+
+// Compiler-scheduled forms for register-resident operand pairs (the fixed-
+// modulus field products of mp.hpp).  There the products' 28-bit operands
+// need no zero-extension copies, and an inline asm statement costs more than
+// it saves: LLVM pads an s_nop 0 after an asm statement before a VALU
+// instruction that reads one of its results, which the scheduler's column-
+// wise MAD chains hit ~every other MAD (P-256 point kernel: 731 s_nops in 7397
+// instructions with asm products, 8 in 6621 with these).  The SGPR-constant
+// reduction MADs stay asm, grouped per row (mad_blocks.hpp), where the
+// compiler would otherwise strength-reduce power-of-two constants into
+// shift + add pairs.
+__device__ __forceinline__ void mad64c(uint64_t& acc, uint32_t a, uint32_t b) { acc += (uint64_t)a * b; }
+__device__ __forceinline__ void mul64c(uint64_t& acc, uint32_t a, uint32_t b) { acc = (uint64_t)a * b; }

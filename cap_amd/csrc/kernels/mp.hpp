@@ -20,6 +20,7 @@
 
 #include "field_consts.hpp"
 #include "mad.hpp"
+#include "mad_blocks.hpp"
 
 #define MP_W 28
 #define MP_MASK 0x0fffffffu
@@ -27,25 +28,65 @@
 
 namespace mp {
 
+// Limb indices j of the reduction row's non-zero constants: m+1 (j >= 1) when
+// m = -1 mod 2^28 (NP1), else m.  One reduction row = one mad_blocks.hpp asm
+// statement per 8 of them (the constants are wave-uniform SGPR operands).
+struct NzIdx {
+  int n;
+  int j[32];
+};
+template <class F>
+constexpr uint32_t red_const(int j) { return F::NP1 ? (j == 0 ? 0u : F::M1[j]) : F::M[j]; }
+template <class F>
+constexpr NzIdx red_idx() {
+  NzIdx r{0, {}};
+  for (int j = 0; j < F::L; ++j)
+    if (red_const<F>(j) != 0) r.j[r.n++] = j;
+  return r;
+}
+
+// t[j] += q * c_j over the non-zero reduction constants, from the S-th on
+template <class F, int S>
+MPD void red_row(uint64_t* t, uint32_t q) {
+  constexpr NzIdx z = red_idx<F>();
+  constexpr int n = z.n - S;
+#define RJ(k) z.j[S + (k)]
+#define RT(k) t[RJ(k)]
+#define RC(k) red_const<F>(RJ(k))
+  if constexpr (n >= 8) {
+    mb::mads8(RT(0), RT(1), RT(2), RT(3), RT(4), RT(5), RT(6), RT(7), q,
+              RC(0), RC(1), RC(2), RC(3), RC(4), RC(5), RC(6), RC(7));
+    red_row<F, S + 8>(t, q);
+  } else if constexpr (n == 7) {
+    mb::mads7(RT(0), RT(1), RT(2), RT(3), RT(4), RT(5), RT(6), q, RC(0), RC(1), RC(2), RC(3), RC(4), RC(5), RC(6));
+  } else if constexpr (n == 6) {
+    mb::mads6(RT(0), RT(1), RT(2), RT(3), RT(4), RT(5), q, RC(0), RC(1), RC(2), RC(3), RC(4), RC(5));
+  } else if constexpr (n == 5) {
+    mb::mads5(RT(0), RT(1), RT(2), RT(3), RT(4), q, RC(0), RC(1), RC(2), RC(3), RC(4));
+  } else if constexpr (n == 4) {
+    mb::mads4(RT(0), RT(1), RT(2), RT(3), q, RC(0), RC(1), RC(2), RC(3));
+  } else if constexpr (n == 3) {
+    mb::mads3(RT(0), RT(1), RT(2), q, RC(0), RC(1), RC(2));
+  } else if constexpr (n == 2) {
+    mb::mads2(RT(0), RT(1), q, RC(0), RC(1));
+  } else if constexpr (n == 1) {
+    mb::mads1(RT(0), q, RC(0));
+  }
+#undef RJ
+#undef RT
+#undef RC
+}
+
 template <class F>
 MPD void mont_reduce(uint32_t* r, uint64_t* t) {
   constexpr int L = F::L;
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    if constexpr (F::NP1) {
-      // m = -1 mod 2^28 => NP = 1, q = t[i] mod 2^28 and q*m = q*(m+1) - q:
-      // the "- q" is exactly the low limb the carry shift drops, and m+1 is
-      // sparse (P-256: 4 non-zero limbs of 10, P-521: 1 of 20).
-      const uint32_t q = (uint32_t)t[i] & MP_MASK;
-#pragma unroll
-      for (int j = 1; j < L; ++j)
-        if (F::M1[j] != 0) mad64s(t[i + j], q, F::M1[j], 2 + (j & 1));
-    } else {
-      const uint32_t q = ((uint32_t)t[i] * F::NP) & MP_MASK;
-#pragma unroll
-      for (int j = 0; j < L; ++j)
-        if (F::M[j] != 0) mad64s(t[i + j], q, F::M[j], 2 + (j & 1));
-    }
+    // NP1: m = -1 mod 2^28 => NP = 1, q = t[i] mod 2^28 and q*m = q*(m+1) - q:
+    // the "- q" is exactly the low limb the carry shift drops, and m+1 is
+    // sparse (P-256: 4 non-zero limbs of 10, P-521: 1 of 20).
+    const uint32_t q = F::NP1 ? ((uint32_t)t[i] & MP_MASK) : (((uint32_t)t[i] * F::NP) & MP_MASK);
+    red_row<F, 0>(t + i, q);
     t[i + 1] += t[i] >> MP_W;
   }
   uint64_t c = 0;
@@ -68,8 +109,8 @@ MPD void mul(uint32_t* r, const uint32_t* a, const uint32_t* b) {
 #pragma unroll
     for (int j = 0; j < L; ++j) {
       // first product of column i+j in this loop order writes, not accumulates
-      if (i == 0 || j == L - 1) mul64(t[i + j], a[i], b[j], j & 1);
-      else mad64(t[i + j], a[i], b[j], j & 1);
+      if (i == 0 || j == L - 1) mul64c(t[i + j], a[i], b[j]);
+      else mad64c(t[i + j], a[i], b[j]);
     }
   mont_reduce<F>(r, t);
 }
@@ -85,12 +126,12 @@ MPD void sqr(uint32_t* r, const uint32_t* a) {
   t[2 * L - 1] = 0;
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    if (i == 0 || i == L - 1) mul64(t[2 * i], a[i], a[i], 1);
-    else mad64(t[2 * i], a[i], a[i], 1);
+    if (i == 0 || i == L - 1) mul64c(t[2 * i], a[i], a[i]);
+    else mad64c(t[2 * i], a[i], a[i]);
 #pragma unroll
     for (int j = i + 1; j < L; ++j) {
-      if (i == 0 || j == L - 1) mul64(t[i + j], a2[i], a[j], (j - i + 1) & 1);
-      else mad64(t[i + j], a2[i], a[j], (j - i + 1) & 1);
+      if (i == 0 || j == L - 1) mul64c(t[i + j], a2[i], a[j]);
+      else mad64c(t[i + j], a2[i], a[j]);
     }
   }
   mont_reduce<F>(r, t);
@@ -218,7 +259,7 @@ MPD void from_mont(uint32_t* r, const uint32_t* a) {
 template <class F>
 MPD void pow_e(uint32_t* r, const uint32_t* x, const uint32_t* E, int ebits, bool minus2) {
   constexpr int L = F::L;
-  constexpr int WB = L <= 10 ? 4 : 2, NT = 1 << WB;
+  constexpr int WB = L <= 10 ? 3 : 2, NT = 1 << WB;
   uint32_t tab[NT][L];
   set_const<F>(tab[0], F::ONE);
   copy<F>(tab[1], x);

@@ -3,7 +3,15 @@
 //     into the scratch rows in the layout the class's arithmetic kernel wants;
 //   * hash the JWS signing input with the alg's SHA-2 (go-jose verifyPayload,
 //     R9); EdDSA hashes R || A || M (crypto/ed25519.Verify, R25).
-// One thread per (padded) token; one 64-thread block = one key-uniform wave.
+// One 64-thread block = one key-uniform wave of tokens, one token per lane.
+//
+// Token bytes reach the lanes through LDS, staged with COALESCED loads: for
+// each 128-byte window of the strings, the wave copies 33 dwords of every one
+// of its 64 tokens (two tokens per load instruction, each half-wave reading
+// 128 contiguous bytes) into a per-token LDS slot, then each lane reads its own
+// slot.  A lane-per-token walk over the arena instead makes every load
+// instruction touch 64 different cache lines (prep ran at ~0.4 TB/s that way:
+// L1 thrash, one L2 request per lane per dword).
 #include <hip/hip_runtime.h>
 
 #include "common.hpp"
@@ -13,6 +21,9 @@
 using namespace jgk;
 
 namespace {
+
+constexpr int WIN = 32;         // dwords per window step (128 bytes of string)
+constexpr int SLOT = 36;        // LDS words per token slot (33 used; stride 36 keeps lanes' reads on distinct banks)
 
 __device__ __forceinline__ int b64val(uint32_t c) {
   if (c - 'A' < 26u) return (int)(c - 'A');
@@ -36,20 +47,57 @@ __device__ __forceinline__ int es_size(int alg) { return alg == 7 ? 32 : alg == 
 // layout of the decoded signature in the scratch rows
 enum Layout { LAY_BE = 0, LAY_SPLIT_BE = 1, LAY_LE = 2 };
 
+// Every lane names the arena dword index `w` where its window starts; the wave
+// copies dwords [w, w+33) of all 64 windows into slot[lane][0..33).  Called in
+// wave-uniform control flow only (one block == one wave; every lane copies
+// words of other lanes' windows).
+__device__ __forceinline__ void stage(uint32_t* slots, uint64_t* wsh, const uint32_t* arena_w, uint64_t w) {
+  const int lane = threadIdx.x;
+  wsh[lane] = w;
+  __syncthreads();
+  const int half = lane >> 5, k = lane & 31;
+#pragma unroll 8
+  for (int i = 0; i < 32; ++i) {
+    const int tt = 2 * i + half;
+    slots[tt * SLOT + k] = arena_w[wsh[tt] + k];
+  }
+  slots[lane * SLOT + 32] = arena_w[w + 32];
+  __syncthreads();
+}
+
+// N big-endian message words i0 .. i0+N-1 (SHA padding applied, length words
+// are the caller's) from a staged window whose dword 0 holds aligned message
+// word i0 (the message starts `shift` bytes into its first aligned dword).
+template <int N>
+__device__ __forceinline__ void window_words(const uint32_t* u, uint32_t i0, uint32_t shift, uint32_t len,
+                                             uint32_t* out) {
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const uint32_t raw = sha2::bswap32(__builtin_amdgcn_alignbyte(u[k + 1], u[k], shift));
+    const int rem = (int)len - (int)(4u * (i0 + k));
+    const uint32_t keep = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : (0xffffffffu << (32 - 8 * rem)));
+    const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80u << (24 - 8 * rem)) : 0u;
+    out[k] = (raw & keep) | pad;
+  }
+}
+
 template <int CLS>
 __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
-  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
+  __shared__ uint32_t slots[WAVE * SLOT];
+  __shared__ uint64_t wsh[WAVE];
+  const int lane = threadIdx.x;
+  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + lane;
   const int64_t np = a.npad;
   const int32_t t = a.perm[p];
+  const bool valid = t >= 0;
   uint32_t* sigw = a.sigw;
   uint32_t* dig = a.dig;
-  if (t < 0) {
-    a.status[p] = ST_REJECT;
-    return;
-  }
-  const jg_tok_dev tk = a.toks[t];
+  const uint32_t* arena_w = reinterpret_cast<const uint32_t*>(a.arena);
+  const uint32_t* my = slots + lane * SLOT;
+  jg_tok_dev tk{};
+  if (valid) tk = a.toks[t];
   const int alg = tk.alg;
-  uint8_t st = ST_OK;
+  uint8_t st = valid ? ST_OK : ST_REJECT;
 
   // ---- base64url decode of the signature segment
   const uint32_t n = tk.sig_b64_len;
@@ -66,94 +114,150 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
     ks = (alg >= 7 && alg <= 9) ? (uint32_t)es_size(alg) : 0u;
     if (ks == 0 || D != 2 * ks) { st = ST_REJECT; D = 0; }
   }
-  // zero the rows this token may leave partially written
-  for (int r = 0; r < a.zrows; ++r) sigw[(int64_t)r * np + p] = 0u;
+  if (valid) {
+    // zero the rows this token may leave partially written
+    for (int r = 0; r < a.zrows; ++r) sigw[(int64_t)r * np + p] = 0u;
+  }
 
-  // characters are fetched as aligned dwords (4 per load) from the arena
   const uint64_t sbyte = tk.off + tk.sig_rel_off;
-  const uint32_t* sw32 = reinterpret_cast<const uint32_t*>(a.arena + (sbyte & ~3ull));
+  const uint64_t sw0 = sbyte >> 2;                     // arena dword of the segment's first char
   const uint32_t first = (uint32_t)(sbyte & 3ull);
+  const uint32_t nchars = (valid && D) ? n : 0u;
+  const uint32_t span = nchars ? first + nchars : 0u;  // window bytes the chars occupy
   uint32_t acc = 0, bitsn = 0, outi = 0;
   uint32_t cur_row = 0xffffffffu, cur_word = 0;
-  uint32_t R_le[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // Ed25519: first 32 bytes (R)
-  const uint32_t nchars = D ? n : 0u;
-  uint32_t word = 0;
-  for (uint32_t i = 0; i < nchars; ++i) {
-    const uint32_t pos = first + i;
-    if (i == 0 || (pos & 3u) == 0) word = sw32[pos >> 2];
-    const int v = b64val((word >> ((pos & 3u) * 8)) & 0xffu);
-    if (v < 0) { st = ST_REJECT; break; }
-    acc = (acc << 6) | (uint32_t)v;
-    bitsn += 6;
-    if (bitsn >= 8) {
-      bitsn -= 8;
-      const uint32_t byte = (acc >> bitsn) & 0xffu;
-      // map output byte outi -> (row, shift)
-      uint32_t row, sh;
-      if (layout == LAY_BE) {
-        const uint32_t j = D - 1 - outi;
-        row = j >> 2; sh = (j & 3u) * 8u;
-      } else if (layout == LAY_SPLIT_BE) {
-        const uint32_t h = outi >= ks ? 1u : 0u;
-        const uint32_t j = ks - 1 - (outi - h * ks);
-        row = h * EC_S_ROW + (j >> 2); sh = (j & 3u) * 8u;
-      } else {
-        row = outi >> 2; sh = (outi & 3u) * 8u;
-        if (outi < 32) {
+  uint32_t R_le[8] = {0, 0, 0, 0, 0, 0, 0, 0};          // Ed25519: first 32 bytes (R)
+  bool bad = false;
+  for (uint32_t c = 0;; ++c) {
+    const bool need = !bad && span > 4u * WIN * c;
+    if (__ballot(need) == 0ull) break;
+    stage(slots, wsh, arena_w, need ? sw0 + (uint64_t)WIN * c : (valid ? sw0 : 0ull));
+    if (!need) continue;
+    const uint32_t lo = 4u * WIN * c;
+    const uint32_t beg = lo > first ? lo : first;
+    const uint32_t end = span < lo + 4u * WIN ? span : lo + 4u * WIN;
+    uint32_t word = my[(beg - lo) >> 2];
+    for (uint32_t pos = beg; pos < end; ++pos) {
+      if ((pos & 3u) == 0) word = my[(pos - lo) >> 2];
+      const int v = b64val((word >> ((pos & 3u) * 8)) & 0xffu);
+      if (v < 0) { st = ST_REJECT; bad = true; break; }
+      acc = (acc << 6) | (uint32_t)v;
+      bitsn += 6;
+      if (bitsn >= 8) {
+        bitsn -= 8;
+        const uint32_t byte = (acc >> bitsn) & 0xffu;
+        // map output byte outi -> (row, shift)
+        uint32_t row, sh;
+        if (layout == LAY_BE) {
+          const uint32_t j = D - 1 - outi;
+          row = j >> 2; sh = (j & 3u) * 8u;
+        } else if (layout == LAY_SPLIT_BE) {
+          const uint32_t h = outi >= ks ? 1u : 0u;
+          const uint32_t j = ks - 1 - (outi - h * ks);
+          row = h * EC_S_ROW + (j >> 2); sh = (j & 3u) * 8u;
+        } else {
+          row = outi >> 2; sh = (outi & 3u) * 8u;
+          if (outi < 32) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if ((outi >> 2) == (uint32_t)k) R_le[k] |= byte << sh;
+            for (int k = 0; k < 8; ++k)
+              if ((outi >> 2) == (uint32_t)k) R_le[k] |= byte << sh;
+          }
         }
+        if (row != cur_row) {
+          if (cur_row != 0xffffffffu) sigw[(int64_t)cur_row * np + p] = cur_word;
+          cur_row = row; cur_word = 0;
+        }
+        cur_word |= byte << sh;
+        ++outi;
       }
-      if (row != cur_row) {
-        if (cur_row != 0xffffffffu) sigw[(int64_t)cur_row * np + p] = cur_word;
-        cur_row = row; cur_word = 0;
-      }
-      cur_word |= byte << sh;
-      ++outi;
     }
   }
   if (cur_row != 0xffffffffu && st == ST_OK) sigw[(int64_t)cur_row * np + p] = cur_word;
-  a.siglen[p] = (uint16_t)D;
+  if (valid) a.siglen[p] = (uint16_t)D;
 
-  // ---- hash of the signing input
-  sha2::MemString m;
-  const uint64_t moff = tk.off;
-  m.aligned = reinterpret_cast<const uint32_t*>(a.arena + (moff & ~3ull));
-  m.shift = (uint32_t)(moff & 3ull);
-  m.len = tk.sig_in_len;
-  uint32_t dout[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) dout[k] = 0;
-  if (CLS == CLS_ED25519) {
-    // SHA-512(R || A || M), A = the key's 32 raw public-key bytes
+  // ---- hash of the signing input.  Tokens of one wave share a key, not
+  // necessarily an alg (RS256 and PS512 under one RSA key), so the window loop
+  // is uniform and each lane runs its own hash on the staged window:
+  //   SHA-256: a 33-dword window holds two 64-byte blocks (message words 32c..);
+  //   SHA-512/384: one 128-byte block per window.  Ed25519 hashes R || A || M:
+  //   block 0 = the 64-byte register prefix + message words 0..15, block
+  //   c >= 1 = message words 32c-16 ..
+  const uint64_t mw0 = tk.off >> 2;
+  const uint32_t mshift = (uint32_t)(tk.off & 3ull);
+  const uint32_t len = tk.sig_in_len;
+  const int hb = CLS == CLS_ED25519 ? 512 : alg_hash_bits(alg);
+  uint32_t pre[16];
+  uint32_t pw = 0;
+  if (CLS == CLS_ED25519 && valid) {
     const uint32_t* A = a.keyblob + a.keys[a.wave_key[p / WAVE]].aux_off;
-    uint32_t pre[16];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       pre[k] = sha2::bswap32(R_le[k]);
       pre[8 + k] = sha2::bswap32(A[k]);
     }
-    uint64_t h[8];
-    sha2::sha512_mem(h, false, m, pre, 64);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { dout[2 * k] = (uint32_t)(h[k] >> 32); dout[2 * k + 1] = (uint32_t)h[k]; }
-  } else {
-    const int hb = alg_hash_bits(alg);
+    pw = 16;
+  }
+  const uint32_t tot = 4 * pw + len;                   // bytes hashed
+  uint32_t nblk = 0, nwin = 0;
+  if (valid) {
+    nblk = hb == 256 ? (len + 9 + 63) / 64 : (tot + 17 + 127) / 128;
+    nwin = hb == 256 ? (nblk + 1) / 2 : nblk;
+  }
+  uint32_t h32[8];
+  uint64_t h64[8];
+  sha2::sha256_init(h32);
+  sha2::sha512_init(h64, hb == 384);
+  for (uint32_t c = 0;; ++c) {
+    const bool need = c < nwin;
+    if (__ballot(need) == 0ull) break;
+    const uint32_t i0 = hb == 256 ? 32u * c : (c == 0 ? 0u : 32u * c - pw);   // message word at window dword 0
+    stage(slots, wsh, arena_w, need ? mw0 + i0 : (valid ? mw0 : 0ull));
+    if (!need) continue;
     if (hb == 256) {
-      uint32_t h[8];
-      sha2::sha256_mem(h, m);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) dout[k] = h[k];
+#pragma unroll 1
+      for (uint32_t hf = 0; hf < 2; ++hf) {
+        const uint32_t blk = 2 * c + hf;
+        if (blk < nblk) {
+          uint32_t w[16];
+          window_words<16>(my + 16 * hf, 16 * blk, mshift, len, w);
+          if (blk == nblk - 1) {
+            w[14] = len >> 29;
+            w[15] = len << 3;
+          }
+          sha2::sha256_compress(h32, w);
+        }
+      }
     } else {
-      uint64_t h[8];
-      sha2::sha512_mem(h, hb == 384, m, nullptr, 0);
+      uint32_t v[32];
+      if (pw != 0 && c == 0) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { dout[2 * k] = (uint32_t)(h[k] >> 32); dout[2 * k + 1] = (uint32_t)h[k]; }
+        for (int k = 0; k < 16; ++k) v[k] = pre[k];
+        window_words<16>(my, 0, mshift, len, v + 16);
+      } else {
+        window_words<32>(my, i0, mshift, len, v);
+      }
+      if (c == nblk - 1) {                               // 128-bit length, high 64 bits zero
+        v[30] = tot >> 29;
+        v[31] = tot << 3;
+      }
+      uint64_t w[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) w[k] = ((uint64_t)v[2 * k] << 32) | v[2 * k + 1];
+      sha2::sha512_compress(h64, w);
     }
   }
+  if (valid) {
+    uint32_t dout[16];
+    if (hb == 256) {
 #pragma unroll
-  for (int k = 0; k < 16; ++k) dig[(int64_t)k * np + p] = dout[k];
+      for (int k = 0; k < 16; ++k) dout[k] = k < 8 ? h32[k] : 0u;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { dout[2 * k] = (uint32_t)(h64[k] >> 32); dout[2 * k + 1] = (uint32_t)h64[k]; }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dig[(int64_t)k * np + p] = dout[k];
+  }
   a.status[p] = st;
 }
 
