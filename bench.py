@@ -34,9 +34,11 @@ BENCHKEYS = os.path.join(ROOT, "tools", "benchkeys")
 TOKGEN = os.path.join(ROOT, "tools", "tokgen", "tokgen")
 TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
 
-# measured v_mad_u64_u32 issue rate, chip-wide (profiles/r01_int_rates.json,
-# 8 waves/SIMD, SGPR operand): the integer multiply-add roofline denominator
-MAD_PEAK_T = 32.27
+# measured v_mad_u64_u32 issue rate, chip-wide: the integer multiply-add
+# roofline denominator.  36.98 T lane-MAD/s = 8 waves/SIMD, 8 MADs per asm
+# statement (no hazard padding), profiles/r01_int_rates2.json -- i.e. one
+# wave64 VALU instruction per 4 cycles per SIMD, the chip's full VALU issue rate.
+MAD_PEAK_T = 36.98
 
 JG_TOK = np.dtype([("off", "<u8"), ("sig_in_len", "<u4"), ("sig_rel_off", "<u4"), ("sig_b64_len", "<u4"),
                    ("key_idx", "<u2"), ("alg", "u1"), ("flags", "u1")])
@@ -51,13 +53,13 @@ def p256_point_mads_per_token():
     token: 28-bit limbs, L = 10; Montgomery product = L^2 (mul) or L(L+1)/2 (sqr)
     + L * 4 for the reduction (p + 1 has 4 non-zero limbs above limb 0, mp.hpp);
     mixed addition = 8 mul + 3 sqr + 3 value folds (6 non-zero limbs of
-    2^256 mod p); signed 16-bit comb digits (ecdsa.hpp ec_comb_w): 16 windows
-    non-zero w.p. 1 - 2^-16 plus a carry window non-zero w.p. ~1/2, for u1 and
-    u2, the first addition an assignment; final check 1 sqr + 2 mul."""
+    2^256 mod p); signed 20-bit comb digits (ecdsa.hpp ec_comb_w): 13 windows
+    non-zero w.p. 1 - 2^-20 (the top window never carries) for u1 and u2, the
+    first addition an assignment; final check 1 sqr + 2 mul."""
     L, red, fold = 10, 10 * 4, 6
     mul, sqr = L * L + red, L * (L + 1) // 2 + red
     madd = 8 * mul + 3 * sqr + 3 * fold
-    adds = 2 * (16 * (1 - 2.0 ** -16) + 0.5) - 1
+    adds = 2 * 13 * (1 - 2.0 ** -20) - 1
     return adds * madd + sqr + 2 * mul
 
 

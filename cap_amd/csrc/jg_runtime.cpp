@@ -60,7 +60,7 @@ int cls_rows_sig(int c) {
 int cls_rows_scratch(int c) {
   switch (c) {
     case CLS_RSA2K: case CLS_RSA3K: case CLS_RSA4K: return 2 * rsa_limbs(c) + SIGW_ROWS;
-    case CLS_P256: case CLS_P384: case CLS_P521: return ec_windows(c) + 2 * ec_limbs(c);
+    case CLS_P256: case CLS_P384: case CLS_P521: return ec_digit_rows(c) + 2 * ec_limbs(c);
     case CLS_ED25519: return 3 * ED_L;
     default: return 0;
   }
@@ -359,8 +359,8 @@ void run(jg_ctx* ctx, jg_batch* b) {
       ea.toks = pa.toks; ea.perm = pa.perm; ea.wave_key = pa.wave_key; ea.keys = pa.keys; ea.keyblob = pa.keyblob;
       ea.sigw = pa.sigw; ea.dig = pa.dig; ea.status = pa.status; ea.verdict_pad = (uint8_t*)B->vpad.p;
       ea.digs = rows;
-      ea.u1w = rows + (size_t)ec_windows(c) * np;
-      ea.u2w = rows + (size_t)(ec_windows(c) + ec_limbs(c)) * np;
+      ea.u1w = rows + (size_t)ec_digit_rows(c) * np;
+      ea.u2w = rows + (size_t)(ec_digit_rows(c) + ec_limbs(c)) * np;
       ea.gtab = d->gtab[c];
       ea.exc_list = (int32_t*)B->exc.p;
       ea.exc_count = (uint32_t*)B->exc_cnt.p;
@@ -492,6 +492,11 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       hk.valid = 0;
     }
   }
+  for (int c = CLS_P256; c <= CLS_P521; ++c)
+    if ((int)S.ec_idx[c].size() > ec_max_keys(c))
+      throw std::runtime_error(std::string(cls_name(c)) + ": at most " + std::to_string(ec_max_keys(c)) +
+                               " keys per table (comb tables are " +
+                               std::to_string(ec_table_words(c) * 4 >> 20) + " MiB each)");
   blob_alloc(S.blob, 0);                                      // align the host part
   for (int k : S.tab_keys) S.dk[k].tab_off += S.blob.size();
 }

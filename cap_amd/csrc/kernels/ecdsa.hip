@@ -124,7 +124,12 @@ __device__ __forceinline__ void store_digits(const EcArgs& a, int64_t p, const u
     int v1 = (int)(b1 & DM) + c1, v2 = (int)(b2 & DM) + c2;
     c1 = v1 >= (1 << (W - 1)); c2 = v2 >= (1 << (W - 1));
     v1 -= c1 << W; v2 -= c2 << W;
-    a.digs[(int64_t)w * a.npad + p] = ((uint32_t)v1 & 0xffffu) | ((uint32_t)v2 << 16);
+    if constexpr (ec_digits_packed(CV::CLS)) {
+      a.digs[(int64_t)w * a.npad + p] = ((uint32_t)v1 & 0xffffu) | ((uint32_t)v2 << 16);
+    } else {
+      a.digs[(int64_t)w * a.npad + p] = (uint32_t)v1;
+      a.digs[(int64_t)(NWIN + w) * a.npad + p] = (uint32_t)v2;
+    }
   }
 }
 
@@ -263,9 +268,15 @@ __global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
   uint32_t X[L], Y[L], Z[L];
   bool empty = true;
   for (int w = 0; w < NWIN; ++w) {
-    const uint32_t dd = a.digs[(int64_t)w * np + p];
-    const int d1 = (int)(int16_t)(dd & 0xffffu);
-    const int d2 = (int)(int16_t)(dd >> 16);
+    int d1, d2;
+    if constexpr (ec_digits_packed(CV::CLS)) {
+      const uint32_t dd = a.digs[(int64_t)w * np + p];
+      d1 = (int)(int16_t)(dd & 0xffffu);
+      d2 = (int)(int16_t)(dd >> 16);
+    } else {
+      d1 = (int)a.digs[(int64_t)w * np + p];
+      d2 = (int)a.digs[(int64_t)(NWIN + w) * np + p];
+    }
     add_window<CV>(X, Y, Z, empty, gtab, w, d1);
     add_window<CV>(X, Y, Z, empty, qtab, w, d2);
   }

@@ -32,11 +32,20 @@ constexpr int ec_order_bits(int cls) { return cls == jgk::CLS_P256 ? 256 : cls =
 // Fixed-base comb over signed w-bit digits: u = sum_w d_w 2^(W w), d_w in
 // [-2^(W-1), 2^(W-1)), so a token costs ceil((bits+1)/W) mixed additions per
 // scalar and each (key, window) holds 2^(W-1) affine multiples d 2^(W w) P.
-// Wider W trades HBM (P-256, W=16: 44.6 MB per key, 288 GB per GPU) for fewer
-// additions; digits are packed as two int16 per word, so W <= 16.
-constexpr int ec_comb_w(int cls) { return cls == jgk::CLS_P256 ? 16 : 12; }
+// Wider W trades HBM for fewer additions -- the point kernel is VALU-issue
+// bound (SQ counters, profiles/), so additions are the cost that matters:
+// P-256 at W = 20 is 13 windows (the top one holds 16 bits of u < n, so its
+// digit never carries out), 25 additions per token instead of ~32 at W = 16,
+// for 545 MB of table per key (and for G) out of 288 GB of HBM.
+constexpr int ec_comb_w(int cls) { return cls == jgk::CLS_P256 ? 20 : 12; }
 constexpr int ec_entries(int cls) { return 1 << (ec_comb_w(cls) - 1); }
 constexpr int ec_windows(int cls) { return (ec_order_bits(cls) + 1 + ec_comb_w(cls) - 1) / ec_comb_w(cls); }
+// digit rows of the scalar -> point hand-off: two int16 per word when W <= 16,
+// else one row of u1 digits then one row of u2 digits per window
+constexpr bool ec_digits_packed(int cls) { return ec_comb_w(cls) <= 16; }
+constexpr int ec_digit_rows(int cls) { return ec_digits_packed(cls) ? ec_windows(cls) : 2 * ec_windows(cls); }
+// comb-table budget: at most this many keys of a class per jg_keys_load
+constexpr int ec_max_keys(int cls) { return cls == jgk::CLS_P256 ? 256 : 65535; }
 constexpr int64_t ec_table_words(int cls) {
   return (int64_t)ec_windows(cls) * ec_entries(cls) * ec_stride(cls);
 }
