@@ -127,6 +127,7 @@ struct jg_batch {
   int sig_rows = 0, scratch_rows = 0;
   int64_t pss_tokens = 0;
   ClassRange ranges[NCLS] = {};
+  int hash_mask[NCLS] = {};       // per class: bit 0 SHA-256 present, bit 1 SHA-384/512
   uint64_t epoch = 0;
   bool timing = true;
   // timing marks of the most recent run: events are created once and
@@ -241,10 +242,13 @@ void stage(jg_ctx* ctx, jg_batch* b, const uint8_t* arena, size_t arena_len, con
   const size_t nbuck = (size_t)NCLS * (nkeys > 0 ? nkeys : 1);
   std::vector<int64_t> cnt(nbuck, 0);
   std::vector<int> tcls(ntok);
+  for (int c = 0; c < NCLS; ++c) b->hash_mask[c] = 0;
   for (size_t i = 0; i < ntok; ++i) {
     const int c = classify(ctx, toks[i]);
     if (c < 0) throw std::invalid_argument("jg_tok.key_idx out of range of the loaded key table");
     tcls[i] = c;
+    const int alg = toks[i].alg;
+    b->hash_mask[c] |= (alg == JG_RS256 || alg == JG_PS256 || alg == JG_ES256) ? 1 : 2;
     cnt[(size_t)c * nkeys + (c == CLS_REJECT ? 0 : toks[i].key_idx)]++;
   }
   // bucket order: classes 1..NCLS-1 by key, then the reject bucket
@@ -339,7 +343,7 @@ void run(jg_ctx* ctx, jg_batch* b) {
     pa.begin = r.begin;
     pa.end = r.end;
     pa.zrows = cls_rows_sig(c);
-    launch_prep(c, pa, s);
+    launch_prep(c, b->hash_mask[c], pa, s);
     mark(b, (std::string(cls_name(c)) + "_prep").c_str());
     if (c <= CLS_RSA4K) {
       RsaArgs ra{};

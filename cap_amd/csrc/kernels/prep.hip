@@ -81,7 +81,11 @@ __device__ __forceinline__ void window_words(const uint32_t* u, uint32_t i0, uin
   }
 }
 
-template <int CLS>
+// HM: hash families present in the launch range (bit 0 SHA-256, bit 1
+// SHA-384/512, from the runtime's dispatch plan).  A single-family variant
+// drops the other SHA's code and registers: the SHA-512 path alone raises the
+// kernel to ~224 VGPRs (2 waves/SIMD).
+template <int CLS, int HM>
 __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   __shared__ uint32_t slots[WAVE * SLOT];
   __shared__ uint64_t wsh[WAVE];
@@ -185,7 +189,11 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   const uint64_t mw0 = tk.off >> 2;
   const uint32_t mshift = (uint32_t)(tk.off & 3ull);
   const uint32_t len = tk.sig_in_len;
-  const int hb = CLS == CLS_ED25519 ? 512 : alg_hash_bits(alg);
+  const int hb_alg = alg_hash_bits(alg);
+  const int hb = CLS == CLS_ED25519 ? 512
+                 : HM == 1          ? 256
+                 : HM == 2          ? (hb_alg == 384 ? 384 : 512)
+                                    : hb_alg;
   uint32_t pre[16];
   uint32_t pw = 0;
   if (CLS == CLS_ED25519 && valid) {
@@ -263,17 +271,26 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
 
 }  // namespace
 
-void launch_prep(int cls, const PrepArgs& a, hipStream_t s) {
+template <int CLS>
+void launch_hm(int hm, dim3 g, dim3 b, const PrepArgs& a, hipStream_t s) {
+  switch (hm) {
+    case 1: hipLaunchKernelGGL((k_prep<CLS, 1>), g, b, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_prep<CLS, 2>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((k_prep<CLS, 3>), g, b, 0, s, a); break;
+  }
+}
+
+void launch_prep(int cls, int hash_mask, const PrepArgs& a, hipStream_t s) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   if (waves <= 0) return;
   dim3 g((unsigned)waves), b(WAVE);
   switch (cls) {
     case CLS_RSA2K: case CLS_RSA3K: case CLS_RSA4K:
-      hipLaunchKernelGGL(k_prep<CLS_RSA2K>, g, b, 0, s, a); break;
+      launch_hm<CLS_RSA2K>(hash_mask, g, b, a, s); break;
     case CLS_P256: case CLS_P384: case CLS_P521:
-      hipLaunchKernelGGL(k_prep<CLS_P256>, g, b, 0, s, a); break;
+      launch_hm<CLS_P256>(hash_mask, g, b, a, s); break;
     case CLS_ED25519:
-      hipLaunchKernelGGL(k_prep<CLS_ED25519>, g, b, 0, s, a); break;
+      hipLaunchKernelGGL((k_prep<CLS_ED25519, 2>), g, b, 0, s, a); break;
     default: break;
   }
 }

@@ -31,4 +31,5 @@ struct PrepArgs {
   int32_t zrows;              // signature rows the class's kernel reads
 };
 
-void launch_prep(int cls, const PrepArgs& a, hipStream_t s);
+// hash_mask: bit 0 = some token of the range uses SHA-256, bit 1 = SHA-384/512
+void launch_prep(int cls, int hash_mask, const PrepArgs& a, hipStream_t s);
