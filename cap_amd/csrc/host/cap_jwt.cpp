@@ -107,15 +107,64 @@ std::shared_ptr<const HdrInfo> make_hdr(std::string_view seg) {
 }
 
 struct HdrCache {
+  // a few recent segments checked by plain compare first (a key set's tokens
+  // cycle through a handful of headers), then the map
+  static constexpr int NRECENT = 8;
+  std::string recent_key[NRECENT];
+  std::shared_ptr<const HdrInfo> recent_val[NRECENT];
+  int nrecent = 0, next = 0;
   std::unordered_map<std::string, std::shared_ptr<const HdrInfo>> m;
-  std::shared_ptr<const HdrInfo> get(std::string_view seg) {
+  const std::shared_ptr<const HdrInfo>& get(std::string_view seg) {
+    for (int i = 0; i < nrecent; ++i)
+      if (recent_key[i] == seg) return recent_val[i];
     auto it = m.find(std::string(seg));
-    if (it != m.end()) return it->second;
-    if (m.size() > 4096) m.clear();
-    auto h = make_hdr(seg);
-    m.emplace(std::string(seg), h);
-    return h;
+    if (it == m.end()) {
+      if (m.size() > 4096) m.clear();
+      it = m.emplace(std::string(seg), make_hdr(seg)).first;
+    }
+    const int slot = next;
+    next = (next + 1) % NRECENT;
+    if (nrecent < NRECENT) ++nrecent;
+    recent_key[slot].assign(seg);
+    recent_val[slot] = it->second;
+    return recent_val[slot];
   }
+};
+
+// decoded length of a base64url segment with no '=' (Go RawURLEncoding)
+inline size_t b64_decoded_len(size_t n) { return n / 4 * 3 + (n % 4 == 2 ? 1 : n % 4 == 3 ? 2 : 0); }
+
+struct PhaseTimer {            // CAPJWT_TRACE=1: per-phase wall times on stderr
+  bool on;
+  std::chrono::steady_clock::time_point t0;
+  const char* what;
+  explicit PhaseTimer(const char* w) : on(std::getenv("CAPJWT_TRACE") != nullptr), t0(std::chrono::steady_clock::now()), what(w) {}
+  void lap(const char* phase) {
+    if (!on) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[capjwt] %s %-12s %8.2f ms\n", what, phase,
+                 std::chrono::duration<double, std::milli>(t1 - t0).count());
+    t0 = t1;
+  }
+};
+
+// Array whose elements are constructed and destroyed by all host threads
+// (a 1M-token batch's per-token records are ~200 MB of strings: serial
+// construction/destruction cost more than the parse itself).
+template <class T>
+struct ParArray {
+  T* p = nullptr;
+  size_t n = 0;
+  int threads = 1;
+  ParArray() = default;
+  ParArray(const ParArray&) = delete;
+  ParArray& operator=(const ParArray&) = delete;
+  void init(size_t count, int th);
+  void release();
+  ~ParArray() { release(); }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+  size_t size() const { return n; }
 };
 
 struct Tok {
@@ -132,6 +181,28 @@ struct Tok {
   uint64_t arena_off = 0;
 };
 
+template <class T>
+void ParArray<T>::init(size_t count, int th) {
+  release();
+  threads = th;
+  p = static_cast<T*>(::operator new(sizeof(T) * (count ? count : 1)));
+  n = count;
+  parallel_for(n, threads, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) new (p + i) T();
+  });
+}
+
+template <class T>
+void ParArray<T>::release() {
+  if (!p) return;
+  parallel_for(n, threads, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) p[i].~T();
+  });
+  ::operator delete(p);
+  p = nullptr;
+  n = 0;
+}
+
 void parse_one(std::string_view token, HdrCache& cache, Tok* t) {
   // compact fast path: no whitespace / non-ASCII, exactly three segments
   if (!token.empty() && token[0] != '{' && !has_go_space_or_nonascii(token)) {
@@ -144,22 +215,30 @@ void parse_one(std::string_view token, HdrCache& cache, Tok* t) {
     }
     const std::string_view hs = token.substr(0, d1), ps = token.substr(d1 + 1, d2 - d1 - 1),
                            ss = token.substr(d2 + 1);
-    auto h = cache.get(hs);
+    const std::shared_ptr<const HdrInfo>& h = cache.get(hs);
     // parseSignedCompact order: protected, payload, signature decodes, then sanitize
     if (!h->b64_ok) { t->info.parse_err = h->b64_err; return; }
     if (!b64url_decode(ps, &t->payload, &t->info.parse_err)) return;
+    // the signature bytes themselves are only needed when the segment is not
+    // canonical (the device decodes canonical base64url itself)
+    const bool sig_canon = b64url_canonical(ss);
     std::string sig;
-    if (!b64url_decode(ss, &sig, &t->info.parse_err)) return;
+    size_t siglen;
+    if (sig_canon) {
+      siglen = b64_decoded_len(ss.size());
+    } else {
+      if (!b64url_decode(ss, &sig, &t->info.parse_err)) return;
+      siglen = sig.size();
+    }
     if (!h->ok) { t->info.parse_err = h->err; return; }
     t->info.parsed = true;
     t->info.nsigs = 1;
-    t->info.sig0_len = sig.size();
+    t->info.sig0_len = siglen;
     t->info.alg = h->sig.alg;
     t->kid = h->sig.kid;
     t->alg = h->alg;
     t->verifiable = h->verifiable && t->alg != 0;
     if (!t->verifiable) return;
-    const bool sig_canon = b64url_canonical(ss);
     if (h->seg_canonical && h->needs_b64 && b64url_canonical(ps) && sig_canon) {
       t->lit = token.data();
       t->lit_len = token.size();
@@ -175,7 +254,7 @@ void parse_one(std::string_view token, HdrCache& cache, Tok* t) {
     t->si_len = (uint32_t)si.size();
     t->owned = std::move(si);
     t->owned.push_back('.');
-    const std::string sb = b64url_encode(sig);
+    const std::string sb = sig_canon ? std::string(ss) : b64url_encode(sig);
     t->sig_b64_len = (uint32_t)sb.size();
     t->owned += sb;
     return;
@@ -257,7 +336,7 @@ int key_family(const PublicKey& k) {
 // The GPU half shared by both key sets: parse, pack, verify.  `cand(t, push)`
 // pushes the key indices to try for token t.
 struct Verified {
-  std::vector<Tok> toks;
+  ParArray<Tok> toks;
   std::vector<uint8_t> any;      // some candidate key verified
 };
 
@@ -266,56 +345,68 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
                 const std::vector<size_t>* subset = nullptr) {
   const size_t n = subset ? subset->size() : tokens.size();
   auto tok_index = [&](size_t i) { return subset ? (*subset)[i] : i; };
+  PhaseTimer pt("verify");
   if (!subset) {
-    V->toks.assign(tokens.size(), Tok());
+    V->toks.init(tokens.size(), eng.threads());
     parallel_for(n, eng.threads(), [&](size_t lo, size_t hi) {
       HdrCache cache;
       for (size_t i = lo; i < hi; ++i) parse_one(tokens[i], cache, &V->toks[i]);
     });
+    pt.lap("parse");
   }
   V->any.resize(tokens.size(), 0);
-  // arena layout: prefix sums of entry sizes
+  // pass 1: candidate keys per token (counted), arena entry sizes
   std::vector<uint64_t> off(n + 1, 0);
   std::vector<uint32_t> njob(n + 1, 0);
-  std::vector<std::vector<uint16_t>> keys_of(n);
-  for (size_t i = 0; i < n; ++i) {
-    Tok& t = V->toks[tok_index(i)];
-    uint64_t sz = 0;
-    if (t.verifiable) {
-      cand(t, keys_of[i]);
-      if (!keys_of[i].empty()) sz = t.lit ? t.lit_len : t.owned.size();
+  parallel_for(n, eng.threads(), [&](size_t lo, size_t hi) {
+    std::vector<uint16_t> ks;
+    for (size_t i = lo; i < hi; ++i) {
+      const Tok& t = V->toks[tok_index(i)];
+      ks.clear();
+      if (t.verifiable) cand(t, ks);
+      njob[i + 1] = (uint32_t)ks.size();
+      off[i + 1] = ks.empty() ? 0 : (t.lit ? t.lit_len : t.owned.size());
     }
-    t.arena_off = off[i];
-    off[i + 1] = off[i] + sz;
-    njob[i + 1] = njob[i] + (uint32_t)keys_of[i].size();
+  });
+  for (size_t i = 0; i < n; ++i) {                  // prefix sums (arena layout, job slots)
+    off[i + 1] += off[i];
+    njob[i + 1] += njob[i];
   }
   const size_t total_jobs = njob[n];
+  pt.lap("plan");
   if (total_jobs == 0) return;
   const uint64_t arena_len = off[n];
   uint8_t* arena = eng.arena_buffer(arena_len);
   std::vector<jg_tok> jobs(total_jobs);
   std::vector<uint32_t> job_tok(total_jobs);
+  // pass 2: pack the arena and the jobs
   parallel_for(n, eng.threads(), [&](size_t lo, size_t hi) {
+    std::vector<uint16_t> ks;
     for (size_t i = lo; i < hi; ++i) {
-      if (keys_of[i].empty()) continue;
-      const Tok& t = V->toks[tok_index(i)];
+      if (njob[i + 1] == njob[i]) continue;
+      Tok& t = V->toks[tok_index(i)];
+      t.arena_off = off[i];
       if (t.lit) std::memcpy(arena + off[i], t.lit, t.lit_len);
       else std::memcpy(arena + off[i], t.owned.data(), t.owned.size());
-      for (size_t k = 0; k < keys_of[i].size(); ++k) {
+      ks.clear();
+      cand(t, ks);
+      for (size_t k = 0; k < ks.size(); ++k) {
         jg_tok& j = jobs[njob[i] + k];
         j.off = off[i];
         j.sig_in_len = t.si_len;
         j.sig_rel_off = t.si_len + 1;
         j.sig_b64_len = t.sig_b64_len;
-        j.key_idx = keys_of[i][k];
+        j.key_idx = ks[k];
         j.alg = (uint8_t)t.alg;
         j.flags = 0;
         job_tok[njob[i] + k] = (uint32_t)tok_index(i);
       }
     }
   });
+  pt.lap("pack");
   std::vector<uint8_t> verdict(total_jobs, 0);
   eng.verify(arena, arena_len, jobs.data(), total_jobs, verdict.data());
+  pt.lap("gpu");
   for (size_t j = 0; j < total_jobs; ++j)
     if (verdict[j] == JG_ACCEPT) V->any[job_tok[j]] = 1;
 }
@@ -338,6 +429,7 @@ class StaticKeySet final : public KeySet {
         if (fam_[k] == fam) out.push_back((uint16_t)k);
     });
     std::vector<Result> res(tokens.size());
+    PhaseTimer pt("static");
     parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         const Tok& t = V.toks[i];
@@ -354,9 +446,12 @@ class StaticKeySet final : public KeySet {
         }
       }
     });
+    pt.lap("payload-json");
     if (info) {
       info->resize(tokens.size());
-      for (size_t i = 0; i < tokens.size(); ++i) (*info)[i] = std::move(V.toks[i].info);
+      parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) (*info)[i] = std::move(V.toks[i].info);
+      });
     }
     return res;
   }
@@ -422,6 +517,7 @@ class JSONWebKeySet final : public KeySet {
       refreshed = true;
       if (refresh(&fetch_err)) gpu_verify(eng_, tokens, &V, cand, &miss);
     }
+    PhaseTimer pt("jwks");
     parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         const Tok& t = V.toks[i];
@@ -437,9 +533,12 @@ class JSONWebKeySet final : public KeySet {
         else { r.claims = json::Value(); r.err = jerr; }
       }
     });
+    pt.lap("payload-json");
     if (info) {
       info->resize(tokens.size());
-      for (size_t i = 0; i < tokens.size(); ++i) (*info)[i] = std::move(V.toks[i].info);
+      parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) (*info)[i] = std::move(V.toks[i].info);
+      });
     }
     return res;
   }
@@ -690,10 +789,18 @@ Result validate_claims(const json::Value& all_claims, const TokenInfo& info, con
   bool has_iat = false, has_exp = false, has_nbf = false;
   int64_t iat = 0, exp = 0, nbf = 0;
   if (all_claims.kind == json::Value::Object) {
-    std::vector<const json::Member*> ms;
-    for (const auto& m : all_claims.obj) ms.push_back(&m);
-    std::sort(ms.begin(), ms.end(), [](const json::Member* a, const json::Member* b) { return a->first < b->first; });
-    for (const json::Member* m : ms) {
+    const json::Member* small[32];
+    std::vector<const json::Member*> big;
+    const json::Member** ms = small;
+    const size_t nm = all_claims.obj.size();
+    if (nm > 32) {
+      big.resize(nm);
+      ms = big.data();
+    }
+    for (size_t k = 0; k < nm; ++k) ms[k] = &all_claims.obj[k];
+    std::sort(ms, ms + nm, [](const json::Member* a, const json::Member* b) { return a->first < b->first; });
+    for (size_t mk = 0; mk < nm; ++mk) {
+      const json::Member* m = ms[mk];
       const json::Value& v = m->second;
       std::string* sfield = fold_eq(m->first, "ISS") ? &iss : fold_eq(m->first, "SUB") ? &sub
                             : fold_eq(m->first, "JTI") ? &jti : nullptr;
@@ -790,6 +897,13 @@ Result validate_claims(const json::Value& all_claims, const TokenInfo& info, con
   return r;
 }
 
+void release_results(std::vector<Result>& rs) {
+  parallel_for(rs.size(), host_threads(), [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) rs[i] = Result();
+  });
+  std::vector<Result>().swap(rs);
+}
+
 Result Validator::Validate(std::string_view token, const Expected& expected) {
   return ValidateBatch({token}, expected)[0];
 }
@@ -797,6 +911,7 @@ Result Validator::Validate(std::string_view token, const Expected& expected) {
 std::vector<Result> Validator::ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected) {
   std::vector<TokenInfo> info;
   std::vector<Result> sig = ks_->verify_batch(tokens, &info);
+  PhaseTimer pt("validate");
   const int64_t now = expected.has_now ? expected.now_unix_ns : wall_now_ns();
   std::vector<Result> out(tokens.size());
   parallel_for(tokens.size(), host_threads(), [&](size_t lo, size_t hi) {
@@ -809,6 +924,12 @@ std::vector<Result> Validator::ValidateBatch(const std::vector<std::string_view>
       if (out[i].ok) out[i].claims = std::move(sig[i].claims);
     }
   });
+  pt.lap("claims");
+  release_results(sig);
+  parallel_for(info.size(), host_threads(), [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) info[i] = TokenInfo();
+  });
+  pt.lap("release");
   return out;
 }
 

@@ -144,6 +144,10 @@ Result validate_claims(const json::Value& all_claims, const TokenInfo& info, con
 
 bool ParsePublicKeyPEM(std::string_view data, PublicKey* out, std::string* err);
 
+// Frees a large result vector with all host threads (1M claims maps are ~10M
+// allocations; a serial free costs more than the batch's parse).
+void release_results(std::vector<Result>& rs);
+
 // Host threads used by batch parsing / claims (CAPJWT_HOST_THREADS, default
 // min(hardware threads, 16)).
 int host_threads();

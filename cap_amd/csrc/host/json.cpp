@@ -145,7 +145,7 @@ struct Reader {
           case 'r': out->push_back('\r'); break;
           case 't': out->push_back('\t'); break;
           case 'u': {
-            uint32_t r;
+            uint32_t r = 0;
             if (!u4(&r)) return false;
             if (r >= 0xD800 && r < 0xE000) {
               // utf16 surrogate: valid only as a high+low pair written as two escapes

@@ -6,6 +6,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstring>
+
 #include "cap_jwt.hpp"
 
 namespace py = pybind11;
@@ -60,14 +62,16 @@ std::vector<std::string_view> views(const std::vector<std::string>& s) {
 
 // newline-separated token blob -> views (end-to-end benchmark input, no
 // per-token Python objects)
-std::vector<std::string_view> split_lines(const std::string& blob) {
+std::vector<std::string_view> split_lines(const char* p, size_t n) {
   std::vector<std::string_view> v;
-  size_t s = 0;
-  for (size_t i = 0; i <= blob.size(); ++i)
-    if (i == blob.size() || blob[i] == '\n') {
-      if (i > s) v.emplace_back(blob.data() + s, i - s);
-      s = i + 1;
-    }
+  v.reserve(n / 256 + 1);
+  const char* end = p + n;
+  while (p < end) {
+    const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(end - p)));
+    const char* e = nl ? nl : end;
+    if (e > p) v.emplace_back(p, (size_t)(e - p));
+    p = e + 1;
+  }
   return v;
 }
 
@@ -330,14 +334,19 @@ PYBIND11_MODULE(_capjwt_host, m) {
       .def("validate_blob", [](PyValidator& s, py::bytes blob, const Expected& e) {
         // end-to-end throughput entry: newline-separated tokens in, per-token
         // accept bytes out (claims stay on the C++ side)
-        std::string b = blob;
+        // zero-copy: the bytes object is immutable and stays referenced by the
+        // caller for the duration of the call
+        char* bp = nullptr;
+        Py_ssize_t bn = 0;
+        if (PyBytes_AsStringAndSize(blob.ptr(), &bp, &bn) != 0) throw py::error_already_set();
         std::string ok;
         {
           py::gil_scoped_release rel;
-          auto toks = split_lines(b);
+          auto toks = split_lines(bp, (size_t)bn);
           auto rs = s.v->ValidateBatch(toks, e);
           ok.resize(rs.size());
           for (size_t i = 0; i < rs.size(); ++i) ok[i] = rs[i].ok ? 1 : 0;
+          release_results(rs);
         }
         return py::bytes(ok);
       });
