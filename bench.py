@@ -406,8 +406,8 @@ def load_traffic(kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--tokens", type=int, default=1 << 20, help="tokens per GPU per step")
     ap.add_argument("--pool", type=int, default=1 << 17, help="unique signed tokens (replicated)")
     ap.add_argument("--no-rs256", action="store_true")

@@ -134,7 +134,7 @@ __device__ __forceinline__ void store_digits(const EcArgs& a, int64_t p, const u
 }
 
 // Batched scalar stage (Montgomery's trick): thread i owns the B tokens
-// p_j = begin + i + j*S and pays ONE Fermat inversion for all of them:
+// p_j = begin + i + j*S and pays ONE (safegcd) inversion for all of them:
 //   pass 1: c_j = s_0 ... s_j (Montgomery), c_j and s_j parked in the u1/u2 rows
 //   inv = c_{B-1}^-1
 //   pass 2 (j descending): w_j = inv * c_{j-1}, inv *= s_j;

@@ -43,6 +43,13 @@ __constant__ static const uint64_t K512[80] = {
   0x431d67c49c100d4cULL,0x4cc5d4becb3e42b6ULL,0x597f299cfc657e2aULL,0x5fcb6fab3ad6faecULL,0x6c44198c4a475817ULL};
 
 SHD uint32_t rotr32(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+// a ^ b ^ c as one gfx950 v_bitop3_b32 (truth table 0x96); LLVM emits two
+// v_xor_b32 for the plain expression
+SHD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+SHD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+  return ((uint64_t)xor3((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+         xor3((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
 // 64-bit rotate as two v_alignbit_b32 on the halves (n is a compile-time
 // constant at every call site): 2 VALU instead of two 64-bit shifts + 2 ors
 SHD uint64_t rotr64(uint64_t x, int n) {
@@ -107,15 +114,15 @@ SHD void sha256_compress(uint32_t h[8], uint32_t w[16]) {
       wi = w[i];
     } else {
       const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
       wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
       w[i & 15] = wi;
     }
-    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t S1 = xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
     const uint32_t ch = (e & f) ^ (~e & g);
     const uint32_t t1 = hh + S1 + ch + K256[i] + wi;
-    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t S0 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
     const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
     hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }
@@ -154,15 +161,15 @@ SHD void sha512_compress(uint64_t h[8], uint64_t w[16]) {
       wi = w[i];
     } else {
       const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
       wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
       w[i & 15] = wi;
     }
-    const uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+    const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
     const uint64_t ch = (e & f) ^ (~e & g);
     const uint64_t t1 = hh + S1 + ch + K512[i] + wi;
-    const uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+    const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
     const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
     hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }

@@ -87,11 +87,22 @@ def test_mont_mul_sqr_inv(tk, fid):
             v = from_limbs(o)
             assert v < 2 * m and v % m == fn(x, y) % m, (op, x, y)
     # inverse of Montgomery-form values
-    xs2 = [rng.randrange(1, m) for _ in range(64)]
-    xm = [x * R % m for x in xs2]
+    # (safegcd: random values plus the small / near-m / power-of-two / lazy
+    # inputs that stress the divstep sign handling and the final normalisation)
+    specials = [1, 2, 3, m - 1, m - 2, (m + 1) // 2, m // 3]
+    specials += [1 << k for k in range(1, m.bit_length() - 1, 37)]
+    specials += [m - (1 << k) for k in range(1, m.bit_length() - 1, 41)]
+    xs2 = [rng.randrange(1, m) for _ in range(1024)]
+    xm = [x * R % m for x in xs2] + [s * R % m for s in specials]
+    xs2 += specials
+    xm = [v + (m if i % 5 == 0 and v + m < R else 0) for i, v in enumerate(xm)]
     out = run_field(tk, fid, 2, xm, xm)
     for x, o in zip(xs2, out):
-        assert from_limbs(o) % m == pow(x, -1, m) * R % m
+        assert from_limbs(o) % m == pow(x, -1, m) * R % m, x
+    out = run_field(tk, fid, 2, [0], [0])
+    assert from_limbs(out[0]) % m == 0
+    xs2 = xs2[:64]
+    xm = [x * R % m for x in xs2]
     # to / from Montgomery
     out = run_field(tk, fid, 3, xs2, xs2)
     assert all(from_limbs(o) % m == x * R % m for x, o in zip(xs2, out))
