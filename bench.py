@@ -53,13 +53,14 @@ def p256_point_mads_per_token():
     token: 28-bit limbs, L = 10; Montgomery product = L^2 (mul) or L(L+1)/2 (sqr)
     + L * 4 for the reduction (p + 1 has 4 non-zero limbs above limb 0, mp.hpp);
     mixed addition = 8 mul + 3 sqr + 3 value folds (6 non-zero limbs of
-    2^256 mod p); signed 20-bit comb digits (ecdsa.hpp ec_comb_w): 13 windows
-    non-zero w.p. 1 - 2^-20 (the top window never carries) for u1 and u2, the
-    first addition an assignment; final check 1 sqr + 2 mul."""
+    2^256 mod p); signed comb digits (ecdsa.hpp ec_comb_w): 11 windows of 24
+    bits for u1 (generator table) and 13 of 20 bits for u2 (key table), each
+    non-zero w.p. 1 - 2^-W (the top windows never carry), the first addition an
+    assignment; final check 1 sqr + 2 mul."""
     L, red, fold = 10, 10 * 4, 6
     mul, sqr = L * L + red, L * (L + 1) // 2 + red
     madd = 8 * mul + 3 * sqr + 3 * fold
-    adds = 2 * 13 * (1 - 2.0 ** -20) - 1
+    adds = 11 * (1 - 2.0 ** -24) + 13 * (1 - 2.0 ** -20) - 1
     return adds * madd + sqr + 2 * mul
 
 

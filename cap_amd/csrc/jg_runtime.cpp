@@ -467,7 +467,7 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       K.cls = cls;
       K.kbytes = cb;
       K.aux_off = blob_alloc(S.blob, 2 * L);
-      K.tab_off = tab_alloc(S, i, (uint64_t)ec_table_words(cls));
+      K.tab_off = tab_alloc(S, i, (uint64_t)ec_table_words(cls, false));
       const size_t cl = k.coord_len > 0 ? (size_t)k.coord_len : 0;
       // crypto/ecdsa pointFromAffine: coordinates must fit the curve's bit size
       bool ok = k.x && k.y && cl > 0 && bitlen_be(k.x, cl) <= (cls == CLS_P521 ? 521 : cb * 8) &&
@@ -500,7 +500,7 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
     if ((int)S.ec_idx[c].size() > ec_max_keys(c))
       throw std::runtime_error(std::string(cls_name(c)) + ": at most " + std::to_string(ec_max_keys(c)) +
                                " keys per table (comb tables are " +
-                               std::to_string(ec_table_words(c) * 4 >> 20) + " MiB each)");
+                               std::to_string(ec_table_words(c, false) * 4 >> 20) + " MiB each)");
   blob_alloc(S.blob, 0);                                      // align the host part
   for (int k : S.tab_keys) S.dk[k].tab_off += S.blob.size();
 }
@@ -509,7 +509,7 @@ void ensure_tables(Device* d, const StagedKeys& S) {
   HIPCHK(hipSetDevice(d->id));
   for (int c = CLS_P256; c <= CLS_P521; ++c) {
     if (S.ec_idx[c].empty() || d->gtab[c]) continue;
-    HIPCHK(hipMalloc(&d->gtab[c], sizeof(uint32_t) * ec_table_words(c)));
+    HIPCHK(hipMalloc(&d->gtab[c], sizeof(uint32_t) * ec_table_words(c, true)));
     launch_ec_gtable(c, d->gtab[c], d->stream);
   }
   if (!S.ed_idx.empty() && !d->btab) {

@@ -5,7 +5,7 @@
 //   k_ec_scalar_batch : r, s in [1, n-1] (sizes from the alg, curve from the
 //                 key), e = leftmost bits of H, w = s^-1 (one inversion per B
 //                 tokens), u1 = e w, u2 = r w (mod n), recoded to signed W-bit
-//                 digits (W = ec_comb_w: 16 for P-256, 12 for P-384/P-521)
+//                 digits (W = ec_comb_w: generator 24 / key 20 for P-256, 20 / 16 above)
 //   k_ec_point  : R = u1 G + u2 Q as a sum of one precomputed affine multiple of
 //                 G and one of Q per window (comb tables in HBM: entries
 //                 d * 2^(W w) * P, d = 1..2^(W-1)), mixed Jacobian+affine
@@ -109,28 +109,30 @@ __device__ __forceinline__ bool ec_scalar_inputs(const EcArgs& a, int64_t p, uin
 }
 
 // Signed W-bit recoding: u = sum_w d_w 2^(W w), d_w in [-2^(W-1), 2^(W-1)),
-// stored as two int16 per window row (u1 digit low, u2 digit high).
-template <class CV>
-__device__ __forceinline__ void store_digits(const EcArgs& a, int64_t p, const uint32_t* u1, const uint32_t* u2) {
+// one int32 row per window starting at digit row `row0`.
+template <class CV, int W, int NWIN>
+__device__ __forceinline__ void store_digit_rows(const EcArgs& a, int64_t p, const uint32_t* u, int row0) {
   constexpr int L = CV::Fn::L;
-  constexpr int W = ec_comb_w(CV::CLS), NWIN = ec_windows(CV::CLS);
   constexpr uint32_t DM = (1u << W) - 1u;
-  int c1 = 0, c2 = 0;
+  int c = 0;
 #pragma unroll
   for (int w = 0; w < NWIN; ++w) {
     const int bit = W * w, q = bit / MP_W, sh = bit % MP_W;
-    uint32_t b1 = q < L ? (u1[q] >> sh) : 0u, b2 = q < L ? (u2[q] >> sh) : 0u;
-    if (sh > MP_W - W && q + 1 < L) { b1 |= u1[q + 1] << (MP_W - sh); b2 |= u2[q + 1] << (MP_W - sh); }
-    int v1 = (int)(b1 & DM) + c1, v2 = (int)(b2 & DM) + c2;
-    c1 = v1 >= (1 << (W - 1)); c2 = v2 >= (1 << (W - 1));
-    v1 -= c1 << W; v2 -= c2 << W;
-    if constexpr (ec_digits_packed(CV::CLS)) {
-      a.digs[(int64_t)w * a.npad + p] = ((uint32_t)v1 & 0xffffu) | ((uint32_t)v2 << 16);
-    } else {
-      a.digs[(int64_t)w * a.npad + p] = (uint32_t)v1;
-      a.digs[(int64_t)(NWIN + w) * a.npad + p] = (uint32_t)v2;
-    }
+    uint32_t b = q < L ? (u[q] >> sh) : 0u;
+    if (sh > MP_W - W && q + 1 < L) b |= u[q + 1] << (MP_W - sh);
+    int v = (int)(b & DM) + c;
+    c = v >= (1 << (W - 1));
+    v -= c << W;
+    a.digs[(int64_t)(row0 + w) * a.npad + p] = (uint32_t)v;
   }
+}
+
+template <class CV>
+__device__ __forceinline__ void store_digits(const EcArgs& a, int64_t p, const uint32_t* u1, const uint32_t* u2) {
+  constexpr int WG = ec_comb_w(CV::CLS, true), NG = ec_windows(CV::CLS, true);
+  constexpr int WQ = ec_comb_w(CV::CLS, false), NQ = ec_windows(CV::CLS, false);
+  store_digit_rows<CV, WG, NG>(a, p, u1, 0);
+  store_digit_rows<CV, WQ, NQ>(a, p, u2, NG);
 }
 
 // Batched scalar stage (Montgomery's trick): thread i owns the B tokens
@@ -228,11 +230,11 @@ __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, cons
   mp::sub<Fp>(Y, Y, t); mp::freduce<Fp>(Y);
 }
 
-template <class CV>
+template <class CV, bool GEN>
 __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z, bool& empty,
                                            const uint32_t* __restrict__ tab, int w, int d) {
   using Fp = typename CV::Fp;
-  constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS), NE = ec_entries(CV::CLS);
+  constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS), NE = ec_entries(CV::CLS, GEN);
   if (d == 0) return;
   const int ad = d < 0 ? -d : d;
   const uint32_t* ent = tab + ((int64_t)w * NE + (ad - 1)) * STRIDE;
@@ -255,7 +257,8 @@ __global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
   using Fp = typename CV::Fp;
   using Fn = typename CV::Fn;
   constexpr int L = Fp::L;
-  constexpr int NWIN = ec_windows(CV::CLS);
+  constexpr int NG = ec_windows(CV::CLS, true), NQ = ec_windows(CV::CLS, false);
+  constexpr int NWIN = NG > NQ ? NG : NQ;
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
   const int32_t t = a.perm[p];
@@ -268,17 +271,8 @@ __global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
   uint32_t X[L], Y[L], Z[L];
   bool empty = true;
   for (int w = 0; w < NWIN; ++w) {
-    int d1, d2;
-    if constexpr (ec_digits_packed(CV::CLS)) {
-      const uint32_t dd = a.digs[(int64_t)w * np + p];
-      d1 = (int)(int16_t)(dd & 0xffffu);
-      d2 = (int)(int16_t)(dd >> 16);
-    } else {
-      d1 = (int)a.digs[(int64_t)w * np + p];
-      d2 = (int)a.digs[(int64_t)(NWIN + w) * np + p];
-    }
-    add_window<CV>(X, Y, Z, empty, gtab, w, d1);
-    add_window<CV>(X, Y, Z, empty, qtab, w, d2);
+    if (w < NG) add_window<CV, true>(X, Y, Z, empty, gtab, w, (int)a.digs[(int64_t)w * np + p]);
+    if (w < NQ) add_window<CV, false>(X, Y, Z, empty, qtab, w, (int)a.digs[(int64_t)(NG + w) * np + p]);
   }
   if (empty) { a.verdict_pad[p] = 0; return; }           // R = infinity (unreachable: u2 != 0)
   uint32_t zc[L];
@@ -510,24 +504,24 @@ __device__ void store_affine(uint32_t* out, const JPt<typename CV::Fp>& P) {
 }
 
 // window base 2^(W w) * B (= entry d = 1 of window w), affine Montgomery form
-template <class CV>
+template <class CV, int W>
 __device__ void window_base(uint32_t* out, const uint32_t* bx, const uint32_t* by, int w) {
   using Fp = typename CV::Fp;
   JPt<Fp> P;
   affine_point<CV>(P, bx, by);
-  for (int i = 0; i < ec_comb_w(CV::CLS) * w; ++i) jdbl<CV>(P, P);
+  for (int i = 0; i < W * w; ++i) jdbl<CV>(P, P);
   store_affine<CV>(out, P);
 }
 
 // entry d * base (d < 2^W), affine Montgomery form
-template <class CV>
+template <class CV, int W>
 __device__ void table_entry(uint32_t* out, const uint32_t* base, int d) {
   using Fp = typename CV::Fp;
   constexpr int L = Fp::L;
   JPt<Fp> P, acc;
   affine_point<CV>(P, base, base + L);
   acc.inf = true;
-  for (int bit = ec_comb_w(CV::CLS) - 1; bit >= 0; --bit) {
+  for (int bit = W - 1; bit >= 0; --bit) {
     jdbl<CV>(acc, acc);
     if ((d >> bit) & 1) jadd<CV>(acc, acc, P);
   }
@@ -538,45 +532,49 @@ __device__ void table_entry(uint32_t* out, const uint32_t* base, int d) {
 // bases (entry 1), then thread per (key, entry >= 2) from its window's base.
 template <class CV>
 __global__ void k_ec_table_base_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
-  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS), STRIDE = ec_stride(CV::CLS);
+  constexpr int W = ec_comb_w(CV::CLS, false), NWIN = ec_windows(CV::CLS, false);
+  constexpr int NE = ec_entries(CV::CLS, false), STRIDE = ec_stride(CV::CLS);
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (k >= n || w >= NWIN) return;
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
   const uint32_t* aux = blob + K.aux_off;
-  window_base<CV>(blob + K.tab_off + (int64_t)w * NE * STRIDE, aux, aux + CV::Fp::L, w);
+  window_base<CV, W>(blob + K.tab_off + (int64_t)w * NE * STRIDE, aux, aux + CV::Fp::L, w);
 }
 
 template <class CV>
 __global__ void k_ec_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
-  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS), STRIDE = ec_stride(CV::CLS);
+  constexpr int W = ec_comb_w(CV::CLS, false), NWIN = ec_windows(CV::CLS, false);
+  constexpr int NE = ec_entries(CV::CLS, false), STRIDE = ec_stride(CV::CLS);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (k >= n || e >= NWIN * NE || e % NE == 0) return;
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
   uint32_t* tab = blob + K.tab_off;
-  table_entry<CV>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
+  table_entry<CV, W>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
 }
 
 template <class CV>
 __global__ void k_ec_table_base_g(uint32_t* tab) {
-  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS), STRIDE = ec_stride(CV::CLS);
+  constexpr int W = ec_comb_w(CV::CLS, true), NWIN = ec_windows(CV::CLS, true);
+  constexpr int NE = ec_entries(CV::CLS, true), STRIDE = ec_stride(CV::CLS);
   using Fp = typename CV::Fp;
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= NWIN) return;
   uint32_t gx[Fp::L], gy[Fp::L];
   mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
-  window_base<CV>(tab + (int64_t)w * NE * STRIDE, gx, gy, w);
+  window_base<CV, W>(tab + (int64_t)w * NE * STRIDE, gx, gy, w);
 }
 
 template <class CV>
 __global__ void k_ec_table_g(uint32_t* tab) {
-  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS), STRIDE = ec_stride(CV::CLS);
+  constexpr int W = ec_comb_w(CV::CLS, true), NWIN = ec_windows(CV::CLS, true);
+  constexpr int NE = ec_entries(CV::CLS, true), STRIDE = ec_stride(CV::CLS);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= NWIN * NE || e % NE == 0) return;
-  table_entry<CV>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
+  table_entry<CV, W>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
 }
 
 template <class CV>
@@ -598,7 +596,7 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
 
 template <class CV>
 void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
-  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS);
+  constexpr int NWIN = ec_windows(CV::CLS, false), NE = ec_entries(CV::CLS, false);
   dim3 b(64);
   hipLaunchKernelGGL(k_ec_keyprep<CV>, dim3((n + 63) / 64), b, 0, s, keys, blob, idx, n);
   hipLaunchKernelGGL(k_ec_table_base_keys<CV>, dim3((NWIN + 63) / 64, n), b, 0, s, keys, blob, idx, n);
@@ -607,7 +605,7 @@ void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipS
 
 template <class CV>
 void gtable_chain(uint32_t* tab, hipStream_t s) {
-  constexpr int NWIN = ec_windows(CV::CLS), NE = ec_entries(CV::CLS);
+  constexpr int NWIN = ec_windows(CV::CLS, true), NE = ec_entries(CV::CLS, true);
   hipLaunchKernelGGL(k_ec_table_base_g<CV>, dim3((NWIN + 63) / 64), dim3(64), 0, s, tab);
   hipLaunchKernelGGL(k_ec_table_g<CV>, dim3((NWIN * NE + 63) / 64), dim3(64), 0, s, tab);
 }

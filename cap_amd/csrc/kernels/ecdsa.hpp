@@ -16,7 +16,7 @@ struct EcArgs {
   const uint32_t* dig;        // digest rows (big-endian words)
   uint8_t* status;
   uint8_t* verdict_pad;
-  uint32_t* digs;             // per window: packed signed digits (d1 | d2 << 16), int16 each
+  uint32_t* digs;             // signed digit rows: u1 windows (generator) then u2 windows (key)
   uint32_t* u1w;              // u1, u2 canonical 28-bit limb rows (exact path)
   uint32_t* u2w;
   const uint32_t* gtab;       // comb table of the generator for this curve
@@ -29,25 +29,33 @@ struct EcArgs {
 constexpr int ec_limbs(int cls) { return cls == jgk::CLS_P256 ? 10 : cls == jgk::CLS_P384 ? 15 : 20; }
 constexpr int ec_stride(int cls) { return (2 * ec_limbs(cls) + 3) & ~3; }
 constexpr int ec_order_bits(int cls) { return cls == jgk::CLS_P256 ? 256 : cls == jgk::CLS_P384 ? 384 : 521; }
-// Fixed-base comb over signed w-bit digits: u = sum_w d_w 2^(W w), d_w in
+// Fixed-base comb over signed W-bit digits: u = sum_w d_w 2^(W w), d_w in
 // [-2^(W-1), 2^(W-1)), so a token costs ceil((bits+1)/W) mixed additions per
-// scalar and each (key, window) holds 2^(W-1) affine multiples d 2^(W w) P.
+// scalar and each (point, window) holds 2^(W-1) affine multiples d 2^(W w) P.
 // Wider W trades HBM for fewer additions -- the point kernel is VALU-issue
-// bound (SQ counters, profiles/), so additions are the cost that matters:
-// P-256 at W = 20 is 13 windows (the top one holds 16 bits of u < n, so its
-// digit never carries out), 25 additions per token instead of ~32 at W = 16,
-// for 545 MB of table per key (and for G) out of 288 GB of HBM.
-constexpr int ec_comb_w(int cls) { return cls == jgk::CLS_P256 ? 20 : 12; }
-constexpr int ec_entries(int cls) { return 1 << (ec_comb_w(cls) - 1); }
-constexpr int ec_windows(int cls) { return (ec_order_bits(cls) + 1 + ec_comb_w(cls) - 1) / ec_comb_w(cls); }
-// digit rows of the scalar -> point hand-off: two int16 per word when W <= 16,
-// else one row of u1 digits then one row of u2 digits per window
-constexpr bool ec_digits_packed(int cls) { return ec_comb_w(cls) <= 16; }
-constexpr int ec_digit_rows(int cls) { return ec_digits_packed(cls) ? ec_windows(cls) : 2 * ec_windows(cls); }
+// bound (SQ counters, profiles/), so additions are the cost that matters.  The
+// generator's table is built once per engine and shared by every key, so it
+// gets the wider window (gen = true); per-key tables stay narrower so a JWKS of
+// hundreds of keys still fits:
+//   P-256: G W=24 (11 windows, 7.4 GB), keys W=20 (13 windows, 545 MB each):
+//          23 additions per token (25 with W=20/20, ~32 with 16/16)
+//   P-384: G W=20 (20 windows, 1.3 GB), keys W=16 (25 windows, 105 MB): 44 (65 at 12/12)
+//   P-521: G W=20 (27 windows, 2.3 GB), keys W=16 (33 windows, 173 MB): 59 (87 at 12/12)
+// The top window of each scalar (u < n) never carries out of the last digit.
+constexpr int ec_comb_w(int cls, bool gen) {
+  return cls == jgk::CLS_P256 ? (gen ? 24 : 20) : (gen ? 20 : 16);
+}
+constexpr int ec_entries(int cls, bool gen) { return 1 << (ec_comb_w(cls, gen) - 1); }
+constexpr int ec_windows(int cls, bool gen) {
+  return (ec_order_bits(cls) + 1 + ec_comb_w(cls, gen) - 1) / ec_comb_w(cls, gen);
+}
+// digit rows of the scalar -> point hand-off: one int32 row per window, the
+// u1 (generator) digits first, then the u2 (key) digits
+constexpr int ec_digit_rows(int cls) { return ec_windows(cls, true) + ec_windows(cls, false); }
 // comb-table budget: at most this many keys of a class per jg_keys_load
-constexpr int ec_max_keys(int cls) { return cls == jgk::CLS_P256 ? 256 : 65535; }
-constexpr int64_t ec_table_words(int cls) {
-  return (int64_t)ec_windows(cls) * ec_entries(cls) * ec_stride(cls);
+constexpr int ec_max_keys(int cls) { return 256; }
+constexpr int64_t ec_table_words(int cls, bool gen) {
+  return (int64_t)ec_windows(cls, gen) * ec_entries(cls, gen) * ec_stride(cls);
 }
 
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);

@@ -46,6 +46,14 @@ DEF_KERNEL(k_fma_f64,
   asm volatile("v_fma_f64 %0, %0, %1, %0" : "+v"(d[k]) : "v"(db)))
 DEF_KERNEL(k_lshl_add_u64,
   asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(c[k]) : "v"((uint64_t)b)))
+DEF_KERNEL(k_lshrrev_b64,
+  asm volatile("v_lshrrev_b64 %0, 28, %0" : "+v"(c[k])))
+DEF_KERNEL(k_and_b32,
+  asm volatile("v_and_b32 %0, %0, %1" : "+v"(a[k]) : "v"(b)))
+DEF_KERNEL(k_alignbit_b32,
+  asm volatile("v_alignbit_b32 %0, %0, %1, 28" : "+v"(a[k]) : "v"(b)))
+DEF_KERNEL(k_bitop3_b32,
+  asm volatile("v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96" : "+v"(a[k]) : "v"(b)))
 DEF_KERNEL(k_mad_u64_u32_dep,
   asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(c[0]) : "v"(a[k]), "v"(b) : "vcc"))
 
@@ -75,6 +83,8 @@ int main() {
     {"v_add_co_u32", k_add_co_u32}, {"v_addc_co_u32", k_addc_co_u32},
     {"v_add3_u32", k_add3_u32}, {"v_lshl_add_u32", k_lshl_add_u32},
     {"v_lshl_add_u64", k_lshl_add_u64}, {"v_fma_f64", k_fma_f64},
+    {"v_lshrrev_b64", k_lshrrev_b64}, {"v_and_b32", k_and_b32},
+    {"v_alignbit_b32", k_alignbit_b32}, {"v_bitop3_b32", k_bitop3_b32},
   };
   int occ[] = {1, 2, 4, 8};  // waves per SIMD
   uint32_t* out; hipMalloc(&out, 256 * 8 * 4 * 256 * sizeof(uint32_t) * 2);
