@@ -484,7 +484,7 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       K.cls = CLS_ED25519;
       K.kbytes = 32;
       K.aux_off = blob_alloc(S.blob, 8 + 2 * ED_L);
-      K.tab_off = tab_alloc(S, i, (uint64_t)ED_TABLE_WORDS);
+      K.tab_off = tab_alloc(S, i, (uint64_t)ed_table_words(false));
       // crypto/ed25519.Verify panics on len(pub) != 32; go-jose never hands it one
       const bool ok = k.x && k.coord_len == 32;
       if (ok) std::memcpy(S.blob.data() + K.aux_off, k.x, 32);
@@ -501,6 +501,9 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       throw std::runtime_error(std::string(cls_name(c)) + ": at most " + std::to_string(ec_max_keys(c)) +
                                " keys per table (comb tables are " +
                                std::to_string(ec_table_words(c, false) * 4 >> 20) + " MiB each)");
+  if ((int)S.ed_idx.size() > ED_MAX_KEYS)
+    throw std::runtime_error("Ed25519: at most " + std::to_string(ED_MAX_KEYS) + " keys per table (comb tables are " +
+                             std::to_string(ed_table_words(false) * 4 >> 20) + " MiB each)");
   blob_alloc(S.blob, 0);                                      // align the host part
   for (int k : S.tab_keys) S.dk[k].tab_off += S.blob.size();
 }
@@ -513,7 +516,7 @@ void ensure_tables(Device* d, const StagedKeys& S) {
     launch_ec_gtable(c, d->gtab[c], d->stream);
   }
   if (!S.ed_idx.empty() && !d->btab) {
-    HIPCHK(hipMalloc(&d->btab, sizeof(uint32_t) * ED_TABLE_WORDS));
+    HIPCHK(hipMalloc(&d->btab, sizeof(uint32_t) * ed_table_words(true)));
     launch_ed_btable(d->btab, d->stream);
   }
 }

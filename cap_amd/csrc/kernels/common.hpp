@@ -48,7 +48,6 @@ struct DevKey {
 
 // Comb tables: 8-bit signed windows, entries 1..128 per window.
 constexpr int COMB_W = 8;
-constexpr int COMB_ENTRIES = 128;
 
 // Timing hook: the runtime records a HIP event on the batch's stream after
 // each kernel a launcher enqueues (names: "<class>_<kernel>").

@@ -4,10 +4,10 @@
 // rules R23-R26): len(sig) == 64, sig[63] & 0xE0 == 0, S < L,
 // k = SHA-512(R || A || M) mod L, R' = [S]B + [k](-A) (cofactorless), accept iff
 // encode(R') == sig[:32] byte for byte.
-//   k_ed_point  : S and k recoded to signed 8-bit windows; R' as a sum of one
-//                 precomputed multiple of B and one of -A per window (Niels-form
-//                 comb tables), extended twisted-Edwards coordinates with the
-//                 complete a = -1 addition law (no exceptional cases at all)
+//   k_ed_point  : S and k recoded to signed W-bit windows (ed25519.hpp); R' as
+//                 a sum of one precomputed multiple of B and one of -A per window
+//                 (Niels-form comb tables), extended twisted-Edwards coordinates
+//                 with the complete a = -1 addition law (no exceptional cases)
 //   k_ed_finish : Z^-1, canonical encoding, byte compare with R
 // Key staging decodes A with filippo.io/edwards25519 SetBytes semantics
 // (non-canonical y accepted, x = 0 with the sign bit set accepted).
@@ -61,10 +61,11 @@ __device__ void add_full(EPt& R, const EPt& P, const EPt& Q) {
   mp::mul<Fp>(R.X, E, F); mp::mul<Fp>(R.Y, G, H); mp::mul<Fp>(R.T, E, H); mp::mul<Fp>(R.Z, F, G);
 }
 
+template <bool BASE>
 __device__ __forceinline__ void add_window(EPt& P, const uint32_t* __restrict__ tab, int w, int d) {
   if (d == 0) return;
   const int ad = d < 0 ? -d : d;
-  const uint32_t* ent = tab + ((int64_t)w * COMB_ENTRIES + (ad - 1)) * ED_STRIDE;
+  const uint32_t* ent = tab + ((int64_t)w * ed_entries(BASE) + (ad - 1)) * ED_STRIDE;
   uint32_t ypx[L], ymx[L], t2d[L];
 #pragma unroll
   for (int j = 0; j < L; ++j) { ypx[j] = ent[j]; ymx[j] = ent[L + j]; t2d[j] = ent[2 * L + j]; }
@@ -76,16 +77,19 @@ __device__ __forceinline__ void add_window(EPt& P, const uint32_t* __restrict__ 
   }
 }
 
+// signed W-bit digits d_w in [-2^(W-1), 2^(W-1)], s = sum d_w 2^(W w)
+template <int W, int NWIN>
 __device__ __forceinline__ void recode(int* dg, const uint32_t* s) {
+  constexpr uint32_t DM = (1u << W) - 1u;
   int c = 0;
 #pragma unroll
-  for (int w = 0; w < ED_WINDOWS; ++w) {
-    const int bit = 8 * w, q = bit / MP_W, sh = bit % MP_W;
+  for (int w = 0; w < NWIN; ++w) {
+    const int bit = W * w, q = bit / MP_W, sh = bit % MP_W;
     uint32_t b = q < L ? (s[q] >> sh) : 0u;
-    if (sh > MP_W - 8 && q + 1 < L) b |= s[q + 1] << (MP_W - sh);
-    int v = (int)(b & 0xffu) + c;
-    c = v > 128;
-    dg[w] = v - (c << 8);
+    if (sh > MP_W - W && q + 1 < L) b |= s[q + 1] << (MP_W - sh);
+    int v = (int)(b & DM) + c;
+    c = v > (1 << (W - 1));
+    dg[w] = v - (c << W);
   }
 }
 
@@ -125,20 +129,23 @@ __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
     mp::mul<Fl>(k, kr, rr);                 // H mod L (< 2L)
     mp::csub<Fl>(k);
   }
-  int d1[ED_WINDOWS], d2[ED_WINDOWS];
-  recode(d1, s);
-  recode(d2, k);
+  constexpr int NB = ed_windows(true), NA = ed_windows(false), NW = NB > NA ? NB : NA;
+  int d1[NB], d2[NA];
+  recode<ed_comb_w(true), NB>(d1, s);
+  recode<ed_comb_w(false), NA>(d2, k);
   EPt P;
 #pragma unroll
   for (int j = 0; j < L; ++j) { P.X[j] = 0; P.T[j] = 0; P.Y[j] = Fp::ONE[j]; P.Z[j] = Fp::ONE[j]; }
   const uint32_t* __restrict__ atab = a.keyblob + K.tab_off;
 #pragma unroll 1
-  for (int w = 0; w < ED_WINDOWS; ++w) {
-    int e1 = 0, e2 = 0;
+  for (int w = 0; w < NW; ++w) {
+    int e1 = 0, e2 = 0;                       // uniform select: no dynamic register indexing
 #pragma unroll
-    for (int i = 0; i < ED_WINDOWS; ++i) if (i == w) { e1 = d1[i]; e2 = d2[i]; }
-    add_window(P, a.btab, w, e1);
-    add_window(P, atab, w, e2);
+    for (int i = 0; i < NB; ++i) if (i == w) e1 = d1[i];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) if (i == w) e2 = d2[i];
+    add_window<true>(P, a.btab, w, e1);
+    add_window<false>(P, atab, w, e2);
   }
 #pragma unroll
   for (int j = 0; j < L; ++j) {
@@ -191,26 +198,66 @@ __device__ void niels_entry(uint32_t* out, const EPt& P) {
   for (int j = 0; j < L; ++j) { out[j] = ypx[j]; out[L + j] = ymx[j]; out[2 * L + j] = t2d[j]; }
 }
 
-__device__ void table_entry(uint32_t* out, const uint32_t* bx, const uint32_t* by, int w, int d) {
-  EPt P, acc;
+// canonical a -> a / 2 mod p (canonical)
+__device__ void half_mod(uint32_t* r, const uint32_t* a) {
+  uint32_t v[L];
+  const uint32_t odd = 0u - (a[0] & 1u);
+#pragma unroll
+  for (int j = 0; j < L; ++j) v[j] = a[j] + (Fp::M[j] & odd);
+  mp::norm<Fp>(v);                              // a (+ p) < 2p < 2^(28L): even, limbs < 2^28
+#pragma unroll
+  for (int j = 0; j < L; ++j) r[j] = (v[j] >> 1) | (j + 1 < L ? (v[j + 1] & 1u) << (MP_W - 1) : 0u);
+}
+
+// affine (x, y) of a Niels entry (y+x, y-x, 2dxy)
+__device__ void niels_affine(uint32_t* x, uint32_t* y, const uint32_t* ent) {
+  uint32_t t[L];
+  mp::sub<Fp>(t, ent, ent + L); mp::canon<Fp>(t); half_mod(x, t);
+  mp::add<Fp>(t, ent, ent + L); mp::canon<Fp>(t); half_mod(y, t);
+}
+
+// window base 2^(W w) * P as the Niels entry d = 1 of window w
+__device__ void window_base(uint32_t* out, const uint32_t* bx, const uint32_t* by, int shifts) {
+  EPt P;
   mp::copy<Fp>(P.X, bx); mp::copy<Fp>(P.Y, by); mp::set_const<Fp>(P.Z, Fp::ONE);
   mp::mul<Fp>(P.T, bx, by);
-  for (int i = 0; i < 8 * w; ++i) add_full(P, P, P);
+  for (int i = 0; i < shifts; ++i) add_full(P, P, P);
+  niels_entry(out, P);
+}
+
+// entry d * base (d <= 2^(W-1)) from the window's d = 1 entry
+template <int W>
+__device__ void table_entry(uint32_t* out, const uint32_t* base_ent, int d) {
+  EPt P, acc;
+  uint32_t bx[L], by[L];
+  niels_affine(bx, by, base_ent);
+  mp::copy<Fp>(P.X, bx); mp::copy<Fp>(P.Y, by); mp::set_const<Fp>(P.Z, Fp::ONE);
+  mp::mul<Fp>(P.T, bx, by);
 #pragma unroll
   for (int j = 0; j < L; ++j) { acc.X[j] = 0; acc.T[j] = 0; acc.Y[j] = Fp::ONE[j]; acc.Z[j] = Fp::ONE[j]; }
-  for (int bit = 7; bit >= 0; --bit) {
+  for (int bit = W - 1; bit >= 0; --bit) {
     add_full(acc, acc, acc);
     if ((d >> bit) & 1) add_full(acc, acc, P);
   }
   niels_entry(out, acc);
 }
 
-__global__ void k_ed_table_b(uint32_t* tab) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= ED_WINDOWS * COMB_ENTRIES) return;
+// Tables in two launches (as ecdsa.hip): thread per window for the bases, then
+// thread per entry d >= 2 from its window's base.
+__global__ void k_ed_table_base_b(uint32_t* tab) {
+  constexpr int W = ed_comb_w(true), NWIN = ed_windows(true), NE = ed_entries(true);
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= NWIN) return;
   uint32_t bx[L], by[L];
   mp::set_const<Fp>(bx, ED25519C::BX_M); mp::set_const<Fp>(by, ED25519C::BY_M);
-  table_entry(tab + (int64_t)e * ED_STRIDE, bx, by, e / COMB_ENTRIES, e % COMB_ENTRIES + 1);
+  window_base(tab + (int64_t)w * NE * ED_STRIDE, bx, by, W * w);
+}
+
+__global__ void k_ed_table_b(uint32_t* tab) {
+  constexpr int W = ed_comb_w(true), NWIN = ed_windows(true), NE = ed_entries(true);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= NWIN * NE || e % NE == 0) return;
+  table_entry<W>(tab + (int64_t)e * ED_STRIDE, tab + (int64_t)(e / NE) * NE * ED_STRIDE, e % NE + 1);
 }
 
 // thread per key: decode A (SetBytes semantics), store -A affine at aux + 8
@@ -263,14 +310,26 @@ __global__ void k_ed_decode(DevKey* keys, uint32_t* blob, const int32_t* idx, in
   K.valid = (K.valid && ok) ? 1 : 0;
 }
 
-__global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_ed_table_base_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  constexpr int W = ed_comb_w(false), NWIN = ed_windows(false), NE = ed_entries(false);
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
-  if (k >= n || e >= ED_WINDOWS * COMB_ENTRIES) return;
+  if (k >= n || w >= NWIN) return;
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
   const uint32_t* aux = blob + K.aux_off + 8;
-  table_entry(blob + K.tab_off + (int64_t)e * ED_STRIDE, aux, aux + L, e / COMB_ENTRIES, e % COMB_ENTRIES + 1);
+  window_base(blob + K.tab_off + (int64_t)w * NE * ED_STRIDE, aux, aux + L, W * w);
+}
+
+__global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  constexpr int W = ed_comb_w(false), NWIN = ed_windows(false), NE = ed_entries(false);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (k >= n || e >= NWIN * NE || e % NE == 0) return;
+  const DevKey& K = keys[idx[k]];
+  if (!K.valid) return;
+  uint32_t* tab = blob + K.tab_off;
+  table_entry<W>(tab + (int64_t)e * ED_STRIDE, tab + (int64_t)(e / NE) * NE * ED_STRIDE, e % NE + 1);
 }
 
 }  // namespace
@@ -287,11 +346,14 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
 
 void launch_ed_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
   if (n <= 0) return;
+  constexpr int NWIN = ed_windows(false), NE = ed_entries(false);
   hipLaunchKernelGGL(k_ed_decode, dim3((n + 63) / 64), dim3(64), 0, s, keys, blob, idx, n);
-  hipLaunchKernelGGL(k_ed_table_keys, dim3((ED_WINDOWS * COMB_ENTRIES + 63) / 64, n), dim3(64), 0, s,
-                     keys, blob, idx, n);
+  hipLaunchKernelGGL(k_ed_table_base_keys, dim3((NWIN + 63) / 64, n), dim3(64), 0, s, keys, blob, idx, n);
+  hipLaunchKernelGGL(k_ed_table_keys, dim3((NWIN * NE + 63) / 64, n), dim3(64), 0, s, keys, blob, idx, n);
 }
 
 void launch_ed_btable(uint32_t* tab, hipStream_t s) {
-  hipLaunchKernelGGL(k_ed_table_b, dim3((ED_WINDOWS * COMB_ENTRIES + 63) / 64), dim3(64), 0, s, tab);
+  constexpr int NWIN = ed_windows(true), NE = ed_entries(true);
+  hipLaunchKernelGGL(k_ed_table_base_b, dim3((NWIN + 63) / 64), dim3(64), 0, s, tab);
+  hipLaunchKernelGGL(k_ed_table_b, dim3((NWIN * NE + 63) / 64), dim3(64), 0, s, tab);
 }

@@ -23,8 +23,15 @@ struct EdArgs {
 
 constexpr int ED_L = 10;
 constexpr int ED_STRIDE = 32;                   // 3 x 10 limbs, padded to 16 B
-constexpr int ED_WINDOWS = 33;
-constexpr int64_t ED_TABLE_WORDS = (int64_t)ED_WINDOWS * jgk::COMB_ENTRIES * ED_STRIDE;
+// Signed-digit comb geometry (as ecdsa.hpp): scalars S, k < L < 2^253, so
+// ceil(254 / W) windows.  The base point's table is shared by all keys and gets
+// the wider window: B W=20 (13 windows, 872 MB), keys W=16 (16 windows, 67 MB
+// each) -> 29 additions per token (66 at W=8).
+constexpr int ed_comb_w(bool base) { return base ? 20 : 16; }
+constexpr int ed_entries(bool base) { return 1 << (ed_comb_w(base) - 1); }
+constexpr int ed_windows(bool base) { return (253 + 1 + ed_comb_w(base) - 1) / ed_comb_w(base); }
+constexpr int64_t ed_table_words(bool base) { return (int64_t)ed_windows(base) * ed_entries(base) * ED_STRIDE; }
+constexpr int ED_MAX_KEYS = 256;
 
 void launch_ed(const EdArgs& a, hipStream_t s, const jgk::Marker& mk);
 // key staging: decode each listed key's 32 public-key bytes (words at aux_off),
