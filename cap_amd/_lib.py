@@ -20,7 +20,7 @@ CURVE_IDS = {"P-256": 1, "P-384": 2, "P-521": 3}
 # every symbol include/jg.h declares
 EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_last_error",
            "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_enqueue", "jg_batch_sync",
-           "jg_batch_free", "jg_batch_kernel_times", "jg_version"]
+           "jg_batch_free", "jg_batch_kernel_times", "jg_hash_batch", "jg_version"]
 
 
 class JgKey(ctypes.Structure):
@@ -69,6 +69,7 @@ def lib():
         L.jg_batch_free.argtypes = [vp, vp]
         L.jg_batch_kernel_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
                                             ctypes.c_int]
+        L.jg_hash_batch.argtypes = [vp, vp, sz, vp, sz, vp]
         L.jg_version.restype = ctypes.c_char_p
         _lib = L
     return _lib

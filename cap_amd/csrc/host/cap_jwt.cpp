@@ -933,4 +933,193 @@ std::vector<Result> Validator::ValidateBatch(const std::vector<std::string_view>
   return out;
 }
 
+// ====================================================================== oidc hash claims
+void Engine::hash(const uint8_t* arena, size_t arena_len, const void* jobs, size_t njobs, uint8_t* digests) {
+  std::lock_guard<std::mutex> g(mu_);
+  const int rc = jg_hash_batch(ctx_, arena, arena_len, (const jg_hjob*)jobs, njobs, digests);
+  if (rc != 0) throw std::runtime_error(std::string("capjwt: jg_hash_batch: ") + jg_last_error(ctx_));
+}
+
+namespace {
+
+// unicode.IsPrint for the runes an alg header can carry: ASCII graphic + space,
+// and every other rune except the C0/C1 controls and the common non-printing
+// format / separator runes (Go's tables list more unassigned code points; an
+// alg name with those is not a supported alg either way, only its %q differs).
+bool go_is_print(uint32_t r) {
+  if (r < 0x80) return r >= 0x20 && r < 0x7f;
+  if (r < 0xa0 || r == 0xad) return false;
+  if (r == 0xa0 || r == 0x1680 || (r >= 0x2000 && r <= 0x200f) || (r >= 0x2028 && r <= 0x202f) ||
+      (r >= 0x205f && r <= 0x2064) || r == 0x3000 || r == 0xfeff || (r >= 0xfff9 && r <= 0xfffb) ||
+      r == 0xfffe || r == 0xffff || (r >= 0xd800 && r <= 0xdfff) || r > 0x10ffff)
+    return false;
+  return true;
+}
+
+// fmt %q of a string (strconv.Quote)
+std::string go_quote(std::string_view s) {
+  static const char* hex = "0123456789abcdef";
+  std::string o = "\"";
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t w = 1;
+    const uint32_t r = json::decode_rune((const unsigned char*)s.data() + i, s.size() - i, &w);
+    if (r == 0xfffd && w == 1) {                       // invalid byte
+      const unsigned char b = (unsigned char)s[i];
+      o += "\\x";
+      o.push_back(hex[b >> 4]);
+      o.push_back(hex[b & 15]);
+    } else if (r == '"' || r == '\\') {
+      o.push_back('\\');
+      o.push_back((char)r);
+    } else if (go_is_print(r)) {
+      o.append(s.substr(i, w));
+    } else if (r == '\a') { o += "\\a"; } else if (r == '\b') { o += "\\b"; } else if (r == '\f') { o += "\\f"; }
+    else if (r == '\n') { o += "\\n"; } else if (r == '\r') { o += "\\r"; } else if (r == '\t') { o += "\\t"; }
+    else if (r == '\v') { o += "\\v"; }
+    else if (r < ' ' || r == 0x7f) {
+      o += "\\x";
+      o.push_back(hex[r >> 4]);
+      o.push_back(hex[r & 15]);
+    } else {
+      const int nd = r < 0x10000 ? 4 : 8;
+      o += nd == 4 ? "\\u" : "\\U";
+      for (int k = nd - 1; k >= 0; --k) o.push_back(hex[(r >> (4 * k)) & 15]);
+    }
+    i += w;
+  }
+  o.push_back('"');
+  return o;
+}
+
+// oidc.UnmarshalClaims(rawToken, &map[string]interface{})   (oidc/token.go:170-184)
+bool unmarshal_claims(std::string_view raw, json::Value* claims, std::string* err) {
+  size_t parts = 1;
+  for (char c : raw) parts += c == '.';
+  if (parts != 3) {
+    *err = "UnmarshalClaims: malformed jwt, expected 3 parts got " + std::to_string(parts) + ": invalid parameter";
+    return false;
+  }
+  const size_t d1 = raw.find('.'), d2 = raw.find('.', d1 + 1);
+  std::string payload, e;
+  if (!b64rawurl_decode(raw.substr(d1 + 1, d2 - d1 - 1), &payload, &e)) {
+    *err = "UnmarshalClaims: malformed jwt claims: " + e;
+    return false;
+  }
+  if (!claims_map(payload, claims, &e)) {
+    *err = "UnmarshalClaims: unable to marshal jwt JSON: " + e;
+    return false;
+  }
+  return true;
+}
+
+struct HashPlan {
+  int fam = 0;                   // jg_hash_fam, 0 = no hash (decided already)
+  std::string want;              // the claim's value
+};
+
+// verifyHashClaim up to the hash: fills r (decided) or p (hash needed)
+void hash_claim_plan(const std::string& claim, std::string_view t, HashClaimResult* r, HashPlan* p) {
+  const std::string op = "verifyHashClaim";
+  json::Value claims;
+  std::string e;
+  if (t.empty()) {
+    r->err = op + ": IDToken.Claims: id_token is empty: invalid parameter";
+    return;
+  }
+  if (!unmarshal_claims(t, &claims, &e)) {
+    r->err = op + ": " + e;
+    return;
+  }
+  const json::Value* v = claims.kind == json::Value::Object ? claims.get(claim) : nullptr;
+  if (!v || v->kind != json::Value::String) return;        // (false, nil)
+  JWS jws;
+  if (!parse_signed(t, &jws, &e)) {
+    r->err = op + ": malformed jwt (" + e + "): token malformed";
+    return;
+  }
+  if (jws.sigs.empty()) {
+    r->err = op + ": id_token not signed: token is not signed";
+    return;
+  }
+  if (jws.sigs.size() > 1) {
+    r->err = op + ": multiple signatures on id_token not supported";
+    return;
+  }
+  const int alg = alg_id(jws.sigs[0].alg);
+  if (!alg) {
+    r->err = op + ": id_token signed with algorithm " + go_quote(jws.sigs[0].alg) + ": unsupported signing algorithm";
+    return;
+  }
+  switch (alg) {
+    case JG_RS256: case JG_ES256: case JG_PS256: p->fam = JG_SHA256; break;
+    case JG_RS384: case JG_ES384: case JG_PS384: p->fam = JG_SHA384; break;
+    case JG_RS512: case JG_ES512: case JG_PS512: p->fam = JG_SHA512; break;
+    default: return;                                        // EdDSA: (false, nil)
+  }
+  p->want = v->str;
+}
+
+std::vector<HashClaimResult> verify_hash_claim_batch(Engine& eng, const std::string& claim,
+                                                     const std::vector<std::string_view>& id_tokens,
+                                                     const std::vector<std::string_view>& values) {
+  if (id_tokens.size() != values.size()) throw std::invalid_argument("id_tokens and values differ in length");
+  const size_t n = id_tokens.size();
+  std::vector<HashClaimResult> out(n);
+  std::vector<HashPlan> plan(n);
+  parallel_for(n, host_threads(), [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) hash_claim_plan(claim, id_tokens[i], &out[i], &plan[i]);
+  });
+  // one GPU batch over the values that need hashing
+  std::vector<size_t> idx;
+  size_t bytes = 0;
+  for (size_t i = 0; i < n; ++i)
+    if (plan[i].fam) {
+      idx.push_back(i);
+      bytes += values[i].size();
+    }
+  if (!idx.empty()) {
+    std::string arena;
+    arena.reserve(bytes);
+    std::vector<jg_hjob> jobs(idx.size());
+    for (size_t k = 0; k < idx.size(); ++k) {
+      jobs[k] = jg_hjob{};
+      jobs[k].off = arena.size();
+      jobs[k].len = (uint32_t)values[idx[k]].size();
+      jobs[k].fam = (uint8_t)plan[idx[k]].fam;
+      arena.append(values[idx[k]]);
+    }
+    std::vector<uint8_t> dig(64 * idx.size());
+    eng.hash((const uint8_t*)arena.data(), arena.size(), jobs.data(), jobs.size(), dig.data());
+    parallel_for(idx.size(), host_threads(), [&](size_t lo, size_t hi) {
+      for (size_t k = lo; k < hi; ++k) {
+        const size_t i = idx[k];
+        const size_t half = (plan[i].fam == JG_SHA256 ? 32 : plan[i].fam == JG_SHA384 ? 48 : 64) / 2;
+        const std::string actual = b64url_encode(std::string_view((const char*)dig.data() + 64 * k, half));
+        if (actual != plan[i].want) {
+          out[i].err = claim == "at_hash" ? "verifyHashClaim: access_token hash does not match value in id_token"
+                                          : "verifyHashClaim: authorization code hash does not match value in id_token";
+        } else {
+          out[i].verified = true;
+        }
+      }
+    });
+  }
+  for (auto& r : out)
+    if (!r.err.empty()) r.err = "VerifyAccessToken: " + r.err;     // both public methods use this op
+  return out;
+}
+
+}  // namespace
+
+std::vector<HashClaimResult> VerifyAccessTokenBatch(Engine& eng, const std::vector<std::string_view>& id_tokens,
+                                                    const std::vector<std::string_view>& access_tokens) {
+  return verify_hash_claim_batch(eng, "at_hash", id_tokens, access_tokens);
+}
+
+std::vector<HashClaimResult> VerifyAuthorizationCodeBatch(Engine& eng, const std::vector<std::string_view>& id_tokens,
+                                                          const std::vector<std::string_view>& codes) {
+  return verify_hash_claim_batch(eng, "c_hash", id_tokens, codes);
+}
+
 }  // namespace capjwt

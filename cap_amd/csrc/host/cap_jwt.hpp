@@ -74,6 +74,8 @@ class Engine {
   void load(const std::vector<PublicKey>& keys);      // jg_keys_load
   // verify (arena entry, key, alg) jobs; verdicts[i] = 1 accept, 0 reject
   void verify(const uint8_t* arena, size_t arena_len, const void* jobs, size_t njobs, uint8_t* verdicts);
+  // SHA-2 of (arena span, family) jobs: digests njobs x 64 bytes (jg_hash_batch)
+  void hash(const uint8_t* arena, size_t arena_len, const void* jobs, size_t njobs, uint8_t* digests);
   uint8_t* arena_buffer(size_t bytes);                 // pinned, grow-only
   int threads() const { return threads_; }
  private:
@@ -151,5 +153,22 @@ void release_results(std::vector<Result>& rs);
 // Host threads used by batch parsing / claims (CAPJWT_HOST_THREADS, default
 // min(hardware threads, 16)).
 int host_threads();
+
+// ---------------------------------------------------------------- oidc hash claims
+// IDToken.VerifyAccessToken / VerifyAuthorizationCode (oidc/id_token.go:59-145,
+// verifyHashClaim) for many (id_token, value) pairs: claims via UnmarshalClaims
+// (oidc/token.go:170-184), the claim as a string, jose.ParseSigned, exactly one
+// signature with a supported alg, then base64url(left half of SHA-2(value)) ==
+// claim.  The SHA-2 runs on the GPU in one jg_hash_batch.  verified/err are Go's
+// (bool, error); err == "" <=> nil.  Error strings follow the reference,
+// including its "VerifyAccessToken" op prefix on the c_hash path.
+struct HashClaimResult {
+  bool verified = false;
+  std::string err;
+};
+std::vector<HashClaimResult> VerifyAccessTokenBatch(Engine& eng, const std::vector<std::string_view>& id_tokens,
+                                                    const std::vector<std::string_view>& access_tokens);
+std::vector<HashClaimResult> VerifyAuthorizationCodeBatch(Engine& eng, const std::vector<std::string_view>& id_tokens,
+                                                          const std::vector<std::string_view>& codes);
 
 }  // namespace capjwt

@@ -98,6 +98,10 @@ bool b64url_decode(std::string_view s, std::string* out, std::string* err) {
   return raw_decode(tabs().url, s.substr(0, n), out, err);
 }
 
+bool b64rawurl_decode(std::string_view s, std::string* out, std::string* err) {
+  return raw_decode(tabs().url, s, out, err);
+}
+
 std::string b64url_encode(std::string_view raw) {
   std::string o;
   o.reserve((raw.size() * 4 + 2) / 3);

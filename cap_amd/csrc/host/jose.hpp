@@ -24,6 +24,9 @@ int alg_key_kind(int id);           // JG_KEY_RSA / JG_KEY_EC / JG_KEY_ED25519, 
 // trailing bits are accepted, a final group of one character is an error.
 // Returns false on error (err = Go's "illegal base64 data at input byte N").
 bool b64url_decode(std::string_view s, std::string* out, std::string* err = nullptr);
+// base64.RawURLEncoding.DecodeString itself ('=' is an illegal byte), as cap's
+// oidc.UnmarshalClaims calls it (oidc/token.go:176).
+bool b64rawurl_decode(std::string_view s, std::string* out, std::string* err = nullptr);
 std::string b64url_encode(std::string_view raw);
 // Go base64.StdEncoding.DecodeString (x5c entries): padded, strict length.
 bool b64std_decode(std::string_view s, std::string* out);

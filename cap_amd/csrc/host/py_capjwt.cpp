@@ -350,4 +350,35 @@ PYBIND11_MODULE(_capjwt_host, m) {
         }
         return py::bytes(ok);
       });
+
+  // ---- oidc at_hash / c_hash (oidc/id_token.go:59-145) over one GPU context
+  struct PyHashEngine {
+    std::unique_ptr<Engine> eng;
+  };
+  auto hash_claims = [](PyHashEngine& s, py::sequence ids, py::sequence vals, bool code) {
+    auto a = as_strings(ids), b = as_strings(vals);
+    if (a.size() != b.size()) throw py::value_error("id_tokens and values differ in length");
+    std::vector<HashClaimResult> rs;
+    {
+      py::gil_scoped_release rel;
+      rs = code ? VerifyAuthorizationCodeBatch(*s.eng, views(a), views(b))
+                : VerifyAccessTokenBatch(*s.eng, views(a), views(b));
+    }
+    py::list out;
+    for (const auto& r : rs)
+      out.append(py::make_tuple(r.verified, r.err.empty() ? py::object(py::none()) : py::object(py::str(r.err))));
+    return out;
+  };
+  py::class_<PyHashEngine>(m, "HashEngine")
+      .def(py::init([](const std::vector<int>& devices) {
+        auto p = std::make_unique<PyHashEngine>();
+        p->eng = std::make_unique<Engine>(devices);
+        return p;
+      }), py::arg("devices") = std::vector<int>{})
+      .def("verify_access_token_batch", [hash_claims](PyHashEngine& s, py::sequence ids, py::sequence ats) {
+        return hash_claims(s, ids, ats, false);
+      })
+      .def("verify_authorization_code_batch", [hash_claims](PyHashEngine& s, py::sequence ids, py::sequence codes) {
+        return hash_claims(s, ids, codes, true);
+      });
 }

@@ -30,6 +30,7 @@
 #include "kernels/common.hpp"
 #include "kernels/ecdsa.hpp"
 #include "kernels/ed25519.hpp"
+#include "kernels/hash.hpp"
 #include "kernels/prep.hpp"
 #include "kernels/rsa.hpp"
 
@@ -778,6 +779,46 @@ int jg_verify_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
       return rc[k];
     }
   return 0;
+}
+
+int jg_hash_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
+                  const jg_hjob* jobs, size_t njobs, uint8_t* digest_out) {
+  if (!ctx || (njobs > 0 && (!jobs || !digest_out)) || (arena_len > 0 && !arena)) return -1;
+  if (njobs == 0) return 0;
+  for (size_t i = 0; i < njobs; ++i) {
+    const jg_hjob& J = jobs[i];
+    if (J.fam < JG_SHA256 || J.fam > JG_SHA512 || J.off > arena_len || J.len > arena_len - J.off) {
+      ctx->set_err("jg_hash_batch: job " + std::to_string(i) + " has an unknown hash or a span past the arena");
+      return -1;
+    }
+  }
+  try {
+    Device* d = ctx->devs[0].get();
+    std::lock_guard<std::mutex> g(d->mu);
+    HIPCHK(hipSetDevice(d->id));
+    Grow da, dj, dout;
+    uint8_t* a = (uint8_t*)da.get(arena_len + ARENA_SLACK);
+    HIPCHK(hipMemsetAsync(a + arena_len, 0, ARENA_SLACK, d->stream));
+    if (arena_len) HIPCHK(hipMemcpyAsync(a, arena, arena_len, hipMemcpyHostToDevice, d->stream));
+    jg_hjob* j = (jg_hjob*)dj.get(sizeof(jg_hjob) * njobs);
+    HIPCHK(hipMemcpyAsync(j, jobs, sizeof(jg_hjob) * njobs, hipMemcpyHostToDevice, d->stream));
+    uint32_t* o = (uint32_t*)dout.get(64 * njobs);
+    launch_hash(a, j, (int64_t)njobs, o, d->stream);
+    HIPCHK(hipGetLastError());
+    std::vector<uint32_t> w(16 * njobs);
+    HIPCHK(hipMemcpyAsync(w.data(), o, 64 * njobs, hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    for (size_t k = 0; k < w.size(); ++k) {              // big-endian words -> digest bytes
+      digest_out[4 * k] = (uint8_t)(w[k] >> 24);
+      digest_out[4 * k + 1] = (uint8_t)(w[k] >> 16);
+      digest_out[4 * k + 2] = (uint8_t)(w[k] >> 8);
+      digest_out[4 * k + 3] = (uint8_t)w[k];
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    ctx->set_err(e.what());
+    return -2;
+  }
 }
 
 const char* jg_last_error(jg_ctx* ctx) {

@@ -122,6 +122,25 @@ void jg_batch_free(jg_ctx* ctx, jg_batch* b);
  * events on the batch's stream.  names/ms arrays of length cap; returns count. */
 int jg_batch_kernel_times(jg_batch* b, const char** names, float* ms, int cap);
 
+/* ---- batched SHA-2 of byte strings ----
+ * The hash of cap's OIDC hash-claim checks: oidc/id_token.go:121-135
+ * (verifyHashClaim, behind IDToken.VerifyAccessToken :59 and
+ * VerifyAuthorizationCode :83) hashes the access token / authorization code
+ * with SHA-256, SHA-384 or SHA-512 by the id_token's alg.  Job i hashes
+ * arena[off, off + len) with `fam`; digest_out receives njobs x 64 bytes, the
+ * digest (32 / 48 / 64 bytes) left-aligned and zero-filled.  Blocking; runs on
+ * the context's first device.  Returns 0, or <0 on bad arguments (a span past
+ * arena_len, unknown fam) or an infrastructure error. */
+enum jg_hash_fam { JG_SHA256 = 1, JG_SHA384 = 2, JG_SHA512 = 3 };
+typedef struct jg_hjob {
+  uint64_t off;
+  uint32_t len;
+  uint8_t fam;             /* jg_hash_fam */
+  uint8_t pad_[3];
+} jg_hjob;
+int jg_hash_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
+                  const jg_hjob* jobs, size_t njobs, uint8_t* digest_out);
+
 /* Library build information (gfx target, version). */
 const char* jg_version(void);
 

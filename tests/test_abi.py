@@ -34,6 +34,8 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.JgTok) == 24
     assert _lib.JgTok.key_idx.offset == 20 and _lib.JgTok.alg.offset == 22
     assert _lib.JgKey.e.offset == 24 and _lib.JgKey.coord_len.offset == 48
+    src = open(os.path.join(ROOT, "include", "jg.h")).read()
+    assert "uint64_t off;\n  uint32_t len;\n  uint8_t fam;" in src        # jg_hjob: 16 bytes
 
 
 def test_no_device_fails_loudly():
