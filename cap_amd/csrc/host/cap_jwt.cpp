@@ -494,40 +494,16 @@ class JSONWebKeySet final : public KeySet {
   std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, std::vector<TokenInfo>* info) override {
     std::lock_guard<std::mutex> g(mu_);
     Verified V;
-    auto cand = [&](const Tok& t, std::vector<uint16_t>& out) {
-      // remoteKeySet.verify: keyID == "" || key.KeyID == keyID   [R31, R34]
-      const int fam = alg_key_kind(t.alg);
-      for (size_t k = 0; k < keys_.size(); ++k)
-        if ((t.kid.empty() || keys_[k].kid == t.kid) && fam_[k] == fam) out.push_back((uint16_t)k);
-    };
+    std::string miss_err;
+    remote_verify(tokens, &V, &miss_err);
     std::vector<Result> res(tokens.size());
-    if (have_keys_) {
-      gpu_verify(eng_, tokens, &V, cand);
-    } else {
-      gpu_verify(eng_, tokens, &V, [](const Tok&, std::vector<uint16_t>&) {});
-    }
-    // tokens that parsed but did not verify: refresh once if the cache has
-    // expired (now + keysExpiryDelta(30s) after expiry), then retry them
-    std::vector<size_t> miss;
-    for (size_t i = 0; i < tokens.size(); ++i)
-      if (V.toks[i].info.parsed && !V.any[i]) miss.push_back(i);
-    std::string fetch_err;
-    bool refreshed = false;
-    if (!miss.empty() && (!have_keys_ || wall_now_ns() + 30 * kSecond > expiry_ns_)) {
-      refreshed = true;
-      if (refresh(&fetch_err)) gpu_verify(eng_, tokens, &V, cand, &miss);
-    }
     PhaseTimer pt("jwks");
     parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         const Tok& t = V.toks[i];
         Result& r = res[i];
         if (!t.info.parsed) { r.err = "oidc: malformed jwt: " + t.info.parse_err; continue; }
-        if (!V.any[i]) {
-          r.err = refreshed && !fetch_err.empty() ? "fetching keys " + fetch_err
-                                                  : "failed to verify id token signature";
-          continue;
-        }
+        if (!V.any[i]) { r.err = miss_err; continue; }
         std::string jerr;       // jsonWebKeySet.VerifySignature: json.Unmarshal(payload)
         if (claims_map(t.payload, &r.claims, &jerr)) r.ok = true;
         else { r.claims = json::Value(); r.err = jerr; }
@@ -543,7 +519,54 @@ class JSONWebKeySet final : public KeySet {
     return res;
   }
 
+  // go-oidc remoteKeySet.VerifySignature itself: the verified payload bytes
+  std::vector<PayloadResult> verify_payload_batch(const std::vector<std::string_view>& tokens) {
+    std::lock_guard<std::mutex> g(mu_);
+    Verified V;
+    std::string miss_err;
+    remote_verify(tokens, &V, &miss_err);
+    std::vector<PayloadResult> res(tokens.size());
+    parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        Tok& t = V.toks[i];
+        if (!t.info.parsed) res[i].err = "oidc: malformed jwt: " + t.info.parse_err;
+        else if (!V.any[i]) res[i].err = miss_err;
+        else { res[i].ok = true; res[i].payload = std::move(t.payload); }
+      }
+    });
+    return res;
+  }
+
  private:
+  // remoteKeySet.verify over a batch: kid-filtered keys from the cache, then
+  // (for the tokens that missed) one refresh if the cache has expired and a
+  // retry.  *miss_err = the error every unverified, parsed token gets.
+  void remote_verify(const std::vector<std::string_view>& tokens, Verified* V, std::string* miss_err) {
+    auto cand = [&](const Tok& t, std::vector<uint16_t>& out) {
+      // remoteKeySet.verify: keyID == "" || key.KeyID == keyID   [R31, R34]
+      const int fam = alg_key_kind(t.alg);
+      for (size_t k = 0; k < keys_.size(); ++k)
+        if ((t.kid.empty() || keys_[k].kid == t.kid) && fam_[k] == fam) out.push_back((uint16_t)k);
+    };
+    if (have_keys_) {
+      gpu_verify(eng_, tokens, V, cand);
+    } else {
+      gpu_verify(eng_, tokens, V, [](const Tok&, std::vector<uint16_t>&) {});
+    }
+    // tokens that parsed but did not verify: refresh once if the cache has
+    // expired (now + keysExpiryDelta(30s) after expiry), then retry them
+    std::vector<size_t> miss;
+    for (size_t i = 0; i < tokens.size(); ++i)
+      if (V->toks[i].info.parsed && !V->any[i]) miss.push_back(i);
+    std::string fetch_err;
+    bool refreshed = false;
+    if (!miss.empty() && (!have_keys_ || wall_now_ns() + 30 * kSecond > expiry_ns_)) {
+      refreshed = true;
+      if (refresh(&fetch_err)) gpu_verify(eng_, tokens, V, cand, &miss);
+    }
+    *miss_err = refreshed && !fetch_err.empty() ? "fetching keys " + fetch_err : "failed to verify id token signature";
+  }
+
   bool refresh(std::string* err) {
     // go-oidc updateKeys
     FetchResponse resp;
@@ -702,6 +725,24 @@ std::unique_ptr<KeySet> NewJSONWebKeySet(const std::string& jwks_url, const std:
   if (jwks_url.empty()) { *err = "jwksURL must not be empty"; return nullptr; }
   if (!jwks_ca_pem.empty() && !ca_pem_ok(jwks_ca_pem)) { *err = "could not parse CA PEM value successfully"; return nullptr; }
   return std::make_unique<JSONWebKeySet>(jwks_url, jwks_ca_pem, std::move(fetch), devices);
+}
+
+// go-oidc's oidc.KeySet over the same GPU JWKS machinery
+class RemoteKeySet::Impl {
+ public:
+  Impl(const std::string& url, Fetcher f, const std::vector<int>& devices) : ks(url, "", std::move(f), devices) {}
+  JSONWebKeySet ks;
+};
+RemoteKeySet::RemoteKeySet(const std::string& jwks_url, Fetcher fetch, const std::vector<int>& devices)
+    : impl_(std::make_unique<Impl>(jwks_url, std::move(fetch), devices)) {}
+RemoteKeySet::~RemoteKeySet() = default;
+PayloadResult RemoteKeySet::VerifySignature(std::string_view jwt) { return impl_->ks.verify_payload_batch({jwt})[0]; }
+std::vector<PayloadResult> RemoteKeySet::VerifySignatureBatch(const std::vector<std::string_view>& jwts) {
+  return impl_->ks.verify_payload_batch(jwts);
+}
+std::unique_ptr<RemoteKeySet> NewRemoteKeySet(const std::string& jwks_url, Fetcher fetch,
+                                              const std::vector<int>& devices) {
+  return std::make_unique<RemoteKeySet>(jwks_url, std::move(fetch), devices);
 }
 
 std::unique_ptr<KeySet> NewOIDCDiscoveryKeySet(const std::string& issuer, const std::string& issuer_ca_pem,

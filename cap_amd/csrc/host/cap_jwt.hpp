@@ -113,6 +113,32 @@ std::unique_ptr<KeySet> NewJSONWebKeySet(const std::string& jwks_url, const std:
 std::unique_ptr<KeySet> NewOIDCDiscoveryKeySet(const std::string& issuer, const std::string& issuer_ca_pem,
                                                Fetcher fetch, std::string* err, const std::vector<int>& devices = {});
 
+// ---------------------------------------------------------------- go-oidc KeySet adapter
+// go-oidc v2.2.1's `oidc.KeySet` (VerifySignature(ctx, jwt) ([]byte, error)) as
+// returned by oidc.NewRemoteKeySet: the interface cap's jsonWebKeySet wraps
+// (jwt/keyset.go:101,120,127) and go-oidc's IDTokenVerifier calls -- the path
+// behind cap's oidc.Provider.VerifyIDToken (oidc/provider.go:418-441).  Same
+// kid filtering, refresh-on-miss and error strings as the JWKS key set above
+// ("oidc: malformed jwt: ...", "failed to verify id token signature",
+// "fetching keys ..."), returning the verified payload bytes.
+struct PayloadResult {
+  bool ok = false;
+  std::string payload;
+  std::string err;
+};
+class RemoteKeySet {
+ public:
+  RemoteKeySet(const std::string& jwks_url, Fetcher fetch, const std::vector<int>& devices);
+  ~RemoteKeySet();
+  PayloadResult VerifySignature(std::string_view jwt);
+  std::vector<PayloadResult> VerifySignatureBatch(const std::vector<std::string_view>& jwts);
+ private:
+  class Impl;
+  std::unique_ptr<Impl> impl_;
+};
+std::unique_ptr<RemoteKeySet> NewRemoteKeySet(const std::string& jwks_url, Fetcher fetch,
+                                              const std::vector<int>& devices = {});
+
 // ---------------------------------------------------------------- Validator
 constexpr int64_t kSecond = 1000000000LL;
 constexpr int64_t DefaultLeewaySeconds = 150;          // jwt/jwt.go:16

@@ -351,6 +351,41 @@ PYBIND11_MODULE(_capjwt_host, m) {
         return py::bytes(ok);
       });
 
+  // ---- go-oidc oidc.KeySet adapter (NewRemoteKeySet): payload bytes out
+  struct PyRemoteKeySet {
+    std::unique_ptr<RemoteKeySet> ks;
+  };
+  auto payload_py = [](const PayloadResult& r) {
+    return py::make_tuple(r.ok ? py::object(py::bytes(r.payload)) : py::object(py::none()),
+                          r.ok ? py::object(py::none()) : py::object(py::str(r.err)));
+  };
+  py::class_<PyRemoteKeySet>(m, "RemoteKeySet")
+      .def("verify_signature", [payload_py](PyRemoteKeySet& s, py::object tok) {
+        std::string t = tok.cast<std::string>();
+        PayloadResult r;
+        {
+          py::gil_scoped_release rel;
+          r = s.ks->VerifySignature(t);
+        }
+        return payload_py(r);
+      })
+      .def("verify_signature_batch", [payload_py](PyRemoteKeySet& s, py::sequence toks) {
+        auto v = as_strings(toks);
+        std::vector<PayloadResult> rs;
+        {
+          py::gil_scoped_release rel;
+          rs = s.ks->VerifySignatureBatch(views(v));
+        }
+        py::list out;
+        for (const auto& r : rs) out.append(payload_py(r));
+        return out;
+      });
+  m.def("new_remote_keyset", [](const std::string& url, py::object fetch, const std::vector<int>& devices) {
+    auto p = std::make_unique<PyRemoteKeySet>();
+    p->ks = NewRemoteKeySet(url, wrap_fetch(std::move(fetch)), devices);
+    return p;
+  }, py::arg("url"), py::arg("fetch"), py::arg("devices") = std::vector<int>{});
+
   // ---- oidc at_hash / c_hash (oidc/id_token.go:59-145) over one GPU context
   struct PyHashEngine {
     std::unique_ptr<Engine> eng;

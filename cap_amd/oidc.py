@@ -52,3 +52,26 @@ class IDToken(str):
 
 
 AccessToken = str
+
+
+class RemoteKeySet:
+    """go-oidc v2.2.1 `oidc.KeySet` from oidc.NewRemoteKeySet: VerifySignature
+    returns the verified payload bytes.  This is the interface cap's
+    jsonWebKeySet wraps (jwt/keyset.go:101,120,127) and go-oidc's ID token
+    verifier calls behind cap's Provider.VerifyIDToken (oidc/provider.go:418-441);
+    here every signature check is the GPU verifier's."""
+
+    def __init__(self, impl):
+        self._impl = impl
+
+    def VerifySignature(self, ctx, jwt) -> Tuple[Optional[bytes], Optional[str]]:
+        return tuple(self._impl.verify_signature(jwt))
+
+    def VerifySignatureBatch(self, ctx, jwts: Sequence) -> List[Tuple[Optional[bytes], Optional[str]]]:
+        return [tuple(r) for r in self._impl.verify_signature_batch(list(jwts))]
+
+
+def NewRemoteKeySet(ctx, jwks_url: str, fetch=None, devices=()) -> RemoteKeySet:
+    """oidc.NewRemoteKeySet(ctx, jwksURL); `fetch(url, ca_pem)` stands in for
+    the context's HTTP client (see cap_amd.jwt)."""
+    return RemoteKeySet(_h.new_remote_keyset(jwks_url, fetch, list(devices)))

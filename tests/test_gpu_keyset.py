@@ -223,6 +223,34 @@ def test_jwks_payload_json_errors(cases, keys, J):
     assert names["claims-invalid-utf8"][0]["iss"] == "a��b"
 
 
+def test_remote_keyset_adapter_payloads(cases, keys, J):
+    """go-oidc oidc.KeySet (NewRemoteKeySet): the verified payload bytes, and
+    the same outcome as cap's jsonWebKeySet minus its json.Unmarshal step
+    (jwt/keyset.go:126-139 wraps exactly this call)."""
+    from cap_amd import oidc
+    kids = ["rsa2048-a", "rsa3072-a", "rsa4096-a", "p256-a", "p256-b", "p384-a", "p521-a", "ed-a"]
+    doc = {"keys": [keys[k][2] for k in kids]}
+    rks = oidc.NewRemoteKeySet(None, "https://idp.example/jwks", FakeJWKS(doc))
+    jks, _ = J.NewJSONWebKeySet(None, "https://idp.example/jwks", "", FakeJWKS(doc))
+    toks = [t for t in cases["tokens"] if t["name"].startswith(("alg-", "nokid-", "kid-", "key_id-", "claims-"))]
+    res = rks.VerifySignatureBatch(None, [t["token"] for t in toks])
+    jres = jks.VerifySignatureBatch([t["token"] for t in toks])
+    nverified = 0
+    for t, (payload, err), (claims, jerr) in zip(toks, res, jres):
+        if err is None:
+            nverified += 1
+            assert payload == jws.parse_jws(t["token"]).payload, t["name"]
+            if jerr is not None:                       # only the JSON step may still fail
+                with pytest.raises(jws.GoJSONError):
+                    jws._claims_map(payload)
+        else:
+            assert payload is None and err == jerr, (t["name"], err, jerr)
+    assert nverified >= 20
+    single = rks.VerifySignature(None, toks[0]["token"])
+    assert single == tuple(res[0])
+    assert rks.VerifySignature(None, "a.b")[1].startswith("oidc: malformed jwt")
+
+
 def test_new_json_web_keyset_errors(J):
     assert J.NewJSONWebKeySet(None, "", "", FakeJWKS({})) == (None, "jwksURL must not be empty")
     assert J.NewJSONWebKeySet(None, "https://x", "not a pem", FakeJWKS({})) == \
