@@ -66,16 +66,17 @@ int cls_rows_scratch(int c) {
     default: return 0;
   }
 }
-// relative cost per token, for splitting a batch over devices
+// relative device time per token (1 x MI355X kernel times, profiles/r01_s4_*),
+// for splitting a batch over devices
 double cls_cost(int c) {
   switch (c) {
-    case CLS_RSA2K: return 1.0;
-    case CLS_RSA3K: return 3.3;
-    case CLS_RSA4K: return 7.5;
+    case CLS_RSA2K: return 3.6;
+    case CLS_RSA3K: return 8.0;
+    case CLS_RSA4K: return 16.0;
     case CLS_P256: return 1.0;
-    case CLS_P384: return 3.0;
-    case CLS_P521: return 7.0;
-    case CLS_ED25519: return 0.9;
+    case CLS_P384: return 3.6;
+    case CLS_P521: return 8.4;
+    case CLS_ED25519: return 1.9;
     default: return 0.01;
   }
 }

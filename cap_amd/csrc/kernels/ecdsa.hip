@@ -216,18 +216,18 @@ __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, cons
   mp::mul<Fp>(hhh, h, hh);
   mp::mul<Fp>(v, X, hh);
   mp::mul<Fp>(Z, Z, h);
-  // X3 = r^2 - (hhh + 2v)
-  mp::add<Fp>(t, hhh, v); mp::add<Fp>(t, t, v); mp::freduce<Fp>(t);
+  // X3 = r^2 - hhh - v - v: three lazy subtractions of normalized products
+  // (limbs < 7 * 2^28, value < 14m) and one single-chain value fold
   uint32_t r2[L];
   mp::sqr<Fp>(r2, r);
   uint32_t y1[L];
   mp::copy<Fp>(y1, Y);
-  mp::sub<Fp>(X, r2, t); mp::freduce<Fp>(X);
+  mp::sub<Fp>(X, r2, hhh); mp::sub<Fp>(X, X, v); mp::sub<Fp>(X, X, v); mp::freduce_lazy<Fp>(X);
   // Y3 = r (v - X3) - Y1 hhh
   mp::sub<Fp>(t, v, X);
   mp::mul<Fp>(Y, r, t);
   mp::mul<Fp>(t, y1, hhh);
-  mp::sub<Fp>(Y, Y, t); mp::freduce<Fp>(Y);
+  mp::sub<Fp>(Y, Y, t); mp::freduce_lazy<Fp>(Y);
 }
 
 template <class CV, bool GEN>

@@ -189,9 +189,36 @@ MPD void freduce(uint32_t* r) {
 #pragma unroll
   for (int j = 0; j < L; ++j) {
     uint64_t v = (uint64_t)r[j] + c;
-    if (F::FOLDC[j] != 0) mad64s(v, h, F::FOLDC[j], 2 + (j & 1));
+    if (F::FOLDC[j] != 0) mad64c(v, h, F::FOLDC[j]);
     r[j] = (uint32_t)v & MP_MASK;
     c = v >> MP_W;
+  }
+}
+
+// One-chain value fold for the madd outputs of P-256 (FOLD_S in the top limb):
+// input limbs < 2^31 with the top limb < 2^29, i.e. a normalized value plus at
+// most three lazy subtractions.  Only the top limb's bits >= FOLD_S are folded
+// (the lower limbs' pending carries stay put), then ONE carry chain: the lower
+// limbs sum to < 2^31 * 2^(28(L-2)) * (1 + 2^-27) < 2^(FOLD_S-1), so the result
+// is < 2^FOLD_S + 2^(FOLD_S-1) + h * 2^(FOLD_S-32) < 2m -- freduce's output
+// invariant at one chain instead of two.  Other fields: freduce.
+template <class F>
+MPD void freduce_lazy(uint32_t* r) {
+  constexpr int L = F::L;
+  constexpr int q = F::FOLD_S / MP_W, s = F::FOLD_S % MP_W;
+  if constexpr (q != L - 1 || 31 + MP_W * (L - 2) + 1 > F::FOLD_S) {
+    freduce<F>(r);
+  } else {
+    const uint32_t h = r[q] >> s;
+    r[q] &= (1u << s) - 1u;
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      uint64_t v = (uint64_t)r[j] + c;
+      if (F::FOLDC[j] != 0) mad64c(v, h, F::FOLDC[j]);
+      r[j] = (uint32_t)v & MP_MASK;
+      c = v >> MP_W;
+    }
   }
 }
 

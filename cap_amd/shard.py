@@ -11,8 +11,8 @@ devices of one jg_ctx.
 import numpy as np
 
 # relative verify cost per token by alg (jg_runtime.cpp cls_cost; RSA by key size)
-ALG_COST = {"RS256": 1.0, "PS256": 1.0, "RS384": 3.3, "PS384": 3.3, "RS512": 7.5, "PS512": 7.5,
-            "ES256": 1.0, "ES384": 3.0, "ES512": 7.0, "EdDSA": 0.9}
+ALG_COST = {"RS256": 3.6, "PS256": 3.6, "RS384": 8.0, "PS384": 8.0, "RS512": 16.0, "PS512": 16.0,
+            "ES256": 1.0, "ES384": 3.6, "ES512": 8.4, "EdDSA": 1.9}
 
 
 def shard_bounds(costs, world: int):

@@ -174,19 +174,25 @@ def test_madd_matches_affine_add(tk, cid):
     G = (c["gx"], c["gy"])
     rng = random.Random(cid)
     ins, want = [], []
-    for _ in range(64):
+    N = 256
+    for i in range(N):
         P1 = ec_mul(c, rng.randrange(1, c["n"]), G)
         P2 = ec_mul(c, rng.randrange(1, c["n"]), G)
         z = rng.randrange(1, p)
         X, Y, Z = P1[0] * z * z % p, P1[1] * z * z * z % p, z
         vals = [X * R % p, Y * R % p, Z * R % p, P2[0] * R % p, P2[1] * R % p]
+        if i % 2:                           # lazy Jacobian inputs: values in [p, 2p) where they fit
+            vals[:3] = [v + p if v + p < (1 << (W * L)) else v for v in vals[:3]]
         ins += [l for v in vals for l in to_limbs(v, L)]
         want.append(ec_add(c, P1, P2))
     A = (ctypes.c_uint32 * len(ins))(*ins)
-    O = (ctypes.c_uint32 * (64 * 3 * L))()
-    assert tk.tk_ec(cid, 0, A, ctypes.sizeof(A), O, ctypes.sizeof(O), 64) == 0
+    O = (ctypes.c_uint32 * (N * 3 * L))()
+    assert tk.tk_ec(cid, 0, A, ctypes.sizeof(A), O, ctypes.sizeof(O), N) == 0
     Ri = pow(R, -1, p)
     for i, w in enumerate(want):
+        for k in range(3):                  # outputs keep the normalized invariant: limbs < 2^28, value < 2p
+            ls = O[(3 * i + k) * L:(3 * i + k + 1) * L]
+            assert max(ls) <= MASK and from_limbs(ls) < 2 * p
         X, Y, Z = (from_limbs(O[(3 * i + k) * L:(3 * i + k + 1) * L]) * Ri % p for k in range(3))
         zi = pow(Z, -1, p)
         assert (X * zi * zi % p, Y * zi * zi * zi % p) == w
