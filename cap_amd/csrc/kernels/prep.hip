@@ -89,6 +89,7 @@ template <int CLS, int HM>
 __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   __shared__ uint32_t slots[WAVE * SLOT];
   __shared__ uint64_t wsh[WAVE];
+  __shared__ int8_t b64tab[256];
   const int lane = threadIdx.x;
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + lane;
   const int64_t np = a.npad;
@@ -118,10 +119,32 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
     ks = (alg >= 7 && alg <= 9) ? (uint32_t)es_size(alg) : 0u;
     if (ks == 0 || D != 2 * ks) { st = ST_REJECT; D = 0; }
   }
+  // Fast path: whole 32-bit words of decoded bytes (D and, for ECDSA, each of
+  // r and s a multiple of 4 bytes -- every standard key size but P-521): 16
+  // characters -> 12 bytes -> 3 big-endian words per step, characters mapped
+  // through an LDS table, each word stored straight to its row.  Otherwise
+  // the byte-serial loop below.
+  const bool fast = valid && D != 0 && (D & 3u) == 0 && (layout != LAY_SPLIT_BE || (ks & 3u) == 0);
+  const uint32_t DW = D >> 2;                          // decoded words
   if (valid) {
-    // zero the rows this token may leave partially written
-    for (int r = 0; r < a.zrows; ++r) sigw[(int64_t)r * np + p] = 0u;
+    // zero the rows this token may leave unwritten (scratch is reused across batches)
+    for (int r = 0; r < a.zrows; ++r) {
+      bool written = false;
+      if (fast) {
+        if (layout == LAY_SPLIT_BE) {
+          const uint32_t kw4 = ks >> 2;
+          written = (uint32_t)r < kw4 || ((uint32_t)r >= (uint32_t)EC_S_ROW && (uint32_t)r < EC_S_ROW + kw4);
+        } else {
+          written = (uint32_t)r < DW;
+        }
+      }
+      if (!written) sigw[(int64_t)r * np + p] = 0u;
+    }
   }
+  b64tab[lane] = (int8_t)b64val((uint32_t)lane);        // table for the fast path (all 256 bytes)
+  b64tab[64 + lane] = (int8_t)b64val(64u + lane);
+  b64tab[128 + lane] = (int8_t)b64val(128u + lane);
+  b64tab[192 + lane] = (int8_t)b64val(192u + lane);    // made visible by stage()'s first barrier
 
   const uint64_t sbyte = tk.off + tk.sig_rel_off;
   const uint64_t sw0 = sbyte >> 2;                     // arena dword of the segment's first char
@@ -137,6 +160,50 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
     if (__ballot(need) == 0ull) break;
     stage(slots, wsh, arena_w, need ? sw0 + (uint64_t)WIN * c : (valid ? sw0 : 0ull));
     if (!need) continue;
+    if (fast) {
+      // window c holds characters [128c, 128c + 128) at byte offset `first`
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const uint32_t i0 = 128u * c + 16u * g;         // first character of the step
+        if (i0 >= nchars) break;
+        uint32_t b24[4];
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+          const int k = 4 * g + qd;
+          const uint32_t q = __builtin_amdgcn_alignbyte(my[k + 1], my[k], first);
+          const int cnt = (int)nchars - (int)(i0 + 4u * qd);   // characters of this quad inside the segment
+          int t0 = b64tab[q & 0xffu], t1 = b64tab[(q >> 8) & 0xffu];
+          int t2 = b64tab[(q >> 16) & 0xffu], t3 = b64tab[q >> 24];
+          if (cnt < 4) t3 = 0;
+          if (cnt < 3) t2 = 0;
+          if (cnt < 2) t1 = 0;
+          if (cnt < 1) t0 = 0;
+          bad |= (t0 | t1 | t2 | t3) < 0;
+          b24[qd] = ((uint32_t)t0 << 18) | ((uint32_t)t1 << 12) | ((uint32_t)t2 << 6) | (uint32_t)t3;
+        }
+        const uint32_t w3[3] = {(b24[0] << 8) | (b24[1] >> 16), (b24[1] << 16) | (b24[2] >> 8),
+                                (b24[2] << 24) | b24[3]};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const uint32_t kw = 24u * c + 3u * g + j;     // big-endian word index in the byte stream
+          if (kw >= DW) continue;
+          uint32_t row, val = w3[j];
+          if (layout == LAY_BE) {
+            row = DW - 1u - kw;
+          } else if (layout == LAY_SPLIT_BE) {
+            const uint32_t kw4 = ks >> 2, h = kw >= kw4 ? 1u : 0u;
+            row = h * EC_S_ROW + (kw4 - 1u - (kw - h * kw4));
+          } else {
+            row = kw;
+            val = sha2::bswap32(val);
+            if (c == 0 && 3 * g + j < 8) R_le[3 * g + j] = val;
+          }
+          sigw[(int64_t)row * np + p] = val;
+        }
+      }
+      if (bad) st = ST_REJECT;
+      continue;
+    }
     const uint32_t lo = 4u * WIN * c;
     const uint32_t beg = lo > first ? lo : first;
     const uint32_t end = span < lo + 4u * WIN ? span : lo + 4u * WIN;
