@@ -30,6 +30,47 @@ def test_golden_vectors(ctx):
     assert not bad, bad
 
 
+def test_device_base64_decoder_edges(ctx):
+    """The device base64url decoder (prep.hip: word-at-a-time fast path, and the
+    byte-serial fallback for P-521 and odd-length RSA signatures) against Go's
+    base64.RawURLEncoding after go-jose's '=' trim (R3): a byte outside the
+    alphabet anywhere rejects, non-zero unused tail bits are accepted (Go's
+    decoder is not strict), a 4k+1 length rejects -- at every arena alignment."""
+    from cap_amd import _lib
+    from oracle import jws
+    keys, toks = H.golden()
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_"
+    names = ["valid-RS256-rsa2048-a-0", "valid-PS512-rsa4096-a-1", "valid-ES256-p256-a-0", "valid-ES384-p384-a-0",
+             "valid-ES512-p521-a-0", "valid-EdDSA-ed-a-0", "valid-RS256-rsa2049-a-0"]
+    by = {t["name"]: t for t in toks}
+    arena = _lib.Arena()
+    want = []
+    for name in names:
+        t = by[name]
+        p = jws.parse_jws(t["token"])
+        sig = jws.b64url_encode(p.signature)
+        n = len(sig)
+        variants = [(sig, 1)]
+        for pos in sorted({0, 1, 2, 3, 15, 16, 63, 64, 127, 128, 129, 255, 256, n // 2, n - 2, n - 1}):
+            if pos < n:
+                for bad in "*=+/. \x7f":
+                    variants.append((sig[:pos] + bad + sig[pos + 1:], 0))
+        variants.append((sig + "A", 0))                          # one character too many
+        if n % 4 in (2, 3):                                     # flip the unused low bits of the last char
+            unused = 4 if n % 4 == 2 else 2
+            last = alpha.index(sig[-1]) ^ ((1 << unused) - 1)
+            variants.append((sig[:-1] + alpha[last], 1))
+        variants.append((sig[:-1] + alpha[(alpha.index(sig[-1]) + 32) % 64], 0))  # a used bit flips
+        for vi, (s, w) in enumerate(variants):
+            arena.buf += b"#" * (vi % 4)                        # every alignment of the segment
+            arena.add(p.signing_input, s.encode(), p.alg, kid_index[t["key"]])
+            want.append(w)
+    out = ctx.verify(arena)
+    bad = [i for i, w in enumerate(want) if out[i] != w]
+    assert not bad, (len(bad), [(i, want[i]) for i in bad[:20]])
+
+
 def test_cross_product_every_token_every_key(ctx):
     """Every golden token against every loaded key in ONE batch (mixed classes,
     signatures longer than the key, wrong families): each verdict equals the
