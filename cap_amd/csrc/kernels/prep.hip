@@ -129,6 +129,8 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   if (valid) {
     // zero the rows this token may leave unwritten (scratch is reused across batches)
     for (int r = 0; r < a.zrows; ++r) {
+      // ECDSA reads r from rows [0, 17) and s from [EC_S_ROW, EC_S_ROW + 17) only
+      if (layout == LAY_SPLIT_BE && r >= 17 && r < EC_S_ROW) continue;
       bool written = false;
       if (fast) {
         if (layout == LAY_SPLIT_BE) {
