@@ -200,33 +200,37 @@ __global__ void __launch_bounds__(64) k_ec_scalar_batch(EcArgs a, int B) {
 // ------------------------------------------------------------------ point ops
 // Mixed addition P1 (Jacobian, normalized < 2p) += P2 (affine x2, y2).
 // 8M + 3S, lazy; X3, Y3 value-reduced (freduce) so they can be subtrahends.
+// Products go through mulf / sqrf (P-384: special-form reduction, which needs
+// one operand with 28-bit limbs per product -- h and r are normalised for it).
 // An exceptional pair (P1 == +-P2) yields H == 0 and so Z3 == 0, which is
 // absorbing in later additions and is detected at the end.
 template <class Fp>
 __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, const uint32_t* x2, const uint32_t* y2) {
   constexpr int L = Fp::L;
   uint32_t z1z1[L], u2[L], t[L], s2[L], h[L], r[L], hh[L], hhh[L], v[L];
-  mp::sqr<Fp>(z1z1, Z);
-  mp::mul<Fp>(u2, x2, z1z1);
-  mp::mul<Fp>(t, Z, z1z1);
-  mp::mul<Fp>(s2, y2, t);
+  mp::sqrf<Fp>(z1z1, Z);
+  mp::mulf<Fp>(u2, x2, z1z1);
+  mp::mulf<Fp>(t, Z, z1z1);
+  mp::mulf<Fp>(s2, y2, t);
   mp::sub<Fp>(h, u2, X);
   mp::sub<Fp>(r, s2, Y);
-  mp::sqr<Fp>(hh, h);
-  mp::mul<Fp>(hhh, h, hh);
-  mp::mul<Fp>(v, X, hh);
-  mp::mul<Fp>(Z, Z, h);
+  mp::norm_for_mulf<Fp>(h);                  // P-384: h, r are squared (mulf precondition)
+  mp::norm_for_mulf<Fp>(r);
+  mp::sqrf<Fp>(hh, h);
+  mp::mulf<Fp>(hhh, h, hh);
+  mp::mulf<Fp>(v, X, hh);
+  mp::mulf<Fp>(Z, Z, h);
   // X3 = r^2 - hhh - v - v: three lazy subtractions of normalized products
   // (limbs < 7 * 2^28, value < 14m) and one single-chain value fold
   uint32_t r2[L];
-  mp::sqr<Fp>(r2, r);
+  mp::sqrf<Fp>(r2, r);
   uint32_t y1[L];
   mp::copy<Fp>(y1, Y);
   mp::sub<Fp>(X, r2, hhh); mp::sub<Fp>(X, X, v); mp::sub<Fp>(X, X, v); mp::freduce_lazy<Fp>(X);
   // Y3 = r (v - X3) - Y1 hhh
   mp::sub<Fp>(t, v, X);
-  mp::mul<Fp>(Y, r, t);
-  mp::mul<Fp>(t, y1, hhh);
+  mp::mulf<Fp>(Y, r, t);
+  mp::mulf<Fp>(t, y1, hhh);
   mp::sub<Fp>(Y, Y, t); mp::freduce_lazy<Fp>(Y);
 }
 

@@ -17,6 +17,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 #include "field_consts.hpp"
 #include "mad.hpp"
@@ -77,9 +78,42 @@ MPD void red_row(uint64_t* t, uint32_t q) {
 #undef RC
 }
 
+MPD int32_t opaque_sgpr(int32_t v) {      // a constant the compiler cannot strength-reduce
+  int32_t r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "i"(v));
+  return r;
+}
+
+// Ed25519's p = 2^255 - 19: q*p = +8q at limb i+9 (255 = 9*28 + 3) and -19q at
+// limb i -- two MADs per row instead of ten.  Columns read as int64: with
+// operand limbs < 3*2^28 (mp.hpp bounds) a column stays below 10*9*2^56 < 2^63.
+MPD void mont_reduce_25519(uint32_t* r, uint64_t* t) {
+  constexpr int L = ED25519P::L;
+  int64_t* s = reinterpret_cast<int64_t*>(t);
+  const int32_t c19 = opaque_sgpr(-19), c8 = opaque_sgpr(8);
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int32_t q = (int32_t)(((uint32_t)s[i] * ED25519P::NP) & MP_MASK);
+    s[i] += (int64_t)q * (int64_t)c19;        // low 28 bits of s[i] become zero
+    s[i + 9] += (int64_t)q * (int64_t)c8;
+    s[i + 1] += s[i] >> MP_W;
+  }
+  int64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    const int64_t v = s[L + j] + c;
+    r[j] = (uint32_t)v & MP_MASK;
+    c = v >> MP_W;
+  }
+}
+
 template <class F>
 MPD void mont_reduce(uint32_t* r, uint64_t* t) {
   constexpr int L = F::L;
+  if constexpr (std::is_same<F, ED25519P>::value) {
+    mont_reduce_25519(r, t);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < L; ++i) {
     // NP1: m = -1 mod 2^28 => NP = 1, q = t[i] mod 2^28 and q*m = q*(m+1) - q:
@@ -98,11 +132,10 @@ MPD void mont_reduce(uint32_t* r, uint64_t* t) {
   }
 }
 
-// r = a*b/R mod m
+// t = a*b (2L 64-bit columns, t[2L-1] = 0)
 template <class F>
-MPD void mul(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+MPD void prod(uint64_t* t, const uint32_t* a, const uint32_t* b) {
   constexpr int L = F::L;
-  uint64_t t[2 * L];
   t[2 * L - 1] = 0;
 #pragma unroll
   for (int i = 0; i < L; ++i)
@@ -112,14 +145,12 @@ MPD void mul(uint32_t* r, const uint32_t* a, const uint32_t* b) {
       if (i == 0 || j == L - 1) mul64c(t[i + j], a[i], b[j]);
       else mad64c(t[i + j], a[i], b[j]);
     }
-  mont_reduce<F>(r, t);
 }
 
-// r = a^2/R mod m  (cross products once, doubled operand)
+// t = a^2  (cross products once, doubled operand)
 template <class F>
-MPD void sqr(uint32_t* r, const uint32_t* a) {
+MPD void sqprod(uint64_t* t, const uint32_t* a) {
   constexpr int L = F::L;
-  uint64_t t[2 * L];
   uint32_t a2[L];
 #pragma unroll
   for (int i = 0; i < L; ++i) a2[i] = a[i] << 1;
@@ -134,9 +165,80 @@ MPD void sqr(uint32_t* r, const uint32_t* a) {
       else mad64c(t[i + j], a2[i], a[j]);
     }
   }
+}
+
+// r = a*b/R mod m
+template <class F>
+MPD void mul(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  uint64_t t[2 * F::L];
+  prod<F>(t, a, b);
   mont_reduce<F>(r, t);
 }
 
+// r = a^2/R mod m
+template <class F>
+MPD void sqr(uint32_t* r, const uint32_t* a) {
+  uint64_t t[2 * F::L];
+  sqprod<F>(t, a);
+  mont_reduce<F>(r, t);
+}
+
+// P-384's special form: p + 1 = 2^384 - 2^128 - 2^96 + 2^32, i.e. per
+// reduction row +q*2^4 at limb i+1, -q*2^12 at i+3, -q*2^16 at i+4 and
+// +q*2^20 at i+13 -- four signed MADs where m+1's dense limbs cost 13.  The
+// columns are read as int64 (arithmetic carries; the low limb's "- q" is the
+// dropped low 28 bits as for every NP1 field), so every product column must
+// stay below 2^63: the caller guarantees 15 * max(a_i) * max(b_j) < 2^62.9,
+// e.g. one operand with limbs < 2^28 and the other < 2^31.  Output as
+// mont_reduce: limbs < 2^28, value < 2m.
+MPD void mont_reduce_p384(uint32_t* r, uint64_t* t) {
+  constexpr int L = P384P::L;
+  int64_t* s = reinterpret_cast<int64_t*>(t);
+  // as SGPR operands of v_mad_i64_i32 (a multiply by a visible power of two
+  // becomes a 64-bit shift + add/sub pair: 2-3 instructions instead of 1)
+  const int32_t c4 = opaque_sgpr(16), c12 = opaque_sgpr(-4096), c16 = opaque_sgpr(-65536),
+                c20 = opaque_sgpr(1048576);
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int32_t q = (int32_t)((uint32_t)s[i] & MP_MASK);
+    s[i + 1] += (int64_t)q * (int64_t)c4;
+    s[i + 3] += (int64_t)q * (int64_t)c12;
+    s[i + 4] += (int64_t)q * (int64_t)c16;
+    s[i + 13] += (int64_t)q * (int64_t)c20;
+    s[i + 1] += s[i] >> MP_W;
+  }
+  int64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    const int64_t v = s[L + j] + c;
+    r[j] = (uint32_t)v & MP_MASK;
+    c = v >> MP_W;
+  }
+}
+
+// Products for the point-addition hot loop: the field's special-form
+// reduction where it has one (P-384), else mul / sqr.  Precondition (P-384):
+// at least one operand has limbs < 2^28 (squares: the operand itself).
+template <class F>
+MPD void mulf(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  if constexpr (std::is_same<F, P384P>::value) {
+    uint64_t t[2 * F::L];
+    prod<F>(t, a, b);
+    mont_reduce_p384(r, t);
+  } else {
+    mul<F>(r, a, b);
+  }
+}
+template <class F>
+MPD void sqrf(uint32_t* r, const uint32_t* a) {
+  if constexpr (std::is_same<F, P384P>::value) {
+    uint64_t t[2 * F::L];
+    sqprod<F>(t, a);
+    mont_reduce_p384(r, t);
+  } else {
+    sqr<F>(r, a);
+  }
+}
 template <class F>
 MPD void add(uint32_t* r, const uint32_t* a, const uint32_t* b) {
 #pragma unroll
@@ -172,6 +274,12 @@ MPD void norm(uint32_t* r) {
     r[j] = v & MP_MASK;
     c = v >> MP_W;
   }
+}
+
+// lazy operands of sqrf / mulf pairs on P-384 are carry-normalised first
+template <class F>
+MPD void norm_for_mulf(uint32_t* r) {
+  if constexpr (std::is_same<F, P384P>::value) norm<F>(r);
 }
 
 // value reduction for pseudo-Mersenne-shaped primes: fold bits >= FOLD_S by 2^FOLD_S mod m

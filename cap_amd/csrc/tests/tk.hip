@@ -29,6 +29,8 @@ __global__ void k_op(int op, const uint32_t* a, const uint32_t* b, uint32_t* out
     case 4: mp::from_mont<F>(r, x); break;
     case 5: mp::sub<F>(r, x, y); mp::norm<F>(r); break;
     case 6: mp::csub<F>(r); break;
+    case 7: mp::mulf<F>(r, x, y); break;      // hot-loop products (P-384: special-form reduction)
+    case 8: mp::sqrf<F>(r, x); break;
     default: break;
   }
   if (op == 6) {

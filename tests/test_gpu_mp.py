@@ -86,6 +86,18 @@ def test_mont_mul_sqr_inv(tk, fid):
             assert max(o) <= MASK
             v = from_limbs(o)
             assert v < 2 * m and v % m == fn(x, y) % m, (op, x, y)
+    # mulf / sqrf (the point loop's products; P-384 uses its special-form
+    # signed reduction): one operand with 28-bit limbs, the other lazy up to
+    # the sub bound (a + KSUB - b); squares of normalized values
+    lz = [x + (2 * m if i % 2 and x + 2 * m < R else 0) for i, x in enumerate(ys)]
+    xn = [x % m + (m if i % 3 == 0 else 0) for i, x in enumerate(xs)]
+    for op, a_, b_, fn in ((7, xn, lz, lambda x, y: x * y * Ri), (7, lz, xn, lambda x, y: x * y * Ri),
+                           (8, xn, xn, lambda x, y: x * x * Ri)):
+        out = run_field(tk, fid, op, a_, b_)
+        for x, y, o in zip(a_, b_, out):
+            assert max(o) <= MASK
+            v = from_limbs(o)
+            assert v < 2 * m and v % m == fn(x, y) % m, (op, x, y)
     # inverse of Montgomery-form values
     # (safegcd: random values plus the small / near-m / power-of-two / lazy
     # inputs that stress the divstep sign handling and the final normalisation)
