@@ -62,7 +62,7 @@ int cls_rows_scratch(int c) {
   switch (c) {
     case CLS_RSA2K: case CLS_RSA3K: case CLS_RSA4K: return 2 * rsa_limbs(c) + SIGW_ROWS;
     case CLS_P256: case CLS_P384: case CLS_P521: return ec_digit_rows(c) + 2 * ec_limbs(c);
-    case CLS_ED25519: return 3 * ED_L;
+    case CLS_ED25519: return 4 * ED_L;
     default: return 0;
   }
 }

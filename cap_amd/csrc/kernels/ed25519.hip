@@ -13,6 +13,8 @@
 // (non-canonical y accepted, x = 0 with the sign bit set accepted).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "common.hpp"
 #include "ed25519.hpp"
 #include "mp.hpp"
@@ -156,30 +158,74 @@ __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
   if (!ok) a.status[p] = ST_REJECT;
 }
 
-__global__ void __launch_bounds__(64) k_ed_finish(EdArgs a) {
-  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
+// Batched finish (Montgomery's trick, as k_ec_scalar_batch): thread i owns the
+// B tokens p_j = begin + i + j*S and pays ONE inversion for all their Z:
+//   pass 1: c_j = Z_0 ... Z_j, parked in the prefix rows;  inv = c_{B-1}^-1
+//   pass 2 (j descending): Z_j^-1 = inv * c_{j-1}, inv *= Z_j; affine x, y,
+//           canonical encoding, byte compare with R.
+// Z != 0 for every output of the complete addition law; padding and rejected
+// tokens contribute Z = 1.
+__global__ void __launch_bounds__(64) k_ed_finish(EdArgs a, int B) {
   const int64_t np = a.npad;
-  const int32_t t = a.perm[p];
-  if (t < 0) return;
-  if (a.status[p] != ST_OK) { a.verdict_pad[p] = 0; return; }
-  uint32_t X[L], Y[L], Z[L];
+  const int64_t n = a.end - a.begin;
+  const int64_t S = (n + B - 1) / B;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S) return;
+  uint32_t* pre = a.xyz + (int64_t)3 * L * np;
+  auto live = [&](int64_t p) { return a.perm[p] >= 0 && a.status[p] == ST_OK; };
+  auto load_z = [&](int64_t p, uint32_t* Z) {
+    if (live(p)) {
 #pragma unroll
-  for (int j = 0; j < L; ++j) {
-    X[j] = a.xyz[(int64_t)j * np + p];
-    Y[j] = a.xyz[(int64_t)(L + j) * np + p];
-    Z[j] = a.xyz[(int64_t)(2 * L + j) * np + p];
+      for (int j = 0; j < L; ++j) Z[j] = a.xyz[(int64_t)(2 * L + j) * np + p];
+    } else {
+      mp::set_const<Fp>(Z, Fp::ONE);
+    }
+  };
+  uint32_t acc[L];
+  mp::set_const<Fp>(acc, Fp::ONE);
+  int nb = 0;
+  for (int j = 0; j < B; ++j) {
+    const int64_t p = a.begin + i + (int64_t)j * S;
+    if (p >= a.end) break;
+    uint32_t Z[L];
+    load_z(p, Z);
+    mp::mul<Fp>(acc, acc, Z);
+#pragma unroll
+    for (int k = 0; k < L; ++k) pre[(int64_t)k * np + p] = acc[k];
+    ++nb;
   }
-  uint32_t zi[L], x[L], y[L], tt[L];
-  mp::inv<Fp>(zi, Z);
-  mp::mul<Fp>(tt, X, zi); mp::from_mont<Fp>(x, tt);
-  mp::mul<Fp>(tt, Y, zi); mp::from_mont<Fp>(y, tt);
-  uint32_t enc[8];
-  mp::limbs_to_words<L, 8>(enc, y);
-  enc[7] = (enc[7] & 0x7fffffffu) | ((x[0] & 1u) << 31);
-  uint32_t diff = 0;
+  uint32_t inv[L];
+  mp::inv<Fp>(inv, acc);
+  for (int j = nb - 1; j >= 0; --j) {
+    const int64_t p = a.begin + i + (int64_t)j * S;
+    uint32_t cprev[L], Z[L], zi[L];
+    if (j > 0) {
 #pragma unroll
-  for (int q = 0; q < 8; ++q) diff |= enc[q] ^ a.sigw[(int64_t)q * np + p];
-  a.verdict_pad[p] = diff == 0;
+      for (int k = 0; k < L; ++k) cprev[k] = pre[(int64_t)k * np + p - S];
+    } else {
+      mp::set_const<Fp>(cprev, Fp::ONE);
+    }
+    load_z(p, Z);
+    mp::mul<Fp>(zi, inv, cprev);                 // Z_j^-1 (Montgomery)
+    mp::mul<Fp>(inv, inv, Z);
+    if (a.perm[p] < 0) continue;
+    if (a.status[p] != ST_OK) { a.verdict_pad[p] = 0; continue; }
+    uint32_t X[L], Y[L], x[L], y[L], tt[L];
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      X[k] = a.xyz[(int64_t)k * np + p];
+      Y[k] = a.xyz[(int64_t)(L + k) * np + p];
+    }
+    mp::mul<Fp>(tt, X, zi); mp::from_mont<Fp>(x, tt);
+    mp::mul<Fp>(tt, Y, zi); mp::from_mont<Fp>(y, tt);
+    uint32_t enc[8];
+    mp::limbs_to_words<L, 8>(enc, y);
+    enc[7] = (enc[7] & 0x7fffffffu) | ((x[0] & 1u) << 31);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) diff |= enc[q] ^ a.sigw[(int64_t)q * np + p];
+    a.verdict_pad[p] = diff == 0;
+  }
 }
 
 // ------------------------------------------------------------------ staging
@@ -340,7 +386,11 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   dim3 g((unsigned)waves), b(WAVE);
   hipLaunchKernelGGL(k_ed_point, g, b, 0, s, a);
   mk("point");
-  hipLaunchKernelGGL(k_ed_finish, g, b, 0, s, a);
+  // tokens per thread for the batched inversion: keep >= ~8 waves per CU
+  const int64_t n = a.end - a.begin;
+  const int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * 8 * WAVE)));
+  const int64_t S = (n + B - 1) / B;
+  hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)((S + WAVE - 1) / WAVE)), b, 0, s, a, B);
   mk("finish");
 }
 

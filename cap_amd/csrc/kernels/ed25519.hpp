@@ -16,7 +16,8 @@ struct EdArgs {
   uint8_t* status;
   const uint16_t* siglen;
   uint8_t* verdict_pad;
-  uint32_t* xyz;              // X, Y, Z of R' (3 x 10 limb rows)
+  uint32_t* xyz;              // X, Y, Z of R' (3 x 10 limb rows), then 10 rows of
+                              // k_ed_finish's prefix products
   const uint32_t* btab;       // comb table of the base point B (Niels form)
   int64_t npad, begin, end;
 };
