@@ -130,6 +130,7 @@ struct jg_batch {
   int64_t pss_tokens = 0;
   ClassRange ranges[NCLS] = {};
   int hash_mask[NCLS] = {};       // per class: bit 0 SHA-256 present, bit 1 SHA-384/512
+  int pss_any[NCLS] = {};         // per class: some token uses RSASSA-PSS (PS256/384/512)
   uint64_t epoch = 0;
   bool timing = true;
   // timing marks of the most recent run: events are created once and
@@ -244,13 +245,14 @@ void stage(jg_ctx* ctx, jg_batch* b, const uint8_t* arena, size_t arena_len, con
   const size_t nbuck = (size_t)NCLS * (nkeys > 0 ? nkeys : 1);
   std::vector<int64_t> cnt(nbuck, 0);
   std::vector<int> tcls(ntok);
-  for (int c = 0; c < NCLS; ++c) b->hash_mask[c] = 0;
+  for (int c = 0; c < NCLS; ++c) b->hash_mask[c] = b->pss_any[c] = 0;
   for (size_t i = 0; i < ntok; ++i) {
     const int c = classify(ctx, toks[i]);
     if (c < 0) throw std::invalid_argument("jg_tok.key_idx out of range of the loaded key table");
     tcls[i] = c;
     const int alg = toks[i].alg;
     b->hash_mask[c] |= (alg == JG_RS256 || alg == JG_PS256 || alg == JG_ES256) ? 1 : 2;
+    if (alg >= JG_PS256 && alg <= JG_PS512) b->pss_any[c] = 1;
     cnt[(size_t)c * nkeys + (c == CLS_REJECT ? 0 : toks[i].key_idx)]++;
   }
   // bucket order: classes 1..NCLS-1 by key, then the reject bucket
@@ -357,6 +359,7 @@ void run(jg_ctx* ctx, jg_batch* b) {
       ra.yw = rows + (size_t)2 * L * np;
       ra.status = pa.status; ra.siglen = pa.siglen; ra.verdict_pad = (uint8_t*)B->vpad.p;
       ra.pss_scratch = (uint8_t*)B->pss.p;
+      ra.has_pss = b->pss_any[c];
       ra.npad = np; ra.begin = r.begin; ra.end = r.end;
       launch_rsa(c, ra, s, marker(b, c));
     } else if (c <= CLS_P521) {

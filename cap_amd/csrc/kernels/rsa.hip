@@ -323,6 +323,7 @@ __device__ void hash_buf(int hb, const uint8_t* buf, uint32_t len, uint32_t* out
   }
 }
 
+template <bool PSS>
 __global__ void __launch_bounds__(64) k_rsa_pad(RsaArgs a) {
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
@@ -350,22 +351,25 @@ __global__ void __launch_bounds__(64) k_rsa_pad(RsaArgs a) {
       const int nw = (k + 3) / 4;
       for (int q = hlen / 4; q < nw; ++q) {
         const uint32_t yv = a.yw[(int64_t)q * np + p];
-        uint32_t ev = 0;
+        uint32_t ev = 0xffffffffu;          // the FF run: every word but the ~8 at its ends
+        if (4 * q <= tlen || 4 * q + 3 >= k - 2) {
+          ev = 0;
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb) {
-          const int j = 4 * q + bb;
-          uint32_t ex;
-          if (j < tlen) ex = DI[tlen - 1 - j];
-          else if (j == tlen) ex = 0;
-          else if (j < k - 2) ex = 0xff;
-          else if (j == k - 2) ex = 1;
-          else ex = 0;                      // j == k-1, and j >= k (y < n < 2^(8k))
-          ev |= ex << (8 * bb);
+          for (int bb = 0; bb < 4; ++bb) {
+            const int j = 4 * q + bb;
+            uint32_t ex;
+            if (j < tlen) ex = DI[tlen - 1 - j];
+            else if (j == tlen) ex = 0;
+            else if (j < k - 2) ex = 0xff;
+            else if (j == k - 2) ex = 1;
+            else ex = 0;                    // j == k-1, and j >= k (y < n < 2^(8k))
+            ev |= ex << (8 * bb);
+          }
         }
         diff |= yv ^ ev;
       }
       verdict = ok && diff == 0;
-    } else {
+    } else if constexpr (PSS) {
       // EMSA-PSS-VERIFY with auto salt length (R16)
       const int embits = K.embits;
       const int emlen = (embits + 7) / 8;
@@ -478,7 +482,8 @@ void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const Marker& mk) {
     default: return;
   }
   mk("modexp");
-  hipLaunchKernelGGL(k_rsa_pad, g, b, 0, s, a);
+  if (a.has_pss) hipLaunchKernelGGL(k_rsa_pad<true>, g, b, 0, s, a);
+  else hipLaunchKernelGGL(k_rsa_pad<false>, g, b, 0, s, a);
   mk("pad");
 }
 

@@ -21,6 +21,7 @@ struct RsaArgs {
   const uint16_t* siglen;
   uint8_t* verdict_pad;
   uint8_t* pss_scratch;       // 2 KiB per token of the class range
+  int32_t has_pss;            // the range holds PS* tokens (else the PKCS#1-only pad kernel)
   int64_t npad, begin, end;
 };
 
