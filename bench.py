@@ -33,6 +33,7 @@ KEYDIR = os.path.join(ROOT, "tests", "golden", "keys")
 BENCHKEYS = os.path.join(ROOT, "tools", "benchkeys")
 TOKGEN = os.path.join(ROOT, "tools", "tokgen", "tokgen")
 TRAFFIC = os.path.join(ROOT, "profiles", "r01_s5_pmc_traffic.json")
+COLL_DEVICE = "cuda"            # device of the timing all-reduce (RCCL); "cpu" under gloo
 
 # measured v_mad_u64_u32 issue rate, chip-wide: the integer multiply-add
 # roofline denominator.  36.98 T lane-MAD/s = 8 waves/SIMD, 8 MADs per asm
@@ -180,7 +181,7 @@ def measure(ctx, arena, toks, steps, warmup, dist):
     if dist:
         import torch
         torch.cuda.synchronize()
-        elapsed = max_over_ranks(elapsed, device="cuda")
+        elapsed = max_over_ranks(elapsed, device=COLL_DEVICE)
     b.free()
     kms = {k: float(np.mean(x)) for k, x in times.items()}
     return elapsed, accepted, kms, v
@@ -422,15 +423,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    dev = local
     if dist:
         import torch
         import torch.distributed as td
-        torch.cuda.set_device(local)
-        td.init_process_group("nccl")
+        ndev = torch.cuda.device_count()          # does not initialise the GPU
+        dev = local % max(1, ndev)
+        # one rank per GPU over RCCL; more ranks than GPUs (a rehearsal of the
+        # N>1 path on a 1-GPU box) share devices and time through gloo
+        global COLL_DEVICE
+        COLL_DEVICE = "cuda" if world <= ndev else "cpu"
+        torch.cuda.set_device(dev)
+        td.init_process_group("nccl" if COLL_DEVICE == "cuda" else "gloo")
     from cap_amd import _lib
 
     host_threads = max(1, min(16, os.cpu_count() or 1))
-    ctx = _lib.Context([local])
+    ctx = _lib.Context([dev])
 
     # ---- ES256, P-256 JWKS with 4 kids (configs[1])
     kids = ["p256-a", "p256-b", "p256-c", "p256-d"]
