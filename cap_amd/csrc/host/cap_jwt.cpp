@@ -516,6 +516,9 @@ class JSONWebKeySet final : public KeySet {
         for (size_t i = lo; i < hi; ++i) (*info)[i] = std::move(V.toks[i].info);
       });
     }
+    pt.lap("info");
+    V.toks.release();
+    pt.lap("free-toks");
     return res;
   }
 
@@ -955,6 +958,7 @@ std::vector<Result> Validator::ValidateBatch(const std::vector<std::string_view>
   PhaseTimer pt("validate");
   const int64_t now = expected.has_now ? expected.now_unix_ns : wall_now_ns();
   std::vector<Result> out(tokens.size());
+  pt.lap("alloc");
   parallel_for(tokens.size(), host_threads(), [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
       if (!sig[i].ok) {

@@ -3,6 +3,10 @@
 // tests do (jwt/keyset_test.go, jwt/jwt_test.go).  Values cross as Go would
 // hand them out: claims map -> dict with float64 numbers; error -> str or None.
 #include <pybind11/functional.h>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -342,11 +346,23 @@ PYBIND11_MODULE(_capjwt_host, m) {
         std::string ok;
         {
           py::gil_scoped_release rel;
+          const bool trace = std::getenv("CAPJWT_TRACE") != nullptr;
+          auto t0 = std::chrono::steady_clock::now();
+          auto lap = [&](const char* what) {
+            if (!trace) return;
+            const auto t1 = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "[capjwt] blob %-12s %8.2f ms\n", what,
+                         std::chrono::duration<double, std::milli>(t1 - t0).count());
+            t0 = t1;
+          };
           auto toks = split_lines(bp, (size_t)bn);
+          lap("split");
           auto rs = s.v->ValidateBatch(toks, e);
+          lap("validate");
           ok.resize(rs.size());
           for (size_t i = 0; i < rs.size(); ++i) ok[i] = rs[i].ok ? 1 : 0;
           release_results(rs);
+          lap("release");
         }
         return py::bytes(ok);
       });
