@@ -954,28 +954,30 @@ Result Validator::Validate(std::string_view token, const Expected& expected) {
 
 std::vector<Result> Validator::ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected) {
   std::vector<TokenInfo> info;
-  std::vector<Result> sig = ks_->verify_batch(tokens, &info);
+  std::vector<Result> res = ks_->verify_batch(tokens, &info);
   PhaseTimer pt("validate");
   const int64_t now = expected.has_now ? expected.now_unix_ns : wall_now_ns();
-  std::vector<Result> out(tokens.size());
-  pt.lap("alloc");
+  // results are rewritten in place (no second 1M-entry vector to build and
+  // free serially); a claims map that fails validation is destroyed here, by
+  // the host threads
   parallel_for(tokens.size(), host_threads(), [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
-      if (!sig[i].ok) {
-        out[i].err = "error verifying token signature: " + sig[i].err;
+      Result& r = res[i];
+      if (!r.ok) {
+        r.err = "error verifying token signature: " + r.err;
         continue;
       }
-      out[i] = validate_claims(sig[i].claims, info[i], expected, now);
-      if (out[i].ok) out[i].claims = std::move(sig[i].claims);
+      Result v = validate_claims(r.claims, info[i], expected, now);
+      if (v.ok) v.claims = std::move(r.claims);
+      r = std::move(v);
     }
   });
   pt.lap("claims");
-  release_results(sig);
   parallel_for(info.size(), host_threads(), [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) info[i] = TokenInfo();
   });
   pt.lap("release");
-  return out;
+  return res;
 }
 
 // ====================================================================== oidc hash claims
