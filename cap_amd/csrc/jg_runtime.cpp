@@ -19,6 +19,7 @@
 #include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -101,11 +102,23 @@ struct HostKey {
   int kind = 0, cls = CLS_REJECT, valid = 0;
 };
 
+// Fixed-base tables of the curve generators / Ed25519 base point depend only
+// on (device, curve), so every jg_ctx of the process shares one copy per device
+// (the P-256 one is 7.4 GB and takes 0.3 s to build).  Freed with the last
+// context that holds it.
+struct SharedTable {
+  uint32_t* p = nullptr;
+  ~SharedTable() { if (p) (void)hipFree(p); }
+};
+std::mutex g_tab_mu;
+std::map<std::pair<int, int>, std::weak_ptr<SharedTable>> g_tabs;   // (device id, class) -> table
+
 struct Device {
   int id = 0;
   hipStream_t stream = nullptr;
   uint32_t* gtab[NCLS] = {};
   uint32_t* btab = nullptr;
+  std::shared_ptr<SharedTable> tab_ref[NCLS];   // keeps gtab / btab alive
   DevKey* dkeys = nullptr;
   uint32_t* dblob = nullptr;
   int32_t* didx = nullptr;
@@ -513,16 +526,34 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
   for (int k : S.tab_keys) S.dk[k].tab_off += S.blob.size();
 }
 
+// the process-wide table of (device, class), built on this device's stream
+// and complete before any other context can see it
+template <class Build>
+std::shared_ptr<SharedTable> shared_table(Device* d, int cls, size_t bytes, Build&& build) {
+  std::lock_guard<std::mutex> g(g_tab_mu);
+  const auto key = std::make_pair(d->id, cls);
+  if (auto t = g_tabs[key].lock()) return t;
+  auto t = std::make_shared<SharedTable>();
+  HIPCHK(hipMalloc(&t->p, bytes));
+  build(t->p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(d->stream));
+  g_tabs[key] = t;
+  return t;
+}
+
 void ensure_tables(Device* d, const StagedKeys& S) {
   HIPCHK(hipSetDevice(d->id));
   for (int c = CLS_P256; c <= CLS_P521; ++c) {
     if (S.ec_idx[c].empty() || d->gtab[c]) continue;
-    HIPCHK(hipMalloc(&d->gtab[c], sizeof(uint32_t) * ec_table_words(c, true)));
-    launch_ec_gtable(c, d->gtab[c], d->stream);
+    d->tab_ref[c] = shared_table(d, c, sizeof(uint32_t) * ec_table_words(c, true),
+                                 [&](uint32_t* t) { launch_ec_gtable(c, t, d->stream); });
+    d->gtab[c] = d->tab_ref[c]->p;
   }
   if (!S.ed_idx.empty() && !d->btab) {
-    HIPCHK(hipMalloc(&d->btab, sizeof(uint32_t) * ed_table_words(true)));
-    launch_ed_btable(d->btab, d->stream);
+    d->tab_ref[CLS_ED25519] = shared_table(d, CLS_ED25519, sizeof(uint32_t) * ed_table_words(true),
+                                           [&](uint32_t* t) { launch_ed_btable(t, d->stream); });
+    d->btab = d->tab_ref[CLS_ED25519]->p;
   }
 }
 
@@ -596,8 +627,7 @@ void jg_destroy(jg_ctx* ctx) {
     (void)hipSetDevice(d->id);
     (void)hipStreamSynchronize(d->stream);
     d->sync_bufs.reset();
-    for (auto& t : d->gtab) if (t) (void)hipFree(t);
-    if (d->btab) (void)hipFree(d->btab);
+    for (auto& t : d->tab_ref) t.reset();         // shared fixed-base tables: last holder frees
     if (d->dkeys) (void)hipFree(d->dkeys);
     if (d->dblob) (void)hipFree(d->dblob);
     if (d->didx) (void)hipFree(d->didx);

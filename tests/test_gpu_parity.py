@@ -93,3 +93,26 @@ def test_cross_product_every_token_every_key(ctx):
     bad = [i for i, w in enumerate(want) if out[i] != w]
     assert not bad, (len(bad), bad[:20])
     assert sum(want) > 150
+
+
+def test_contexts_share_fixed_base_tables():
+    """The generator / base-point tables are one copy per device shared by every
+    jg_ctx (jg_runtime.cpp shared_table): a second context verifies with them,
+    and keeps verifying after the context that built them is destroyed."""
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    pick = [t for t in toks if t["name"].startswith(("valid-ES256", "valid-ES384", "valid-ES512", "valid-EdDSA",
+                                                     "tamper-sig-ES", "tamper-sig-EdDSA"))]
+    a = _lib.Context()
+    a.load_keys([H.abi_key(k) for k in keys])
+    arena, slots = H.jobs_from_tokens(pick, kid_index)
+    want = [t["verdict"] for t in pick]
+    assert [a.verify(arena)[s] for s in slots] == want
+    b = _lib.Context()
+    b.load_keys([H.abi_key(k) for k in keys])
+    assert [b.verify(arena)[s] for s in slots] == want
+    a.close()
+    arena2, slots2 = H.jobs_from_tokens(pick, kid_index)
+    assert [b.verify(arena2)[s] for s in slots2] == want
+    b.close()
