@@ -119,6 +119,11 @@ struct Device {
   uint32_t* gtab[NCLS] = {};
   uint32_t* btab = nullptr;
   std::shared_ptr<SharedTable> tab_ref[NCLS];   // keeps gtab / btab alive
+  // untimed runs with several classes: one stream per class so the classes'
+  // kernel chains overlap (a mixed batch's per-class ranges are each too small
+  // to fill 256 CUs alone); joined back into `stream` before the scatter
+  hipStream_t cstream[NCLS] = {};
+  hipEvent_t ev_start = nullptr, ev_done[NCLS] = {};
   DevKey* dkeys = nullptr;
   uint32_t* dblob = nullptr;
   int32_t* didx = nullptr;
@@ -140,7 +145,8 @@ struct jg_batch {
   int64_t ntok = 0, npad = 0;
   size_t arena_len = 0;
   int sig_rows = 0, scratch_rows = 0;
-  int64_t pss_tokens = 0;
+  int64_t pss_tokens = 0;          // PSS scratch tokens: the RSA classes' ranges back to back
+  int64_t pss_off[NCLS] = {};
   ClassRange ranges[NCLS] = {};
   int hash_mask[NCLS] = {};       // per class: bit 0 SHA-256 present, bit 1 SHA-384/512
   int pss_any[NCLS] = {};         // per class: some token uses RSASSA-PSS (PS256/384/512)
@@ -302,7 +308,10 @@ void stage(jg_ctx* ctx, jg_batch* b, const uint8_t* arena, size_t arena_len, con
     if (b->ranges[c].end <= b->ranges[c].begin) continue;
     b->sig_rows = std::max(b->sig_rows, cls_rows_sig(c));
     b->scratch_rows = std::max(b->scratch_rows, cls_rows_scratch(c));
-    if (c <= CLS_RSA4K) b->pss_tokens = std::max(b->pss_tokens, b->ranges[c].end - b->ranges[c].begin);
+    if (c <= CLS_RSA4K) {
+      b->pss_off[c] = b->pss_tokens;
+      b->pss_tokens += b->ranges[c].end - b->ranges[c].begin;
+    }
   }
   Bufs* B = b->b;
   hipStream_t s = d->stream;
@@ -325,19 +334,25 @@ void stage(jg_ctx* ctx, jg_batch* b, const uint8_t* arena, size_t arena_len, con
   B->rows.get(sizeof(uint32_t) * (size_t)b->scratch_rows * npad);
   B->pss.get((size_t)std::max<int64_t>(b->pss_tokens, 1) * 2048);
   B->exc.get(sizeof(int32_t) * npad);
-  B->exc_cnt.get(sizeof(uint32_t) * 4);
+  B->exc_cnt.get(sizeof(uint32_t) * NCLS);
   // the host vectors die here: the copies above must complete first
   HIPCHK(hipStreamSynchronize(s));
   b->epoch = ctx->epoch;
 }
 
-void run(jg_ctx* ctx, jg_batch* b) {
+// timed: per-kernel HIP events (classes in sequence on the device stream);
+// untimed: classes on their own streams, overlapping.
+void run(jg_ctx* ctx, jg_batch* b, bool timed) {
   Device* d = b->dev;
   HIPCHK(hipSetDevice(d->id));
   if (b->epoch != ctx->epoch) throw std::runtime_error("key table reloaded since this batch was staged");
   Bufs* B = b->b;
   hipStream_t s = d->stream;
+  b->timing = timed;
   b->marks_used = 0;
+  int nact = 0;
+  for (int c = 1; c < NCLS; ++c) nact += b->ranges[c].end > b->ranges[c].begin;
+  const bool conc = !timed && nact > 1;
   const int64_t np = b->npad;
   mark(b, "begin");
   HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, s));
@@ -354,9 +369,18 @@ void run(jg_ctx* ctx, jg_batch* b) {
   pa.siglen = (uint16_t*)B->siglen.p;
   pa.npad = np;
   uint32_t* rows = (uint32_t*)B->rows.p;
+  if (conc) HIPCHK(hipEventRecord(d->ev_start, s));
+  const hipStream_t s0 = s;
   for (int c = 1; c < NCLS; ++c) {
     const ClassRange r = b->ranges[c];
     if (r.end <= r.begin) continue;
+    // every class reads and writes only columns [r.begin, r.end) of the shared
+    // scratch rows, its own exception counter and its own PSS scratch
+    hipStream_t s = s0;
+    if (conc) {
+      s = d->cstream[c];
+      HIPCHK(hipStreamWaitEvent(s, d->ev_start, 0));
+    }
     pa.begin = r.begin;
     pa.end = r.end;
     pa.zrows = cls_rows_sig(c);
@@ -371,7 +395,7 @@ void run(jg_ctx* ctx, jg_batch* b) {
       ra.xlr = rows + (size_t)L * np;
       ra.yw = rows + (size_t)2 * L * np;
       ra.status = pa.status; ra.siglen = pa.siglen; ra.verdict_pad = (uint8_t*)B->vpad.p;
-      ra.pss_scratch = (uint8_t*)B->pss.p;
+      ra.pss_scratch = (uint8_t*)B->pss.p + b->pss_off[c] * 2048;
       ra.has_pss = b->pss_any[c];
       ra.npad = np; ra.begin = r.begin; ra.end = r.end;
       launch_rsa(c, ra, s, marker(b, c));
@@ -384,8 +408,8 @@ void run(jg_ctx* ctx, jg_batch* b) {
       ea.u1w = rows + (size_t)ec_digit_rows(c) * np;
       ea.u2w = rows + (size_t)(ec_digit_rows(c) + ec_limbs(c)) * np;
       ea.gtab = d->gtab[c];
-      ea.exc_list = (int32_t*)B->exc.p;
-      ea.exc_count = (uint32_t*)B->exc_cnt.p;
+      ea.exc_list = (int32_t*)B->exc.p + r.begin;
+      ea.exc_count = (uint32_t*)B->exc_cnt.p + c;
       ea.npad = np; ea.begin = r.begin; ea.end = r.end;
       launch_ec(c, ea, s, marker(b, c));
     } else {
@@ -397,6 +421,10 @@ void run(jg_ctx* ctx, jg_batch* b) {
       ea.btab = d->btab;
       ea.npad = np; ea.begin = r.begin; ea.end = r.end;
       launch_ed(ea, s, marker(b, c));
+    }
+    if (conc) {
+      HIPCHK(hipEventRecord(d->ev_done[c], s));
+      HIPCHK(hipStreamWaitEvent(s0, d->ev_done[c], 0));
     }
   }
   launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s);
@@ -611,6 +639,11 @@ jg_ctx* jg_create(const int* devices, int ndev) {
       d->id = id;
       HIPCHK(hipSetDevice(id));
       HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+      for (int c = 1; c < NCLS; ++c) {
+        HIPCHK(hipStreamCreateWithFlags(&d->cstream[c], hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&d->ev_done[c], hipEventDisableTiming));
+      }
+      HIPCHK(hipEventCreateWithFlags(&d->ev_start, hipEventDisableTiming));
       d->sync_bufs = std::make_unique<Bufs>();
       ctx->devs.push_back(std::move(d));
     }
@@ -631,6 +664,12 @@ void jg_destroy(jg_ctx* ctx) {
     if (d->dkeys) (void)hipFree(d->dkeys);
     if (d->dblob) (void)hipFree(d->dblob);
     if (d->didx) (void)hipFree(d->didx);
+    for (int c = 1; c < NCLS; ++c) {
+      if (d->cstream[c]) (void)hipStreamSynchronize(d->cstream[c]);
+      if (d->cstream[c]) (void)hipStreamDestroy(d->cstream[c]);
+      if (d->ev_done[c]) (void)hipEventDestroy(d->ev_done[c]);
+    }
+    if (d->ev_start) (void)hipEventDestroy(d->ev_start);
     (void)hipStreamDestroy(d->stream);
   }
   delete ctx;
@@ -695,7 +734,7 @@ int jg_batch_run(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out) {
   if (!ctx || !b) return -1;
   try {
     std::lock_guard<std::mutex> g(b->dev->mu);
-    run(ctx, b);
+    run(ctx, b, true);
     if (verdict_out) {
       if (b->ntok > 0)
         HIPCHK(hipMemcpyAsync(verdict_out, b->b->verdict.p, (size_t)b->ntok, hipMemcpyDeviceToHost, b->dev->stream));
@@ -713,7 +752,7 @@ int jg_batch_enqueue(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out) {
   if (!ctx || !b) return -1;
   try {
     std::lock_guard<std::mutex> g(b->dev->mu);
-    run(ctx, b);
+    run(ctx, b, false);
     if (verdict_out && b->ntok > 0)
       HIPCHK(hipMemcpyAsync(verdict_out, b->b->verdict.p, (size_t)b->ntok, hipMemcpyDeviceToHost, b->dev->stream));
     return 0;
@@ -789,7 +828,7 @@ int jg_verify_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
       b.b = d->sync_bufs.get();
       b.timing = false;
       stage(ctx, &b, arena, arena_len, toks + lo, hi - lo);
-      run(ctx, &b);
+      run(ctx, &b, false);
       HIPCHK(hipMemcpyAsync(verdict_out + lo, b.b->verdict.p, hi - lo, hipMemcpyDeviceToHost, d->stream));
       HIPCHK(hipStreamSynchronize(d->stream));
     } catch (const std::invalid_argument& e) {
