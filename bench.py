@@ -57,12 +57,14 @@ def p256_point_mads_per_token():
     2^256 mod p); signed comb digits (ecdsa.hpp ec_comb_w): 11 windows of 24
     bits for u1 (generator table) and 13 of 20 bits for u2 (key table), each
     non-zero w.p. 1 - 2^-W (the top windows never carry), the first addition an
-    assignment; final check 1 sqr + 2 mul."""
+    assignment and the second onto Z == 1 (madd_z1: 4 mul + 2 sqr); final check
+    1 sqr + 2 mul."""
     L, red, fold = 10, 10 * 4, 6
     mul, sqr = L * L + red, L * (L + 1) // 2 + red
-    madd = 8 * mul + 3 * sqr + 3 * fold
+    madd = 8 * mul + 3 * sqr + 2 * fold
+    madd_z1 = 4 * mul + 2 * sqr + 2 * fold
     adds = 11 * (1 - 2.0 ** -24) + 13 * (1 - 2.0 ** -20) - 1
-    return adds * madd + sqr + 2 * mul
+    return (adds - 1) * madd + madd_z1 + sqr + 2 * mul
 
 
 def rsa_modexp_mads_per_token(limbs):

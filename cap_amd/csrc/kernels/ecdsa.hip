@@ -234,7 +234,31 @@ __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, cons
   mp::sub<Fp>(Y, Y, t); mp::freduce_lazy<Fp>(Y);
 }
 
-template <class CV, bool GEN>
+// madd with Z1 == 1 (P1 affine: the accumulator after its first assignment):
+// u2 = x2, s2 = y2, Z3 = h -- 4M + 2S instead of 8M + 3S.
+template <class Fp>
+__device__ __forceinline__ void madd_z1(uint32_t* X, uint32_t* Y, uint32_t* Z, const uint32_t* x2, const uint32_t* y2) {
+  constexpr int L = Fp::L;
+  uint32_t h[L], r[L], hh[L], hhh[L], v[L], t[L], r2[L], y1[L];
+  mp::sub<Fp>(h, x2, X);
+  mp::sub<Fp>(r, y2, Y);
+  mp::norm<Fp>(h);                           // Z3 = h: 28-bit limbs (mulf operand), value < 6m
+  mp::norm_for_mulf<Fp>(r);
+  mp::sqrf<Fp>(hh, h);
+  mp::mulf<Fp>(hhh, h, hh);
+  mp::mulf<Fp>(v, X, hh);
+  mp::copy<Fp>(Z, h);
+  mp::sqrf<Fp>(r2, r);
+  mp::copy<Fp>(y1, Y);
+  mp::sub<Fp>(X, r2, hhh); mp::sub<Fp>(X, X, v); mp::sub<Fp>(X, X, v); mp::freduce_lazy<Fp>(X);
+  mp::sub<Fp>(t, v, X);
+  mp::mulf<Fp>(Y, r, t);
+  mp::mulf<Fp>(t, y1, hhh);
+  mp::sub<Fp>(Y, Y, t); mp::freduce_lazy<Fp>(Y);
+}
+
+// Z1ONE: the accumulator, if not empty, holds exactly one table entry (Z == 1)
+template <class CV, bool GEN, bool Z1ONE = false>
 __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z, bool& empty,
                                            const uint32_t* __restrict__ tab, int w, int d) {
   using Fp = typename CV::Fp;
@@ -251,6 +275,8 @@ __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z
     mp::copy<Fp>(Y, y2); mp::freduce<Fp>(Y);
     mp::set_const<Fp>(Z, Fp::ONE);
     empty = false;
+  } else if constexpr (Z1ONE) {
+    madd_z1<Fp>(X, Y, Z, x2, y2);
   } else {
     madd<Fp>(X, Y, Z, x2, y2);
   }
@@ -274,7 +300,10 @@ __global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
 
   uint32_t X[L], Y[L], Z[L];
   bool empty = true;
-  for (int w = 0; w < NWIN; ++w) {
+  // window 0 peeled: its G entry is an assignment, so its Q entry adds onto Z == 1
+  add_window<CV, true>(X, Y, Z, empty, gtab, 0, (int)a.digs[p]);
+  add_window<CV, false, true>(X, Y, Z, empty, qtab, 0, (int)a.digs[(int64_t)NG * np + p]);
+  for (int w = 1; w < NWIN; ++w) {
     if (w < NG) add_window<CV, true>(X, Y, Z, empty, gtab, w, (int)a.digs[(int64_t)w * np + p]);
     if (w < NQ) add_window<CV, false>(X, Y, Z, empty, qtab, w, (int)a.digs[(int64_t)(NG + w) * np + p]);
   }

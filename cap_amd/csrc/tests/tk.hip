@@ -94,7 +94,7 @@ extern "C" int tk_field_op(int field, int op, const uint32_t* a, const uint32_t*
 // ---------------------------------------------------------------- EC level
 namespace {
 
-template <class CV>
+template <class CV, bool Z1>
 __global__ void k_tk_madd(const uint32_t* in, uint32_t* out, int n) {
   // in per lane: X Y Z x2 y2 (5L words); out: X Y Z (3L)
   using Fp = typename CV::Fp;
@@ -104,7 +104,8 @@ __global__ void k_tk_madd(const uint32_t* in, uint32_t* out, int n) {
   uint32_t X[L], Y[L], Z[L], x2[L], y2[L];
   const uint32_t* s = in + (size_t)i * 5 * L;
   for (int j = 0; j < L; ++j) { X[j] = s[j]; Y[j] = s[L + j]; Z[j] = s[2 * L + j]; x2[j] = s[3 * L + j]; y2[j] = s[4 * L + j]; }
-  madd<Fp>(X, Y, Z, x2, y2);
+  if (Z1) madd_z1<Fp>(X, Y, Z, x2, y2);       // Z must be Montgomery 1
+  else madd<Fp>(X, Y, Z, x2, y2);
   uint32_t* o = out + (size_t)i * 3 * L;
   for (int j = 0; j < L; ++j) { o[j] = X[j]; o[L + j] = Y[j]; o[2 * L + j] = Z[j]; }
 }
@@ -128,7 +129,8 @@ int run_ec(int what, const void* in, size_t in_bytes, uint32_t* out, size_t out_
   void *din, *dout;
   if (hipMalloc(&din, in_bytes) || hipMalloc(&dout, out_bytes)) return -1;
   (void)hipMemcpy(din, in, in_bytes, hipMemcpyHostToDevice);
-  if (what == 0) hipLaunchKernelGGL(k_tk_madd<CV>, dim3((n + 63) / 64), dim3(64), 0, 0, (const uint32_t*)din, (uint32_t*)dout, n);
+  if (what == 0) hipLaunchKernelGGL((k_tk_madd<CV, false>), dim3((n + 63) / 64), dim3(64), 0, 0, (const uint32_t*)din, (uint32_t*)dout, n);
+  else if (what == 2) hipLaunchKernelGGL((k_tk_madd<CV, true>), dim3((n + 63) / 64), dim3(64), 0, 0, (const uint32_t*)din, (uint32_t*)dout, n);
   else hipLaunchKernelGGL(k_tk_entry<CV>, dim3((n + 63) / 64), dim3(64), 0, 0, (const int*)din, (uint32_t*)dout, n);
   const hipError_t e = hipDeviceSynchronize();
   (void)hipMemcpy(out, dout, out_bytes, hipMemcpyDeviceToHost);
@@ -138,7 +140,7 @@ int run_ec(int what, const void* in, size_t in_bytes, uint32_t* out, size_t out_
 
 }  // namespace
 
-// what: 0 madd (in: n x 5L words), 1 generator table entry (in: n x (w, d) ints)
+// what: 0 madd (in: n x 5L words), 2 madd with Z1 = 1, 1 generator table entry (in: n x (w, d) ints)
 extern "C" int tk_ec(int curve, int what, const void* in, size_t in_bytes, uint32_t* out, size_t out_bytes, int n) {
   switch (curve) {
     case 1: return run_ec<CurveP256>(what, in, in_bytes, out, out_bytes, n);

@@ -179,6 +179,36 @@ def ec_mul(c, k, P):
 
 
 @pytest.mark.parametrize("cid", [1, 2, 3])
+def test_madd_z1_matches_affine_add(tk, cid):
+    """madd_z1: the accumulator holds one affine table entry (Z = Montgomery 1)."""
+    c = CURVES[cid]
+    p, L = c["p"], c["L"]
+    R = 1 << (W * L)
+    G = (c["gx"], c["gy"])
+    rng = random.Random(100 + cid)
+    ins, want, N = [], [], 128
+    for i in range(N):
+        P1 = ec_mul(c, rng.randrange(1, c["n"]), G)
+        P2 = ec_mul(c, rng.randrange(1, c["n"]), G)
+        vals = [P1[0] * R % p, P1[1] * R % p, R % p, P2[0] * R % p, P2[1] * R % p]
+        if i % 2:
+            vals[1] = vals[1] + p if vals[1] + p < R else vals[1]
+        ins += [l for v in vals for l in to_limbs(v, L)]
+        want.append(ec_add(c, P1, P2))
+    A = (ctypes.c_uint32 * len(ins))(*ins)
+    O = (ctypes.c_uint32 * (N * 3 * L))()
+    assert tk.tk_ec(cid, 2, A, ctypes.sizeof(A), O, ctypes.sizeof(O), N) == 0
+    Ri = pow(R, -1, p)
+    for i, w in enumerate(want):
+        ls = [O[(3 * i + k) * L:(3 * i + k + 1) * L] for k in range(3)]
+        assert all(max(l) <= MASK for l in ls)
+        assert from_limbs(ls[0]) < 2 * p and from_limbs(ls[1]) < 2 * p
+        X, Y, Z = (from_limbs(l) * Ri % p for l in ls)
+        zi = pow(Z, -1, p)
+        assert (X * zi * zi % p, Y * zi * zi * zi % p) == w
+
+
+@pytest.mark.parametrize("cid", [1, 2, 3])
 def test_madd_matches_affine_add(tk, cid):
     c = CURVES[cid]
     p, L = c["p"], c["L"]
