@@ -306,20 +306,41 @@ __device__ __forceinline__ uint32_t dbyte(const uint32_t* dig, int64_t np, int64
   return (dig[(int64_t)(i >> 2) * np + p] >> (24 - 8 * (i & 3))) & 0xffu;
 }
 
-// hash `len` bytes at buf (4-byte aligned) -> big-endian words
-__device__ void hash_buf(int hb, const uint8_t* buf, uint32_t len, uint32_t* out16) {
-  sha2::MemString m;
-  m.aligned = reinterpret_cast<const uint32_t*>(buf);
-  m.shift = 0;
-  m.len = len;
+// big-endian word of I2OSP(y, k) bytes [m, m+4): the little-endian word of
+// the integer at byte offset k-4-m (integer bytes below 0 are past EM's end)
+__device__ __forceinline__ uint32_t bword(const uint32_t* yw, int64_t np, int64_t p, int k, int m) {
+  const int jlo = k - 4 - m;
+  const int q = jlo >> 2;                    // floor (arithmetic shift)
+  const int nrows = (k + 3) >> 2;
+  const uint32_t lo = (q >= 0 && q < nrows) ? yw[(int64_t)q * np + p] : 0u;
+  const uint32_t hi = (q + 1 >= 0 && q + 1 < nrows) ? yw[(int64_t)(q + 1) * np + p] : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(jlo & 3));
+}
+
+// one MGF1 block: Hash(H || BE32(c)), H = hw big-endian words (one SHA block)
+__device__ __forceinline__ void mgf1_block(int hb, const uint32_t* Hw, int hw, uint32_t c, uint32_t* out16) {
+  const uint32_t len = 4u * (uint32_t)hw + 4u;
   if (hb == 256) {
-    uint32_t h[8];
-    sha2::sha256_mem(h, m);
-    for (int k = 0; k < 8; ++k) out16[k] = h[k];
+    uint32_t w[16], h[8];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = t < hw ? Hw[t] : t == hw ? c : t == hw + 1 ? 0x80000000u : 0u;
+    w[15] = len << 3;
+    sha2::sha256_init(h);
+    sha2::sha256_compress(h, w);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) { out16[t] = h[t]; out16[8 + t] = 0u; }
   } else {
-    uint64_t h[8];
-    sha2::sha512_mem(h, hb == 384, m, nullptr, 0);
-    for (int k = 0; k < 8; ++k) { out16[2 * k] = (uint32_t)(h[k] >> 32); out16[2 * k + 1] = (uint32_t)h[k]; }
+    uint32_t v[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) v[t] = t < hw ? Hw[t] : t == hw ? c : t == hw + 1 ? 0x80000000u : 0u;
+    v[31] = len << 3;
+    uint64_t w[16], h[8];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = ((uint64_t)v[2 * t] << 32) | v[2 * t + 1];
+    sha2::sha512_init(h, hb == 384);
+    sha2::sha512_compress(h, w);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) { out16[2 * t] = (uint32_t)(h[t] >> 32); out16[2 * t + 1] = (uint32_t)h[t]; }
   }
 }
 
@@ -381,44 +402,83 @@ __global__ void __launch_bounds__(64) k_rsa_pad(RsaArgs a) {
       const uint32_t bitmask = 0xffu >> (8 * emlen - embits);
       ok = ok && (ybyte(a.yw, np, p, k, lead) & ~bitmask) == 0;
       if (ok) {
-        // [0,512): DB ; [512,2048): work (H||ctr, then M' = 0^8||mHash||salt <= 584 B,
-        // plus the SHA reader's over-read of one block)
-        uint8_t* buf = a.pss_scratch + (p - a.begin) * 2048;
-        uint8_t* wk = buf + 512;
+        // Word-level EMSA-PSS-VERIFY: EM words come straight from the y rows
+        // (bword), DB = maskedDB ^ MGF1(H) is kept as big-endian words in this
+        // token's 2 KiB scratch, M' = 0^8 || mHash || salt is fed to SHA-2
+        // word by word from the digest rows and the DB words.
+        uint32_t* dbw = reinterpret_cast<uint32_t*>(a.pss_scratch + (p - a.begin) * 2048);
         const int dblen = emlen - hlen - 1;
-        // H = EM[dblen .. dblen+hlen)
-        for (int i = 0; i < hlen; ++i) wk[i] = (uint8_t)ybyte(a.yw, np, p, k, lead + dblen + i);
-        // DB = maskedDB ^ MGF1(H, dblen)
-        uint32_t mask[16];
+        const int hw = hlen / 4;
+        uint32_t Hw[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) Hw[t] = t < hw ? bword(a.yw, np, p, k, lead + dblen + 4 * t) : 0u;
         for (int c = 0; c * hlen < dblen; ++c) {
-          wk[hlen] = (uint8_t)(c >> 24); wk[hlen + 1] = (uint8_t)(c >> 16);
-          wk[hlen + 2] = (uint8_t)(c >> 8); wk[hlen + 3] = (uint8_t)c;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          hash_buf(hb, wk, (uint32_t)hlen + 4, mask);
-          for (int i = 0; i < hlen && c * hlen + i < dblen; ++i) {
-            const int di = c * hlen + i;
-            const uint32_t mb = (mask[i >> 2] >> (24 - 8 * (i & 3))) & 0xffu;
-            buf[di] = (uint8_t)(ybyte(a.yw, np, p, k, lead + di) ^ mb);
+          uint32_t mask[16];
+          mgf1_block(hb, Hw, hw, (uint32_t)c, mask);
+#pragma unroll
+          for (int t = 0; t < 16; ++t) {
+            const int di = c * hlen + 4 * t;
+            if (t < hw && di < dblen) dbw[di >> 2] = bword(a.yw, np, p, k, lead + di) ^ mask[t];
           }
         }
-        buf[0] &= (uint8_t)bitmask;
-        int ps = 0;
-        while (ps < dblen && buf[ps] == 0) ++ps;
-        ok = ps < dblen && buf[ps] == 0x01;
+        // DB[0] &= bitmask; PS = leading zero bytes, then 0x01
+        const int nw = (dblen + 3) / 4;
+        int ps = -1;
+        for (int q = 0; q < nw && ps < 0; ++q) {
+          uint32_t w = dbw[q];
+          if (q == 0) w &= (bitmask << 24) | 0x00ffffffu;
+          const int live = dblen - 4 * q;                    // bytes of DB in this word
+          if (live < 4) w &= 0xffffffffu << (32 - 8 * live);
+          if (w != 0) {
+            const int b = __builtin_clz(w) >> 3;
+            ps = 4 * q + b;
+            ok = ((w >> (24 - 8 * b)) & 0xffu) == 0x01u;
+          }
+        }
+        ok = ok && ps >= 0;
         if (ok) {
           const int slen = dblen - ps - 1;
-          // M' = 0^8 || mHash || salt   (into the work area, H copied out first)
-          uint32_t Hw[16];
-          for (int i = 0; i < 16; ++i) Hw[i] = 0;
-          for (int i = 0; i < hlen; ++i) Hw[i >> 2] |= (uint32_t)wk[i] << (24 - 8 * (i & 3));
-          for (int i = 0; i < 8; ++i) wk[i] = 0;
-          for (int i = 0; i < hlen; ++i) wk[8 + i] = (uint8_t)dbyte(a.dig, np, p, i);
-          for (int i = 0; i < slen; ++i) wk[8 + hlen + i] = buf[ps + 1 + i];
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          const uint32_t mlen = (uint32_t)(8 + hlen + slen);
+          auto mword = [&](uint32_t w) -> uint32_t {          // big-endian word w of M', padded
+            const int o = 4 * (int)w;
+            uint32_t raw;
+            if (o < 8) raw = 0u;
+            else if (o < 8 + hlen) raw = a.dig[(int64_t)((o - 8) >> 2) * np + p];
+            else {
+              const int st = ps + 1 + (o - 8 - hlen);         // DB byte index of the salt bytes
+              const int q = st >> 2, r = st & 3;
+              raw = r == 0 ? dbw[q] : (dbw[q] << (8 * r)) | (dbw[q + 1] >> (32 - 8 * r));
+            }
+            return sha2::pad_word(raw, w, mlen);
+          };
           uint32_t h2[16];
-          hash_buf(hb, wk, (uint32_t)(8 + hlen + slen), h2);
+          if (hb == 256) {
+            uint32_t h[8];
+            sha2::sha256_init(h);
+            const uint32_t nblk = (mlen + 9 + 63) / 64;
+            for (uint32_t blk = 0; blk < nblk; ++blk) {
+              uint32_t w[16];
+              for (int t = 0; t < 16; ++t) w[t] = mword(16 * blk + t);
+              if (blk == nblk - 1) { w[14] = mlen >> 29; w[15] = mlen << 3; }
+              sha2::sha256_compress(h, w);
+            }
+            for (int t = 0; t < 8; ++t) h2[t] = h[t];
+          } else {
+            uint64_t h[8];
+            sha2::sha512_init(h, hb == 384);
+            const uint32_t nblk = (mlen + 17 + 127) / 128;
+            for (uint32_t blk = 0; blk < nblk; ++blk) {
+              uint32_t v[32];
+              for (int t = 0; t < 32; ++t) v[t] = mword(32 * blk + t);
+              if (blk == nblk - 1) { v[30] = mlen >> 29; v[31] = mlen << 3; }
+              uint64_t w[16];
+              for (int t = 0; t < 16; ++t) w[t] = ((uint64_t)v[2 * t] << 32) | v[2 * t + 1];
+              sha2::sha512_compress(h, w);
+            }
+            for (int t = 0; t < 8; ++t) { h2[2 * t] = (uint32_t)(h[t] >> 32); h2[2 * t + 1] = (uint32_t)h[t]; }
+          }
           uint32_t diff = 0;
-          for (int i = 0; i < hlen / 4; ++i) diff |= h2[i] ^ Hw[i];
+          for (int t = 0; t < hw; ++t) diff |= h2[t] ^ Hw[t];
           ok = diff == 0;
         }
       }
