@@ -46,9 +46,6 @@ struct DevKey {
   int32_t pad_;
 };
 
-// Comb tables: 8-bit signed windows, entries 1..128 per window.
-constexpr int COMB_W = 8;
-
 // Timing hook: the runtime records a HIP event on the batch's stream after
 // each kernel a launcher enqueues (names: "<class>_<kernel>").
 struct Marker {

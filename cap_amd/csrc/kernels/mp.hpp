@@ -425,13 +425,6 @@ MPD void pow_e(uint32_t* r, const uint32_t* x, const uint32_t* E, int ebits, boo
   copy<F>(r, acc);
 }
 
-// Fermat inverse r = x^(m-2), Montgomery form in and out (m prime).  Kept as
-// the cross-check for `inv` in the field self-tests (tk.hip op 3).
-template <class F>
-MPD void inv_fermat(uint32_t* r, const uint32_t* x) {
-  pow_e<F>(r, x, F::M, F::BITS, true);
-}
-
 // ---- constant-time modular inversion by Bernstein-Yang "safegcd" ----------
 // (half-delta divsteps, the variant of Bernstein & Yang 2019 as refined by
 // Wuille).  Numbers are in signed radix 2^28: limbs 0..L-2 in [0, 2^28), the
