@@ -386,11 +386,11 @@ MPD void from_mont(uint32_t* r, const uint32_t* a) {
 }
 
 // r = x^E for an exponent held in a constexpr array of 28-bit limbs (read with
-// wave-uniform indices -> scalar loads).  `minus2` subtracts 2 from limb 0
-// (E = m - 2 for Fermat inversion; every modulus here has limb 0 >= 2).
-// Left-to-right fixed window of WB bits (4 for 10-limb fields, 2 above, so the
-// 2^WB-entry table fits the register file); the window value is uniform across
-// the wave, so the table select is a uniform compare chain, not a divergent branch.
+// wave-uniform indices -> scalar loads); used for the Ed25519 square root at
+// key staging.  `minus2` subtracts 2 from limb 0 (E = m - 2, a Fermat
+// exponent).  Left-to-right fixed window of WB bits (3 for 10-limb fields, 2
+// above, so the 2^WB-entry table fits the register file); the window value is
+// uniform across the wave, so the table select is a uniform compare chain.
 template <class F>
 MPD void pow_e(uint32_t* r, const uint32_t* x, const uint32_t* E, int ebits, bool minus2) {
   constexpr int L = F::L;
