@@ -116,3 +116,34 @@ def test_contexts_share_fixed_base_tables():
     arena2, slots2 = H.jobs_from_tokens(pick, kid_index)
     assert [b.verify(arena2)[s] for s in slots2] == want
     b.close()
+
+
+def test_timed_and_streamed_runs_agree(ctx):
+    """jg_batch_run (classes in sequence, per-kernel events) and
+    jg_batch_enqueue (every class on its own stream) give identical verdicts on
+    a batch mixing all seven kernel classes, run after run."""
+    from cap_amd import _lib
+    from oracle import jws
+    keys, toks = H.golden()
+    okeys = [jws.Key.from_fixture(k) for k in keys]
+    arena = _lib.Arena()
+    want = []
+    for t in toks:
+        p = jws.parse_jws(t["token"])
+        if p is None or not p.crit_ok:
+            continue
+        sig_b64 = jws.b64url_encode(p.signature).encode()
+        for ki, k in enumerate(okeys):
+            arena.add(p.signing_input, sig_b64, p.alg, ki)
+            want.append(int(jws.verify_sig(p, k)))
+    b = ctx.stage(arena)
+    timed = b.run(want_verdicts=True)
+    assert list(timed) == want
+    assert {n.split("_")[0] for n, _ in b.kernel_times()} >= {"rsa2048", "p256", "p384", "p521", "ed25519"}
+    pinned = _lib.PinnedBuffer(len(want))
+    for _ in range(3):
+        b.enqueue(pinned)
+    b.sync()
+    assert list(pinned.bytes()[:len(want)]) == want
+    pinned.free()
+    b.free()
