@@ -24,6 +24,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/jg.h"
@@ -124,6 +125,10 @@ struct Device {
   // to fill 256 CUs alone); joined back into `stream` before the scatter
   hipStream_t cstream[NCLS] = {};
   hipEvent_t ev_start = nullptr, ev_done[NCLS] = {};
+  // comb tables of the current key blob by key content (class, coordinates):
+  // a reload (JWKS refresh) copies the tables of keys it already had instead
+  // of rebuilding them (D2D copy ~0.2 ms vs ~80 ms per P-256 key)
+  std::unordered_map<std::string, std::pair<uint64_t, uint64_t>> tab_cache;   // id -> (word offset, words)
   DevKey* dkeys = nullptr;
   uint32_t* dblob = nullptr;
   int32_t* didx = nullptr;
@@ -450,6 +455,7 @@ struct StagedKeys {
   std::vector<uint32_t> blob;      // host-initialised part of the device key blob
   uint64_t tab_words = 0;          // device-only tail: comb tables (built on the GPU)
   std::vector<int32_t> rsa_idx, ec_idx[NCLS], ed_idx, tab_keys;
+  std::vector<std::string> tab_id;  // per key: content id of its comb table ("" = none)
 };
 
 // comb tables never exist on the host: offsets are relative to the device-only
@@ -470,6 +476,7 @@ uint64_t blob_alloc(std::vector<uint32_t>& blob, size_t words) {
 void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
   ctx->keys.assign((size_t)nkeys, HostKey{});
   S.dk.assign((size_t)nkeys, DevKey{});
+  S.tab_id.assign((size_t)nkeys, std::string());
   for (int i = 0; i < nkeys; ++i) {
     const jg_key& k = keys[i];
     HostKey& hk = ctx->keys[i];
@@ -521,6 +528,7 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       if (ok) {
         be_to_limbs(k.x, cl, S.blob.data() + K.aux_off, L);
         be_to_limbs(k.y, cl, S.blob.data() + K.aux_off + L, L);
+        S.tab_id[i] = std::string("E") + (char)cls + std::string((const char*)S.blob.data() + 4 * K.aux_off, 8 * L);
       }
       K.valid = ok;
       if (ok) S.ec_idx[cls].push_back(i);
@@ -533,7 +541,10 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       K.tab_off = tab_alloc(S, i, (uint64_t)ed_table_words(false));
       // crypto/ed25519.Verify panics on len(pub) != 32; go-jose never hands it one
       const bool ok = k.x && k.coord_len == 32;
-      if (ok) std::memcpy(S.blob.data() + K.aux_off, k.x, 32);
+      if (ok) {
+        std::memcpy(S.blob.data() + K.aux_off, k.x, 32);
+        S.tab_id[i] = std::string("D") + std::string((const char*)k.x, 32);
+      }
       K.valid = ok;
       if (ok) S.ed_idx.push_back(i);
       hk.cls = CLS_ED25519;
@@ -590,31 +601,58 @@ void load_keys_device(Device* d, const StagedKeys& S) {
   hipStream_t s = d->stream;
   HIPCHK(hipStreamSynchronize(s));
   if (d->dkeys) (void)hipFree(d->dkeys);
-  if (d->dblob) (void)hipFree(d->dblob);
   if (d->didx) (void)hipFree(d->didx);
-  d->dkeys = nullptr; d->dblob = nullptr; d->didx = nullptr;
+  d->dkeys = nullptr; d->didx = nullptr;
+  uint32_t* old_blob = d->dblob;                   // kept until its reusable tables are copied
+  auto old_cache = std::move(d->tab_cache);
+  d->tab_cache.clear();
+  d->dblob = nullptr;
   const size_t nk = std::max<size_t>(S.dk.size(), 1);
   HIPCHK(hipMalloc(&d->dkeys, sizeof(DevKey) * nk));
   HIPCHK(hipMalloc(&d->dblob, sizeof(uint32_t) * std::max<uint64_t>(S.blob.size() + S.tab_words, 4)));
   if (!S.dk.empty()) HIPCHK(hipMemcpyAsync(d->dkeys, S.dk.data(), sizeof(DevKey) * S.dk.size(), hipMemcpyHostToDevice, s));
   if (!S.blob.empty())
     HIPCHK(hipMemcpyAsync(d->dblob, S.blob.data(), sizeof(uint32_t) * S.blob.size(), hipMemcpyHostToDevice, s));
-  // one index array: rsa | p256 | p384 | p521 | ed
+  // per table class: keys to stage (all) and keys whose tables must be built
+  // (the rest are copied from the previous blob, same key content)
+  auto split = [&](const std::vector<int32_t>& keys, uint64_t words, std::vector<int32_t>& build) {
+    for (int32_t i : keys) {
+      const std::string& id = S.tab_id[(size_t)i];
+      const uint64_t off = S.dk[(size_t)i].tab_off;
+      auto it = id.empty() ? old_cache.end() : old_cache.find(id);
+      if (old_blob && it != old_cache.end() && it->second.second == words) {
+        HIPCHK(hipMemcpyAsync(d->dblob + off, old_blob + it->second.first, sizeof(uint32_t) * words,
+                              hipMemcpyDeviceToDevice, s));
+      } else {
+        build.push_back(i);
+      }
+      if (!id.empty()) d->tab_cache[id] = {off, words};
+    }
+  };
+  std::vector<int32_t> build_ec[NCLS], build_ed;
+  for (int c = CLS_P256; c <= CLS_P521; ++c) split(S.ec_idx[c], (uint64_t)ec_table_words(c, false), build_ec[c]);
+  split(S.ed_idx, (uint64_t)ed_table_words(false), build_ed);
+  // one index array: rsa | p256 | p384 | p521 | ed | builds p256 | p384 | p521 | ed
   std::vector<int32_t> idx;
   std::vector<size_t> at;
   auto push = [&](const std::vector<int32_t>& v) { at.push_back(idx.size()); idx.insert(idx.end(), v.begin(), v.end()); };
   push(S.rsa_idx);
   for (int c = CLS_P256; c <= CLS_P521; ++c) push(S.ec_idx[c]);
   push(S.ed_idx);
+  for (int c = CLS_P256; c <= CLS_P521; ++c) push(build_ec[c]);
+  push(build_ed);
   HIPCHK(hipMalloc(&d->didx, sizeof(int32_t) * std::max<size_t>(idx.size(), 1)));
   if (!idx.empty()) HIPCHK(hipMemcpyAsync(d->didx, idx.data(), sizeof(int32_t) * idx.size(), hipMemcpyHostToDevice, s));
   ensure_tables(d, S);
   if (!S.dk.empty()) launch_rsa_keyprep(d->dkeys, d->dblob, (int)S.dk.size(), s);
   for (int c = CLS_P256; c <= CLS_P521; ++c)
-    launch_ec_keyprep(c, d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(), s);
-  launch_ed_keyprep(d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), s);
+    launch_ec_keyprep(c, d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(),
+                      d->didx + at[5 + c - CLS_P256], (int)build_ec[c].size(), s);
+  launch_ed_keyprep(d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), d->didx + at[8],
+                    (int)build_ed.size(), s);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
+  if (old_blob) (void)hipFree(old_blob);
 }
 
 thread_local std::string g_tls_err;

@@ -628,12 +628,14 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
 }
 
 template <class CV>
-void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
+void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx, int tn,
+                   hipStream_t s) {
   constexpr int NWIN = ec_windows(CV::CLS, false), NE = ec_entries(CV::CLS, false);
   dim3 b(64);
-  hipLaunchKernelGGL(k_ec_keyprep<CV>, dim3((n + 63) / 64), b, 0, s, keys, blob, idx, n);
-  hipLaunchKernelGGL(k_ec_table_base_keys<CV>, dim3((NWIN + 63) / 64, n), b, 0, s, keys, blob, idx, n);
-  hipLaunchKernelGGL(k_ec_table_keys<CV>, dim3((NWIN * NE + 63) / 64, n), b, 0, s, keys, blob, idx, n);
+  if (n > 0) hipLaunchKernelGGL(k_ec_keyprep<CV>, dim3((n + 63) / 64), b, 0, s, keys, blob, idx, n);
+  if (tn <= 0) return;
+  hipLaunchKernelGGL(k_ec_table_base_keys<CV>, dim3((NWIN + 63) / 64, tn), b, 0, s, keys, blob, tidx, tn);
+  hipLaunchKernelGGL(k_ec_table_keys<CV>, dim3((NWIN * NE + 63) / 64, tn), b, 0, s, keys, blob, tidx, tn);
 }
 
 template <class CV>
@@ -655,12 +657,13 @@ void launch_ec(int cls, const EcArgs& a, hipStream_t s, const Marker& mk) {
   }
 }
 
-void launch_ec_keyprep(int cls, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
+void launch_ec_keyprep(int cls, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx,
+                       int tn, hipStream_t s) {
   if (n <= 0) return;
   switch (cls) {
-    case CLS_P256: keyprep_chain<CurveP256>(keys, blob, idx, n, s); break;
-    case CLS_P384: keyprep_chain<CurveP384>(keys, blob, idx, n, s); break;
-    case CLS_P521: keyprep_chain<CurveP521>(keys, blob, idx, n, s); break;
+    case CLS_P256: keyprep_chain<CurveP256>(keys, blob, idx, n, tidx, tn, s); break;
+    case CLS_P384: keyprep_chain<CurveP384>(keys, blob, idx, n, tidx, tn, s); break;
+    case CLS_P521: keyprep_chain<CurveP521>(keys, blob, idx, n, tidx, tn, s); break;
     default: break;
   }
 }

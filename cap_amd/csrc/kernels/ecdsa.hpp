@@ -61,6 +61,9 @@ constexpr int64_t ec_table_words(int cls, bool gen) {
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);
 // key staging: validate each listed key (plain 28-bit limbs x,y at aux_off), write
 // Montgomery affine coordinates back to aux_off and build its comb table.
-void launch_ec_keyprep(int cls, jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);
+// tidx[0..tn): the subset of idx whose tables are (re)built; the others' tables
+// are copied from a previous load by the runtime.
+void launch_ec_keyprep(int cls, jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx,
+                       int tn, hipStream_t s);
 // generator table for a curve into `tab` (ec_table_words(cls) words)
 void launch_ec_gtable(int cls, uint32_t* tab, hipStream_t s);

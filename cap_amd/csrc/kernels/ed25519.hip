@@ -394,12 +394,14 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   mk("finish");
 }
 
-void launch_ed_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
+void launch_ed_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx, int tn,
+                       hipStream_t s) {
   if (n <= 0) return;
   constexpr int NWIN = ed_windows(false), NE = ed_entries(false);
   hipLaunchKernelGGL(k_ed_decode, dim3((n + 63) / 64), dim3(64), 0, s, keys, blob, idx, n);
-  hipLaunchKernelGGL(k_ed_table_base_keys, dim3((NWIN + 63) / 64, n), dim3(64), 0, s, keys, blob, idx, n);
-  hipLaunchKernelGGL(k_ed_table_keys, dim3((NWIN * NE + 63) / 64, n), dim3(64), 0, s, keys, blob, idx, n);
+  if (tn <= 0) return;
+  hipLaunchKernelGGL(k_ed_table_base_keys, dim3((NWIN + 63) / 64, tn), dim3(64), 0, s, keys, blob, tidx, tn);
+  hipLaunchKernelGGL(k_ed_table_keys, dim3((NWIN * NE + 63) / 64, tn), dim3(64), 0, s, keys, blob, tidx, tn);
 }
 
 void launch_ed_btable(uint32_t* tab, hipStream_t s) {

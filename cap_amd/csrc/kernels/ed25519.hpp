@@ -37,5 +37,6 @@ constexpr int ED_MAX_KEYS = 256;
 void launch_ed(const EdArgs& a, hipStream_t s, const jgk::Marker& mk);
 // key staging: decode each listed key's 32 public-key bytes (words at aux_off),
 // mark validity and build the comb table of -A at tab_off
-void launch_ed_keyprep(jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);
+void launch_ed_keyprep(jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx, int tn,
+                       hipStream_t s);
 void launch_ed_btable(uint32_t* tab, hipStream_t s);

@@ -147,3 +147,30 @@ def test_timed_and_streamed_runs_agree(ctx):
     assert list(pinned.bytes()[:len(want)]) == want
     pinned.free()
     b.free()
+
+
+def test_key_reload_reuses_tables():
+    """jg_keys_load keeps the comb tables of keys it already had (copied by
+    content into the new key blob) and builds only new ones: reloading the
+    golden key set in reverse order, then a subset, verifies every golden token
+    exactly as a fresh load does."""
+    import time
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    c = _lib.Context()
+    t0 = time.perf_counter()
+    c.load_keys([H.abi_key(k) for k in keys])
+    first = time.perf_counter() - t0
+    for order in (keys[::-1], keys[::2], keys):
+        t0 = time.perf_counter()
+        c.load_keys([H.abi_key(k) for k in order])
+        again = time.perf_counter() - t0
+        kid_index = {k["kid"]: i for i, k in enumerate(order)}
+        sel = [t for t in toks if t["key"] in kid_index]
+        arena, slots = H.jobs_from_tokens(sel, kid_index)
+        out = c.verify(arena)
+        bad = [(t["name"], out[s] if s is not None else 0, t["verdict"]) for t, s in zip(sel, slots)
+               if (0 if s is None else out[s]) != t["verdict"]]
+        assert not bad, bad
+    assert again < first            # the last reload rebuilds nothing
+    c.close()
