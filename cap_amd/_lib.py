@@ -9,7 +9,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcapjwt.so")
+LIB_PATH = os.environ.get("CAPJWT_LIB") or os.path.join(HERE, "libcapjwt.so")
 
 # jwt/algs.go:12-21
 ALG_IDS = {"RS256": 1, "RS384": 2, "RS512": 3, "PS256": 4, "PS384": 5, "PS512": 6,

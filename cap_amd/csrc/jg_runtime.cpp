@@ -491,7 +491,7 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       // crypto/rsa (Go >= 1.24) public-key checks: odd N of >= 1024 bits
       // (rsa1024min), odd E with 2 <= E <= 2^31-1   [SURVEY R12]
       bool ok = nl > 0 && bits >= 1024 && (n[nl - 1] & 1) && k.e >= 2 && k.e <= 0x7fffffffULL && (k.e & 1);
-      int cls = bits <= 74 * 28 - 2 ? CLS_RSA2K : bits <= 112 * 28 - 2 ? CLS_RSA3K : bits <= 148 * 28 - 2 ? CLS_RSA4K : -1;
+      int cls = bits <= rsa_limbs(CLS_RSA2K) * 28 - 2 ? CLS_RSA2K : bits <= 112 * 28 - 2 ? CLS_RSA3K : bits <= 148 * 28 - 2 ? CLS_RSA4K : -1;
       if (cls < 0) {
         ok = false;
         ctx->set_err("RSA key " + std::to_string(i) + " has " + std::to_string(bits) +

@@ -24,11 +24,15 @@
 #define JG_MAD_SET(PAIR, LO, HI, SRC_B) \
   asm("v_mad_u64_u32 %0, " PAIR ", %1, %2, 0" : "=v"(acc) : "v"(a), SRC_B(b) : LO, HI)
 #define JG_MAD_ASM(ONE, SRC_B)                                  \
-  switch (slot & 3) {                                           \
+  switch (slot & 7) {                                           \
     case 0: ONE("s[88:89]", "s88", "s89", SRC_B); break;        \
     case 1: ONE("s[90:91]", "s90", "s91", SRC_B); break;        \
     case 2: ONE("s[92:93]", "s92", "s93", SRC_B); break;        \
-    default: ONE("s[94:95]", "s94", "s95", SRC_B); break;       \
+    case 3: ONE("s[94:95]", "s94", "s95", SRC_B); break;        \
+    case 4: ONE("s[80:81]", "s80", "s81", SRC_B); break;        \
+    case 5: ONE("s[82:83]", "s82", "s83", SRC_B); break;        \
+    case 6: ONE("s[84:85]", "s84", "s85", SRC_B); break;        \
+    default: ONE("s[86:87]", "s86", "s87", SRC_B); break;       \
   }
 #define JG_V(x) "v"(x)
 #define JG_S(x) "s"(x)

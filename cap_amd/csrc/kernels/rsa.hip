@@ -24,6 +24,10 @@ using namespace jgk;
 
 #define W28 28
 #define M28 0x0fffffffu
+#ifndef SQR_SLOTS
+#define SQR_SLOTS 4
+#endif
+#define SQR_SLOT(k) ((k) % SQR_SLOTS)
 
 namespace {
 
@@ -70,6 +74,33 @@ __device__ __forceinline__ void cios_step(uint64_t* T, uint32_t ai, const uint32
   T[H] = lastl ? 0ull : (((uint64_t)hi << 32) | lo);
 }
 
+// v <- the lane's accumulator window P[0..H), normalised within the lane, then
+// the carries rippled up the group: each round moves every pending carry one
+// lane up (the top lane's carry-out is zero because the value is
+// < 2n < 2^(28L)).
+template <int H, int G>
+__device__ __forceinline__ void finish_product(uint32_t* v, const uint64_t* P, bool lane0) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const uint64_t t = P[j] + c;
+    v[j] = (uint32_t)t & M28;
+    c = t >> W28;
+  }
+#pragma unroll
+  for (int r = 0; r < G - 1; ++r) {
+    const uint32_t clo = from_prev<G>((uint32_t)c), chi = from_prev<G>((uint32_t)(c >> 32));
+    uint64_t cin = lane0 ? 0ull : (((uint64_t)chi << 32) | clo);
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const uint64_t t = (uint64_t)v[j] + cin;
+      v[j] = (uint32_t)t & M28;
+      cin = t >> W28;
+    }
+    c = cin;
+  }
+}
+
 // v <- (a * v) / R mod n with a streamed from LDS (la[i * TPW], shared by the
 // group's lanes: a broadcast read).  R = 2^(28 H G).  In: v < 2n limb-normalized.
 // Out: v < 2n, limbs < 2^28 (carries rippled across the group).
@@ -100,28 +131,63 @@ __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const 
   }
 #pragma unroll
   for (int u = 0; u < REM; ++u) cios_step<H, G>(P + u, la[(NB * U + u) * TPW], v, n, np, lane0, lastl);
-  // normalise within the lane, then ripple the carries up the group: each
-  // round moves every pending carry one lane up (the top lane's carry-out is
-  // zero because the value is < 2n < 2^(28L)).
-  uint64_t c = 0;
+  finish_product<H, G>(v, P + REM, lane0);
+}
+
+// v <- v^2 / R mod n: the squaring form of mont_mul (16 of the 18 products of
+// e = 65537).  Same lazy CIOS rows and the same limb shift, but the multiply
+// half adds every product v_i v_j once (doubled when i != j).  Lane g's
+// register k is limb gH + k, so row i = rH + x multiplies a_i into registers
+// k >= x only, covering the limb pairs {rH + x, gH + k}:
+//   k > x   both rows (r,x) and (g,k) could hold the pair; only (r,x) does (x 2)
+//   k == x  lane g < r: nothing (row (g,x) had it), g == r: the square v_i^2
+//           once, g > r: the cross product (x 2)
+// Any row may add a product v_i v_j as long as it runs before column i + j is
+// reduced, and rows i and j both do.  Multiply MADs: G*H(H+1)/2 per lane
+// instead of G*H^2 (RSA-2048: 1406 + 2738 = 4144 per lane and product instead
+// of 5476).  The column bound is unchanged: the doubled products sum to the
+// same column totals as the full product.  The x loop is unrolled (the
+// triangle needs compile-time register indices), the r loop is not: one
+// physical shift of the window per H rows.
+template <int H, int G, int TPW>
+__device__ __forceinline__ void mont_sqr(uint32_t* v, const uint32_t* la, const uint32_t* n, uint32_t np, int g,
+                                         bool lane0, bool lastl) {
+  constexpr int L = H * G;
+  uint64_t P[2 * H];
 #pragma unroll
-  for (int j = 0; j < H; ++j) {
-    const uint64_t t = P[REM + j] + c;
-    v[j] = (uint32_t)t & M28;
-    c = t >> W28;
-  }
+  for (int j = 0; j < H; ++j) P[j] = 0;
+#pragma unroll 1
+  for (int r = 0; r < G; ++r) {
+    const uint32_t sh = g > r ? 1u : 0u;
+    const uint32_t msk = g >= r ? ~0u : 0u;
+    const uint32_t* lr = la + r * H * TPW;
 #pragma unroll
-  for (int r = 0; r < G - 1; ++r) {
-    const uint32_t clo = from_prev<G>((uint32_t)c), chi = from_prev<G>((uint32_t)(c >> 32));
-    uint64_t cin = lane0 ? 0ull : (((uint64_t)chi << 32) | clo);
+    for (int x = 0; x < H; ++x) {
+      const uint32_t ai = lr[x * TPW];
+      uint64_t* T = P + x;
+      mad64(T[x], (ai << sh) & msk, v[x], SQR_SLOT(x));
+      const uint32_t a2 = ai << 1;
 #pragma unroll
-    for (int j = 0; j < H; ++j) {
-      const uint64_t t = (uint64_t)v[j] + cin;
-      v[j] = (uint32_t)t & M28;
-      cin = t >> W28;
+      for (int k = x + 1; k < H; ++k) mad64(T[k], a2, v[k], SQR_SLOT(k));
+      const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
+#pragma unroll
+      for (int k = 0; k < H; ++k) mad64(T[k], m, n[k], SQR_SLOT(k + 2));
+      const uint64_t c = lane0 ? (T[0] >> W28) : 0ull;
+      T[1] += c;
+      const uint32_t lo = from_next<G>((uint32_t)T[0]);
+      const uint32_t hi = from_next<G>((uint32_t)(T[0] >> 32));
+      T[H] = lastl ? 0ull : (((uint64_t)hi << 32) | lo);
     }
-    c = cin;
+    if constexpr (2 * L > 250) {
+      if (r == G / 2 - 1) {   // keep every 64-bit column < 2^64: normalise half-way
+#pragma unroll
+        for (int j = H; j < 2 * H - 1; ++j) { P[j + 1] += P[j] >> W28; P[j] &= M28; }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < H; ++j) P[j] = P[j + H];
   }
+  finish_product<H, G>(v, P, lane0);
 }
 
 template <int H, int TPW>
@@ -237,7 +303,8 @@ __global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
 #pragma unroll
       for (int j = 0; j < H; ++j) v[j] = (j == 0 && lane0) ? 1u : 0u;
     }
-    mont_mul<H, G, U, TPW>(v, la, n, np28, lane0, lastl);
+    if (op == SQUARE) mont_sqr<H, G, TPW>(v, la, n, np28, g, lane0, lastl);
+    else mont_mul<H, G, U, TPW>(v, la, n, np28, lane0, lastl);
     if (op == TOMONT) {
       if (mid) store_limb_rows<H>(a.xmw, np, loff, v);
       op = SQUARE;
@@ -536,7 +603,7 @@ void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const Marker& mk) {
   if (waves <= 0) return;
   dim3 g((unsigned)waves), b(WAVE);
   switch (cls) {
-    case CLS_RSA2K: hipLaunchKernelGGL((k_rsa_modexp<37, 2, 8>), dim3((unsigned)(waves * 2)), b, 0, s, a); break;
+    case CLS_RSA2K: hipLaunchKernelGGL((k_rsa_modexp<RSA2K_H, RSA2K_G, 8>), dim3((unsigned)(waves * RSA2K_G)), b, 0, s, a); break;
     case CLS_RSA3K: hipLaunchKernelGGL((k_rsa_modexp<28, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a); break;
     case CLS_RSA4K: hipLaunchKernelGGL((k_rsa_modexp<37, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a); break;
     default: return;

@@ -25,12 +25,20 @@ struct RsaArgs {
   int64_t npad, begin, end;
 };
 
-// rows of the signature scratch each RSA class reads
-constexpr int rsa_sig_rows(int cls) {
-  return cls == jgk::CLS_RSA2K ? 66 : cls == jgk::CLS_RSA3K ? 99 : 128;
-}
+// RSA-2048 layout: JG_RSA2K_G lanes per token, H limbs per lane
+#ifndef JG_RSA2K_G
+#define JG_RSA2K_G 2
+#endif
+constexpr int RSA2K_G = JG_RSA2K_G;
+constexpr int RSA2K_H = RSA2K_G == 2 ? 37 : 19;
 constexpr int rsa_limbs(int cls) {
-  return cls == jgk::CLS_RSA2K ? 74 : cls == jgk::CLS_RSA3K ? 112 : 148;
+  return cls == jgk::CLS_RSA2K ? RSA2K_G * RSA2K_H : cls == jgk::CLS_RSA3K ? 112 : 148;
+}
+// rows of the signature scratch each RSA class reads: the modexp's limb loads
+// touch words up to (28 L - 1) / 32 + 1 (load_limbs_from_words), so those
+// rows must be zeroed by prep
+constexpr int rsa_sig_rows(int cls) {
+  return cls == jgk::CLS_RSA4K ? 128 : (28 * rsa_limbs(cls) - 1) / 32 + 2;
 }
 
 void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const jgk::Marker& mk);
