@@ -67,11 +67,16 @@ def p256_point_mads_per_token():
     return (adds - 1) * madd + madd_z1 + sqr + 2 * mul
 
 
-def rsa_modexp_mads_per_token(limbs):
-    """k_rsa_modexp: 18 Montgomery products (to-Montgomery, 16 squarings, final
-    multiply) of 2 * L^2 multiply-accumulates each (L 28-bit limbs: 74 for
-    RSA-2048, 148 for RSA-4096)."""
-    return 18 * 2 * limbs * limbs
+def rsa_modexp_mads_per_token(limbs, lanes):
+    """k_rsa_modexp (e = 65537): 18 Montgomery products on L 28-bit limbs held
+    by `lanes` lanes per token (H = L / lanes each; RSA-2048: L = 74 on 2 lanes,
+    RSA-4096: 148 on 4).  To-Montgomery and the final multiply (mont_mul) are
+    2 L^2 multiply-accumulates each; the 16 squarings (mont_sqr) issue each limb
+    product once -- lanes^2 * H(H+1)/2 for the square (L(L+1)/2 plus the
+    diagonal blocks' duplicated diagonal) + L^2 for the reduction."""
+    h = limbs // lanes
+    sqr = lanes * lanes * h * (h + 1) // 2 + limbs * limbs
+    return 2 * 2 * limbs * limbs + 16 * sqr
 
 
 # ---------------------------------------------------------------- inputs
@@ -365,7 +370,7 @@ def run_configs(ctx, args, threads, rank, world, dist):
     out["ps512_rsa4096"] = config_line(
         ctx, "ps512_rsa4096", "PS512 RSA-4096 (PSS/MGF1-SHA512), 1M tokens / 8 GPUs = 131072 per GPU (configs[2])",
         pool, [ALG_IDS["PS512"]] * len(pool), [0] * len(pool), np.ones(len(pool), bool), 131072,
-        max(1, args.steps // 2), 1, dist, world, "rsa4096_modexp", rsa_modexp_mads_per_token(148))
+        max(1, args.steps // 2), 1, dist, world, "rsa4096_modexp", rsa_modexp_mads_per_token(148, 4))
     # configs[3]: EdDSA Ed25519 + ES384 P-384 mixed, 1M tokens per GPU
     ctx.load_keys(abi_keys(["ed-a", "p384-a"]))
     pe = gen_tokens("EdDSA", 8192, golden_keypaths(["ed-a"]), threads, f"c3r{rank}")
@@ -496,13 +501,13 @@ def main():
         rsteps = max(1, args.steps // 2)
         rel, racc, rkms, _ = measure(ctx, rarena, rtoks, rsteps, 1, dist)
         mexp = rkms.get("rsa2048_modexp", float("nan"))
-        rach = rsa_modexp_mads_per_token(74) * len(rtoks) / (mexp * 1e-3) / 1e12
+        rach = rsa_modexp_mads_per_token(74, 2) * len(rtoks) / (mexp * 1e-3) / 1e12
         result["rs256"] = {"value": world * len(rtoks) * rsteps / rel, "unit": "verified JWTs/s",
                            "ms_per_step": rel * 1000.0 / rsteps, "tokens_per_gpu": len(rtoks),
                            "accepted": racc, "kernel_ms": rkms,
                            "roofline": {"bound": "valu", "kernel": "k_rsa_modexp<37,2,8>", "achieved": rach,
                                         "peak": MAD_PEAK_T, "unit": "TMAD/s", "frac": rach / MAD_PEAK_T,
-                                        "mads_per_token": rsa_modexp_mads_per_token(74),
+                                        "mads_per_token": rsa_modexp_mads_per_token(74, 2),
                                         "traffic": load_traffic("rsa2048_modexp")}}
         if racc != len(rtoks):
             result["rs256"]["error"] = f"only {racc}/{len(rtoks)} valid tokens accepted"

@@ -19,6 +19,7 @@
 #include "rsa.hpp"
 #include "sha2.hpp"
 #include "mad.hpp"
+#include "mad_blocks.hpp"
 
 using namespace jgk;
 
@@ -28,6 +29,12 @@ using namespace jgk;
 #define SQR_SLOTS 4
 #endif
 #define SQR_SLOT(k) ((k) % SQR_SLOTS)
+#ifndef JG_RSA_SHIFT28
+#define JG_RSA_SHIFT28 1
+#endif
+#ifndef JG_RSA_BLOCKS
+#define JG_RSA_BLOCKS 1
+#endif
 
 namespace {
 
@@ -37,22 +44,64 @@ namespace {
 template <int G>
 __device__ __forceinline__ uint32_t bcast0(uint32_t x) {        // value of group lane 0
   constexpr int ctrl = G == 2 ? 0xA0 /* quad_perm 0,0,2,2 */ : 0x00 /* 0,0,0,0 */;
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
 }
 template <int G>
 __device__ __forceinline__ uint32_t bcast_last(uint32_t x) {    // value of group lane G-1
   constexpr int ctrl = G == 2 ? 0xF5 /* quad_perm 1,1,3,3 */ : 0xFF /* 3,3,3,3 */;
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
 }
 template <int G>
 __device__ __forceinline__ uint32_t from_next(uint32_t x) {     // value of group lane g+1
   constexpr int ctrl = G == 2 ? 0xF5 /* 1,1,3,3 */ : 0xF9 /* 1,2,3,3 */;
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
 }
 template <int G>
 __device__ __forceinline__ uint32_t from_prev(uint32_t x) {     // value of group lane g-1
   constexpr int ctrl = G == 2 ? 0xA0 /* quad_perm 0,0,2,2 */ : 0x90 /* 0,0,1,2 */;
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
+}
+
+// T[k] += a * b[k] for k < n (n compile-time after unrolling) as blocks of up
+// to 8 MADs per inline-asm statement: LLVM pads a hazard s_nop after an asm
+// statement whose results the next instruction touches, so one MAD per asm
+// cost ~1 s_nop per 4 MADs here (profiles/r01_int_rates2.json: 28.8 T MAD/s
+// with one MAD per asm vs 33.6 T with 8 per asm at 2 waves/SIMD).
+__device__ __forceinline__ void madv_run(uint64_t* T, uint32_t a, const uint32_t* b, int n) {
+  for (int k = 0; k < n; k += 8) {
+    uint64_t* t = T + k;
+    const uint32_t* c = b + k;
+    switch (n - k < 8 ? n - k : 8) {
+      case 1: mb::madv1(t[0], a, c[0]); break;
+      case 2: mb::madv2(t[0], t[1], a, c[0], c[1]); break;
+      case 3: mb::madv3(t[0], t[1], t[2], a, c[0], c[1], c[2]); break;
+      case 4: mb::madv4(t[0], t[1], t[2], t[3], a, c[0], c[1], c[2], c[3]); break;
+      case 5: mb::madv5(t[0], t[1], t[2], t[3], t[4], a, c[0], c[1], c[2], c[3], c[4]); break;
+      case 6: mb::madv6(t[0], t[1], t[2], t[3], t[4], t[5], a, c[0], c[1], c[2], c[3], c[4], c[5]); break;
+      case 7: mb::madv7(t[0], t[1], t[2], t[3], t[4], t[5], t[6], a, c[0], c[1], c[2], c[3], c[4], c[5], c[6]); break;
+      default: mb::madv8(t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7], a, c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]); break;
+    }
+  }
+}
+
+// The limb shift that ends a CIOS row: every lane keeps T[0]'s bits above
+// 28 in its own T[1] (same weight) and hands the low 28 bits to the lane below,
+// which places them in its fresh top slot T[H] (the top lane's fresh slot is
+// zero).  In lane 0, T[0] mod 2^28 = 0 after the reduction: the limb that the
+// Montgomery division drops.  One 32-bit DPP move per row, no lane-0 select.
+template <int H, int G>
+__device__ __forceinline__ void limb_shift(uint64_t* T, bool lane0, bool lastl) {
+  const uint64_t t0 = T[0];
+#if JG_RSA_SHIFT28
+  T[1] += t0 >> W28;
+  const uint32_t lo = from_next<G>((uint32_t)t0 & M28);
+  T[H] = lastl ? 0ull : (uint64_t)lo;
+#else
+  T[1] += lane0 ? (t0 >> W28) : 0ull;
+  const uint32_t lo = from_next<G>((uint32_t)t0);
+  const uint32_t hi = from_next<G>((uint32_t)(t0 >> 32));
+  T[H] = lastl ? 0ull : (((uint64_t)hi << 32) | lo);
+#endif
 }
 
 // One CIOS iteration on this lane's window T[0..H) of the token's accumulator.
@@ -62,16 +111,18 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t x) {     // value of grou
 template <int H, int G>
 __device__ __forceinline__ void cios_step(uint64_t* T, uint32_t ai, const uint32_t* v, const uint32_t* n,
                                           uint32_t np, bool lane0, bool lastl) {
+#if JG_RSA_BLOCKS
+  madv_run(T, ai, v, H);
+  const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
+  madv_run(T, m, n, H);
+#else
 #pragma unroll
   for (int j = 0; j < H; ++j) mad64(T[j], ai, v[j], j & 1);
   const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
 #pragma unroll
   for (int j = 0; j < H; ++j) mad64(T[j], m, n[j], 2 + (j & 1));
-  const uint64_t c = lane0 ? (T[0] >> W28) : 0ull;
-  T[1] += c;
-  const uint32_t lo = from_next<G>((uint32_t)T[0]);
-  const uint32_t hi = from_next<G>((uint32_t)(T[0] >> 32));
-  T[H] = lastl ? 0ull : (((uint64_t)hi << 32) | lo);
+#endif
+  limb_shift<H, G>(T, lane0, lastl);
 }
 
 // v <- the lane's accumulator window P[0..H), normalised within the lane, then
@@ -167,16 +218,18 @@ __device__ __forceinline__ void mont_sqr(uint32_t* v, const uint32_t* la, const 
       uint64_t* T = P + x;
       mad64(T[x], (ai << sh) & msk, v[x], SQR_SLOT(x));
       const uint32_t a2 = ai << 1;
+#if JG_RSA_BLOCKS
+      madv_run(T + x + 1, a2, v + x + 1, H - x - 1);
+      const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
+      madv_run(T, m, n, H);
+#else
 #pragma unroll
       for (int k = x + 1; k < H; ++k) mad64(T[k], a2, v[k], SQR_SLOT(k));
       const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
 #pragma unroll
       for (int k = 0; k < H; ++k) mad64(T[k], m, n[k], SQR_SLOT(k + 2));
-      const uint64_t c = lane0 ? (T[0] >> W28) : 0ull;
-      T[1] += c;
-      const uint32_t lo = from_next<G>((uint32_t)T[0]);
-      const uint32_t hi = from_next<G>((uint32_t)(T[0] >> 32));
-      T[H] = lastl ? 0ull : (((uint64_t)hi << 32) | lo);
+#endif
+      limb_shift<H, G>(T, lane0, lastl);
     }
     if constexpr (2 * L > 250) {
       if (r == G / 2 - 1) {   // keep every 64-bit column < 2^64: normalise half-way
