@@ -9,9 +9,9 @@ namespace jgk {
 // key's run is padded to a whole wave, so the key is wave-uniform.
 enum Cls : int {
   CLS_REJECT = 0,   // alg/key-type mismatch, unsupported alg, invalid key
-  CLS_RSA2K = 1,    // RSA, modulus <= 2070 bits  (74 x 28-bit limbs)
-  CLS_RSA3K = 2,    // RSA, modulus <= 3078 bits  (110 limbs)
-  CLS_RSA4K = 3,    // RSA, modulus <= 4114 bits  (147 limbs)
+  CLS_RSA2K = 1,    // RSA, modulus <= 2070 bits  (74 x 28-bit limbs; rsa.hpp rsa_limbs)
+  CLS_RSA3K = 2,    // RSA, modulus <= 3134 bits  (112 limbs)
+  CLS_RSA4K = 3,    // RSA, modulus <= 4142 bits  (148 limbs)
   CLS_P256 = 4,
   CLS_P384 = 5,
   CLS_P521 = 6,
@@ -37,7 +37,7 @@ struct DevKey {
   int32_t kbytes;      // RSA: modulus bytes k; EC: coord bytes; Ed: 32
   uint32_t e_lo, e_hi; // RSA public exponent
   uint32_t np;         // RSA: -n^-1 mod 2^28
-  uint32_t nlimbs;     // RSA: limb count used (74/110/147)
+  uint32_t nlimbs;     // RSA: limb count used (74/112/148)
   uint64_t n_off;      // RSA: n (28-bit limbs)        -- word offset in blob
   uint64_t rr_off;     // RSA: R^2 mod n (28-bit limbs)
   uint64_t tab_off;    // EC: comb table of Q / Ed: comb table of -A

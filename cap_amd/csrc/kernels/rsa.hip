@@ -84,23 +84,36 @@ __device__ __forceinline__ void madv_run(uint64_t* T, uint32_t a, const uint32_t
   }
 }
 
+// All-ones in the lanes that keep a cross-lane value, zero in the others, as
+// a value the optimizer cannot see through.  Written as `lane0 ? 0 : dpp(x)`
+// the select may become a branch, and LLVM then sinks the computation of x --
+// and the DPP read of it -- under that branch, where EXEC has switched off the
+// very lanes the DPP reads (they read as 0).  That lost lane 0's borrow in the
+// final subtraction whenever s^e mod n = n - 1 (tests/test_gpu_rsa.py).  An
+// AND with an opaque mask keeps every DPP source computed in every lane.
+__device__ __forceinline__ uint32_t opaque_mask(bool keep) {
+  uint32_t m = keep ? ~0u : 0u;
+  asm volatile("" : "+v"(m));
+  return m;
+}
+
 // The limb shift that ends a CIOS row: every lane keeps T[0]'s bits above
 // 28 in its own T[1] (same weight) and hands the low 28 bits to the lane below,
 // which places them in its fresh top slot T[H] (the top lane's fresh slot is
 // zero).  In lane 0, T[0] mod 2^28 = 0 after the reduction: the limb that the
 // Montgomery division drops.  One 32-bit DPP move per row, no lane-0 select.
 template <int H, int G>
-__device__ __forceinline__ void limb_shift(uint64_t* T, bool lane0, bool lastl) {
+__device__ __forceinline__ void limb_shift(uint64_t* T, bool lane0, uint32_t mlast) {
   const uint64_t t0 = T[0];
 #if JG_RSA_SHIFT28
   T[1] += t0 >> W28;
   const uint32_t lo = from_next<G>((uint32_t)t0 & M28);
-  T[H] = lastl ? 0ull : (uint64_t)lo;
+  T[H] = (uint64_t)(lo & mlast);
 #else
   T[1] += lane0 ? (t0 >> W28) : 0ull;
   const uint32_t lo = from_next<G>((uint32_t)t0);
   const uint32_t hi = from_next<G>((uint32_t)(t0 >> 32));
-  T[H] = lastl ? 0ull : (((uint64_t)hi << 32) | lo);
+  T[H] = ((uint64_t)(hi & mlast) << 32) | (lo & mlast);
 #endif
 }
 
@@ -110,7 +123,7 @@ __device__ __forceinline__ void limb_shift(uint64_t* T, bool lane0, bool lastl) 
 //   places it in its fresh top slot T[H] (the limb shift across lanes).
 template <int H, int G>
 __device__ __forceinline__ void cios_step(uint64_t* T, uint32_t ai, const uint32_t* v, const uint32_t* n,
-                                          uint32_t np, bool lane0, bool lastl) {
+                                          uint32_t np, bool lane0, uint32_t mlast) {
 #if JG_RSA_BLOCKS
   madv_run(T, ai, v, H);
   const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
@@ -122,7 +135,7 @@ __device__ __forceinline__ void cios_step(uint64_t* T, uint32_t ai, const uint32
 #pragma unroll
   for (int j = 0; j < H; ++j) mad64(T[j], m, n[j], 2 + (j & 1));
 #endif
-  limb_shift<H, G>(T, lane0, lastl);
+  limb_shift<H, G>(T, lane0, mlast);
 }
 
 // v <- the lane's accumulator window P[0..H), normalised within the lane, then
@@ -130,7 +143,7 @@ __device__ __forceinline__ void cios_step(uint64_t* T, uint32_t ai, const uint32
 // lane up (the top lane's carry-out is zero because the value is
 // < 2n < 2^(28L)).
 template <int H, int G>
-__device__ __forceinline__ void finish_product(uint32_t* v, const uint64_t* P, bool lane0) {
+__device__ __forceinline__ void finish_product(uint32_t* v, const uint64_t* P, uint32_t ml0) {
   uint64_t c = 0;
 #pragma unroll
   for (int j = 0; j < H; ++j) {
@@ -141,7 +154,7 @@ __device__ __forceinline__ void finish_product(uint32_t* v, const uint64_t* P, b
 #pragma unroll
   for (int r = 0; r < G - 1; ++r) {
     const uint32_t clo = from_prev<G>((uint32_t)c), chi = from_prev<G>((uint32_t)(c >> 32));
-    uint64_t cin = lane0 ? 0ull : (((uint64_t)chi << 32) | clo);
+    uint64_t cin = ((uint64_t)(chi & ml0) << 32) | (clo & ml0);
 #pragma unroll
     for (int j = 0; j < H; ++j) {
       const uint64_t t = (uint64_t)v[j] + cin;
@@ -157,7 +170,7 @@ __device__ __forceinline__ void finish_product(uint32_t* v, const uint64_t* P, b
 // Out: v < 2n, limbs < 2^28 (carries rippled across the group).
 template <int H, int G, int U, int TPW>
 __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const uint32_t* n, uint32_t np,
-                                         bool lane0, bool lastl) {
+                                         bool lane0, uint32_t mlast, uint32_t ml0) {
   constexpr int L = H * G, NB = L / U, REM = L % U;
   uint64_t P[H + U];
 #pragma unroll
@@ -167,7 +180,7 @@ __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const 
 #pragma unroll
     for (int u = 0; u < U; ++u) a[u] = la[(ib * U + u) * TPW];
 #pragma unroll
-    for (int u = 0; u < U; ++u) cios_step<H, G>(P + u, a[u], v, n, np, lane0, lastl);
+    for (int u = 0; u < U; ++u) cios_step<H, G>(P + u, a[u], v, n, np, lane0, mlast);
     if constexpr (2 * L > 250) {
       // keep every 64-bit column < 2^64 (2L products of < 2^56): normalise half-way
       if (ib == NB / 2) {
@@ -181,8 +194,8 @@ __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const 
     for (int j = H; j < H + U; ++j) P[j] = 0;
   }
 #pragma unroll
-  for (int u = 0; u < REM; ++u) cios_step<H, G>(P + u, la[(NB * U + u) * TPW], v, n, np, lane0, lastl);
-  finish_product<H, G>(v, P + REM, lane0);
+  for (int u = 0; u < REM; ++u) cios_step<H, G>(P + u, la[(NB * U + u) * TPW], v, n, np, lane0, mlast);
+  finish_product<H, G>(v, P + REM, ml0);
 }
 
 // v <- v^2 / R mod n: the squaring form of mont_mul (16 of the 18 products of
@@ -202,7 +215,7 @@ __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const 
 // physical shift of the window per H rows.
 template <int H, int G, int TPW>
 __device__ __forceinline__ void mont_sqr(uint32_t* v, const uint32_t* la, const uint32_t* n, uint32_t np, int g,
-                                         bool lane0, bool lastl) {
+                                         bool lane0, uint32_t mlast, uint32_t ml0) {
   constexpr int L = H * G;
   uint64_t P[2 * H];
 #pragma unroll
@@ -229,7 +242,7 @@ __device__ __forceinline__ void mont_sqr(uint32_t* v, const uint32_t* la, const 
 #pragma unroll
       for (int k = 0; k < H; ++k) mad64(T[k], m, n[k], SQR_SLOT(k + 2));
 #endif
-      limb_shift<H, G>(T, lane0, lastl);
+      limb_shift<H, G>(T, lane0, mlast);
     }
     if constexpr (2 * L > 250) {
       if (r == G / 2 - 1) {   // keep every 64-bit column < 2^64: normalise half-way
@@ -240,7 +253,7 @@ __device__ __forceinline__ void mont_sqr(uint32_t* v, const uint32_t* la, const 
 #pragma unroll
     for (int j = 0; j < H; ++j) P[j] = P[j + H];
   }
-  finish_product<H, G>(v, P, lane0);
+  finish_product<H, G>(v, P, ml0);
 }
 
 template <int H, int TPW>
@@ -286,6 +299,7 @@ __global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
   const int lane = threadIdx.x;
   const int g = lane % G, tl = lane / G;
   const bool lane0 = g == 0, lastl = g == G - 1;
+  const uint32_t ml0 = opaque_mask(!lane0), mlast = opaque_mask(!lastl);
   const int64_t pbase = a.begin + (int64_t)blockIdx.x * TPW;
   const int64_t p = pbase + tl;
   const int64_t np = a.npad;
@@ -322,7 +336,7 @@ __global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
 #pragma unroll
     for (int r = 0; r < G - 1; ++r) {
       const int up = (int)from_next<G>((uint32_t)dec);
-      dec = (!lastl && up != 0) ? up : dec;
+      dec = (up & (int)mlast) != 0 ? (up & (int)mlast) : dec;
     }
     dec = (int)bcast0<G>((uint32_t)dec);
     act = act && dec == 1;
@@ -356,8 +370,8 @@ __global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
 #pragma unroll
       for (int j = 0; j < H; ++j) v[j] = (j == 0 && lane0) ? 1u : 0u;
     }
-    if (op == SQUARE) mont_sqr<H, G, TPW>(v, la, n, np28, g, lane0, lastl);
-    else mont_mul<H, G, U, TPW>(v, la, n, np28, lane0, lastl);
+    if (op == SQUARE) mont_sqr<H, G, TPW>(v, la, n, np28, g, lane0, mlast, ml0);
+    else mont_mul<H, G, U, TPW>(v, la, n, np28, lane0, mlast, ml0);
     if (op == TOMONT) {
       if (mid) store_limb_rows<H>(a.xmw, np, loff, v);
       op = SQUARE;
@@ -380,7 +394,7 @@ __global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
     int32_t bout = 0;
 #pragma unroll
     for (int r = 0; r < G; ++r) {
-      int32_t br = lane0 ? 0 : (int32_t)from_prev<G>((uint32_t)bout);
+      int32_t br = (int32_t)(from_prev<G>((uint32_t)bout) & ml0);
 #pragma unroll
       for (int j = 0; j < H; ++j) {
         const int32_t t = (int32_t)v[j] - (int32_t)n[j] + br;
