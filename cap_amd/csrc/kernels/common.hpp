@@ -25,7 +25,7 @@ constexpr int WAVE = 64;
 enum : uint8_t { ST_OK = 0, ST_REJECT = 1, ST_EXCEPTIONAL = 2 };
 
 // scratch rows (each row holds one 32-bit word per padded token, SoA)
-constexpr int SIGW_ROWS = 128;      // decoded signature, up to 512 bytes
+constexpr int SIGW_ROWS = 132;      // decoded signature, up to 528 bytes (RSA-4142: 518)
 constexpr int EC_S_ROW = 32;        // ECDSA: s starts at row 32 (r at row 0)
 constexpr int DIG_ROWS = 16;        // digest, big-endian 32-bit words
 

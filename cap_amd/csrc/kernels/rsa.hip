@@ -269,8 +269,8 @@ __device__ __forceinline__ void load_limbs_from_words(uint32_t* v, const uint32_
 #pragma unroll
   for (int j = 0; j < H; ++j) {
     const int bit = W28 * (g * H + j), q = bit >> 5, s = bit & 31;
-    const uint32_t w0 = q < nrows ? rows[(int64_t)q * np + p] : 0u;
-    const uint32_t w1 = (q + 1) < nrows ? rows[(int64_t)(q + 1) * np + p] : 0u;
+    const uint32_t w0 = rows[(int64_t)q * np + p];       // rows up to (28 L - 1) / 32 + 1
+    const uint32_t w1 = rows[(int64_t)(q + 1) * np + p]; // exist and are zeroed (rsa_sig_rows)
     const uint64_t ww = ((uint64_t)w1 << 32) | w0;
     v[j] = (uint32_t)(ww >> s) & M28;
   }
@@ -294,7 +294,8 @@ __device__ __forceinline__ void store_limb_rows(uint32_t* rows, int64_t np, uint
 template <int H, int G, int U>
 __global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
   constexpr int L = H * G, TPW = WAVE / G;
-  constexpr int NWOUT = (W28 * L + 31) / 32 < SIGW_ROWS ? (W28 * L + 31) / 32 : SIGW_ROWS;
+  constexpr int NWOUT = (W28 * L + 31) / 32;
+  static_assert((W28 * L - 1) / 32 + 2 <= SIGW_ROWS, "limb loads and y words must fit the signature rows");
   __shared__ uint32_t lds[L * TPW];
   const int lane = threadIdx.x;
   const int g = lane % G, tl = lane / G;

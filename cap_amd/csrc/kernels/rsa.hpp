@@ -38,8 +38,9 @@ constexpr int rsa_limbs(int cls) {
 // touch words up to (28 L - 1) / 32 + 1 (load_limbs_from_words), so those
 // rows must be zeroed by prep
 constexpr int rsa_sig_rows(int cls) {
-  return cls == jgk::CLS_RSA4K ? 128 : (28 * rsa_limbs(cls) - 1) / 32 + 2;
+  return (28 * rsa_limbs(cls) - 1) / 32 + 2;
 }
+static_assert(rsa_sig_rows(jgk::CLS_RSA4K) <= jgk::SIGW_ROWS, "RSA-4K signature rows exceed the scratch");
 
 void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const jgk::Marker& mk);
 void launch_rsa_keyprep(jgk::DevKey* keys, uint32_t* blob, int nkeys, hipStream_t s);

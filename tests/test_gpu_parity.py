@@ -1,5 +1,7 @@
 """GPU parity: the HIP path through the C ABI (libcapjwt.so) against the
 golden fixtures (OpenSSL-signed, Go-semantics labelled) and the CPU oracle."""
+import os
+
 import pytest
 
 from tests import gpu_helpers as H
@@ -174,3 +176,24 @@ def test_key_reload_reuses_tables():
         assert not bad, bad
     assert again < first            # the last reload rebuilds nothing
     c.close()
+
+
+def test_rsa_keys_above_4096_bits():
+    """RSA moduli of 4100 and 4142 bits (the largest the 148-limb class holds;
+    signatures of 513-518 bytes): the GPU verdicts equal the oracle's and the
+    fixture's (tests/golden/rsa_big.json, made by make_big_rsa.py)."""
+    import json
+    from oracle import jws
+    d = json.load(open(os.path.join(H.ROOT, "tests", "golden", "rsa_big.json")))
+    from cap_amd import _lib
+    kid_index = {k["kid"]: i for i, k in enumerate(d["keys"])}
+    ctx = _lib.Context()
+    ctx.load_keys([H.abi_key(k) for k in d["keys"]])
+    arena, slots = H.jobs_from_tokens(d["tokens"], kid_index)
+    out = ctx.verify(arena)
+    ctx.close()
+    okeys = {k["kid"]: jws.Key.from_fixture(k) for k in d["keys"]}
+    for t, s in zip(d["tokens"], slots):
+        want = int(jws.verify_sig(jws.parse_jws(t["token"]), okeys[t["key"]]))
+        assert want == t["want"], t["name"]
+        assert out[s] == want, t["name"]

@@ -88,3 +88,17 @@ def test_static_keyset_semantics(golden):
             except jws.ErrNoKey:
                 got = 0
             assert got == t["keyset_verdict"], t["name"]
+
+
+def test_oracle_rsa_keys_above_4096_bits():
+    """RSA-4100 / RSA-4142 keys (tests/golden/rsa_big.json): Go's crypto/rsa
+    has no 4096-bit ceiling, so valid RS256/RS512 tokens accept and
+    signature-flipped ones reject."""
+    import json
+    import os
+    from oracle import jws
+    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rsa_big.json")))
+    keys = {k["kid"]: jws.Key.from_fixture(k) for k in d["keys"]}
+    for t in d["tokens"]:
+        p = jws.parse_jws(t["token"])
+        assert int(jws.verify_sig(p, keys[t["key"]])) == t["want"], t["name"]
