@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 KEYDIR = os.path.join(ROOT, "tests", "golden", "keys")
 BENCHKEYS = os.path.join(ROOT, "tools", "benchkeys")
 TOKGEN = os.path.join(ROOT, "tools", "tokgen", "tokgen")
-TRAFFIC = os.path.join(ROOT, "profiles", "r01_s6_pmc_traffic.json")
+TRAFFIC = os.path.join(ROOT, "profiles", "r01_s7_pmc_traffic.json")
 COLL_DEVICE = "cuda"            # device of the timing all-reduce (RCCL); "cpu" under gloo
 
 # measured v_mad_u64_u32 issue rate, chip-wide: the integer multiply-add
@@ -483,7 +483,7 @@ def main():
                      "note": "integer multiply-add roofline (SURVEY §8d): algorithmic 32x32->64 MADs "
                              f"per token {p256_point_mads_per_token():.0f} x tokens / HIP-event kernel time; "
                              "peak = measured v_mad_u64_u32 rate; traffic = HBM bytes per launch from the "
-                             "rocprofv3 --pmc pass in profiles/r01_s6_pmc_traffic.json"},
+                             "rocprofv3 --pmc pass in profiles/r01_s7_pmc_traffic.json"},
         "kernel_ms": kms,
     }
     if acc != ntok:
