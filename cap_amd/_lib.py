@@ -20,7 +20,8 @@ CURVE_IDS = {"P-256": 1, "P-384": 2, "P-521": 3}
 # every symbol include/jg.h declares
 EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_last_error",
            "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_enqueue", "jg_batch_sync",
-           "jg_batch_free", "jg_batch_kernel_times", "jg_hash_batch", "jg_version"]
+           "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
+           "jg_submit", "jg_wait", "jg_set_chunk"]
 
 
 class JgKey(ctypes.Structure):
@@ -69,6 +70,10 @@ def lib():
         L.jg_batch_free.argtypes = [vp, vp]
         L.jg_batch_kernel_times.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
                                             ctypes.c_int]
+        L.jg_batch_exceptions.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
+        L.jg_submit.argtypes = [vp, vp, sz, ctypes.POINTER(JgTok), sz, vp, ctypes.POINTER(vp)]
+        L.jg_wait.argtypes = [vp, vp]
+        L.jg_set_chunk.argtypes = [vp, sz]
         L.jg_hash_batch.argtypes = [vp, vp, sz, vp, sz, vp]
         L.jg_version.restype = ctypes.c_char_p
         _lib = L
@@ -172,6 +177,14 @@ class Context:
             raise JgError(f"jg_verify_batch rc={rc}: {self.error()}")
         return bytes(out[:n])
 
+    def set_chunk(self, jobs):
+        if lib().jg_set_chunk(self.h, jobs) != 0:
+            raise JgError("jg_set_chunk: chunk must be >= 64 jobs")
+
+    def submit(self, arena: Arena):
+        """jg_submit; returns a Pending whose wait() gives the verdict bytes."""
+        return Pending(self, arena)
+
     # ---- device-resident batches (bench)
     def stage(self, arena: Arena, slot=0):
         h = ctypes.c_void_p()
@@ -181,6 +194,28 @@ class Context:
         if rc != 0:
             raise JgError(f"jg_batch_stage rc={rc}: {self.error()}")
         return Batch(self, h, len(arena.toks))
+
+
+class Pending:
+    """One jg_submit in flight (buffers kept alive until wait())."""
+
+    def __init__(self, ctx, arena):
+        self.ctx = ctx
+        self.n = len(arena.toks)
+        self.buf = ctypes.create_string_buffer(bytes(arena.buf) or b"\0", max(1, len(arena.buf)))
+        self.toks = arena.tok_array()
+        self.out = (ctypes.c_uint8 * max(1, self.n))()
+        self.t = ctypes.c_void_p()
+        rc = lib().jg_submit(ctx.h, self.buf, len(arena.buf), self.toks, self.n, self.out, ctypes.byref(self.t))
+        if rc != 0:
+            raise JgError(f"jg_submit rc={rc}: {ctx.error()}")
+
+    def wait(self):
+        rc = lib().jg_wait(self.ctx.h, self.t)
+        self.t = None
+        if rc != 0:
+            raise JgError(f"jg_wait rc={rc}: {self.ctx.error()}")
+        return bytes(self.out[:self.n])
 
 
 class PinnedBuffer:
@@ -230,6 +265,14 @@ class Batch:
         rc = lib().jg_batch_sync(self.ctx.h, self.h)
         if rc != 0:
             raise JgError(f"jg_batch_sync rc={rc}: {self.ctx.error()}")
+
+    def exceptions(self):
+        """Per-class count of tokens the last run sent down the exact ECDSA path."""
+        c = (ctypes.c_uint32 * 8)()
+        n = lib().jg_batch_exceptions(self.h, c, 8)
+        if n < 0:
+            raise JgError(f"jg_batch_exceptions rc={n}: {self.ctx.error()}")
+        return list(c)
 
     def kernel_times(self):
         names = (ctypes.c_char_p * 64)()

@@ -15,10 +15,13 @@
 //      do not depend on which key verified).
 #include "cap_jwt.hpp"
 
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -38,14 +41,32 @@ std::string SupportedSigningAlgorithm(const std::vector<std::string>& algs) {
   return "";
 }
 
+// CPUs this process may run on: the affinity mask, capped by a cgroup v2 CPU
+// quota (a container's share of a large host), never a fixed number.
+int available_cpus() {
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {0};
+    long period = 0;
+    if (std::fscanf(f, "%31s %ld", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0) {
+      const long q = std::atol(quota);
+      if (q > 0) n = std::min<int>(n, (int)((q + period - 1) / period));
+    }
+    std::fclose(f);
+  }
+  return std::max(1, n);
+}
+
 int host_threads() {
   static const int n = [] {
     if (const char* e = std::getenv("CAPJWT_HOST_THREADS")) {
       const int v = std::atoi(e);
       if (v > 0) return v;
     }
-    const int hw = (int)std::thread::hardware_concurrency();
-    return std::max(1, std::min(hw > 0 ? hw : 1, 16));
+    return available_cpus();
   }();
   return n;
 }
@@ -590,13 +611,22 @@ class JSONWebKeySet final : public KeySet {
       return false;
     }
     if (keys.size() > 65535) { *err = "oidc: too many keys"; return false; }
+    // the new key list is committed only once the device table holds it: a
+    // failed staging keeps the previous cache, as go-oidc keeps its cached
+    // keys when updateKeys fails
     std::vector<PublicKey> pk;
-    fam_.clear();
+    std::vector<int> fam;
     for (const auto& k : keys) {
       pk.push_back(k.key);
-      fam_.push_back(key_family(k.key));
+      fam.push_back(key_family(k.key));
     }
-    eng_.load(pk);
+    try {
+      eng_.load(pk);
+    } catch (const std::exception& e) {
+      *err = std::string("oidc: failed to stage keys: ") + e.what();
+      return false;
+    }
+    fam_ = std::move(fam);
     keys_ = std::move(keys);
     have_keys_ = true;
     expiry_ns_ = wall_now_ns() + (resp.max_age_s > 0 ? resp.max_age_s * kSecond : 0);

@@ -177,8 +177,10 @@ bool ParsePublicKeyPEM(std::string_view data, PublicKey* out, std::string* err);
 void release_results(std::vector<Result>& rs);
 
 // Host threads used by batch parsing / claims (CAPJWT_HOST_THREADS, default
-// min(hardware threads, 16)).
+// available_cpus()).
 int host_threads();
+// CPUs available to this process (affinity mask, cgroup v2 quota)
+int available_cpus();
 
 // ---------------------------------------------------------------- oidc hash claims
 // IDToken.VerifyAccessToken / VerifyAuthorizationCode (oidc/id_token.go:59-145,

@@ -264,6 +264,7 @@ PYBIND11_MODULE(_capjwt_host, m) {
     return result_py(r);
   });
   m.def("host_threads", &host_threads);
+  m.def("available_cpus", &available_cpus);
 
   // ---- GPU-backed key sets and validator
   py::class_<PyKeySet>(m, "KeySet")

@@ -1,6 +1,6 @@
 // jg_runtime.cpp -- host runtime behind include/jg.h.
 //
-// Owns the per-device state (stream, generator / base-point comb tables, the
+// Owns the per-device state (streams, generator / base-point comb tables, the
 // staged key table) and turns a flat job list into a dispatch plan:
 //   1. classify every (alg, key) pair into a kernel class (RSA-2K/3K/4K, P-256,
 //      P-384, P-521, Ed25519, or reject -- go-jose newVerifier/verifyPayload
@@ -9,19 +9,30 @@
 //      whole 64-lane wave, so each wave's key is uniform (scalar key loads,
 //      broadcast modulus limbs);
 //   3. launch prep (base64url + SHA-2) and the class's arithmetic kernels over
-//      the padded ranges on the device's stream; scatter verdicts back.
-// Multiple devices: jobs are split into contiguous chunks weighted by the
-// per-alg cost model and run concurrently, one host thread per device.
+//      the padded ranges; scatter verdicts back.
+//
+// Streaming path (jg_submit / jg_wait / jg_verify_batch): a batch
+// is split over the devices by the per-alg cost model, and each device's part
+// runs through a ring of NSLOT pipeline slots in chunks of CHUNK jobs.  Every
+// slot owns a stream (+ per-class fan-out streams), device scratch and pinned
+// host staging, so the host plan and the H2D copy of chunk k+1 overlap the
+// kernels of chunk k.  One worker thread per device drains a FIFO of submitted
+// work, so chunks of consecutive submissions overlap as well.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstddef>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -45,12 +56,36 @@ using namespace jgk;
 namespace {
 
 constexpr size_t ARENA_SLACK = 256;   // aligned SHA word reads may run past the last string
+constexpr int NSLOT = 3;              // pipeline depth per device
+constexpr int NALG = 16;              // alg ids 0..15 in the class table (jg_alg <= 10)
 
 #define HIPCHK(x)                                                                   \
   do {                                                                              \
     hipError_t e_ = (x);                                                            \
     if (e_ != hipSuccess) throw std::runtime_error(std::string(#x ": ") + hipGetErrorString(e_)); \
   } while (0)
+
+bool pipe_trace() {
+  static const bool on = std::getenv("CAPJWT_PIPE_TRACE") != nullptr;
+  return on;
+}
+hipEvent_t g_trace_ref = nullptr;     // first chunk's H2D start (trace only)
+std::chrono::steady_clock::time_point g_trace_t0;
+
+double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+size_t chunk_jobs() {
+  static const size_t n = [] {
+    if (const char* e = std::getenv("CAPJWT_CHUNK")) {
+      const long v = std::atol(e);
+      if (v >= 64) return (size_t)v;
+    }
+    return (size_t)131072;
+  }();
+  return n;
+}
 
 int cls_rows_sig(int c) {
   switch (c) {
@@ -91,12 +126,31 @@ struct Grow {                     // grow-only device allocation
     if (n > cap) {
       if (p) (void)hipFree(p);
       p = nullptr;
+      cap = 0;
       HIPCHK(hipMalloc(&p, n));
       cap = n;
     }
     return p;
   }
   ~Grow() { if (p) (void)hipFree(p); }
+};
+
+struct HGrow {                    // grow-only pinned host allocation
+  void* p = nullptr;
+  size_t cap = 0;
+  void* get(size_t n) {
+    if (n == 0) n = 16;
+    if (n > cap) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+      const size_t want = std::max(n, cap + cap / 2);
+      HIPCHK(hipHostMalloc(&p, want, hipHostMallocPortable));
+      cap = want;
+    }
+    return p;
+  }
+  ~HGrow() { if (p) (void)hipHostFree(p); }
 };
 
 struct HostKey {
@@ -114,17 +168,109 @@ struct SharedTable {
 std::mutex g_tab_mu;
 std::map<std::pair<int, int>, std::weak_ptr<SharedTable>> g_tabs;   // (device id, class) -> table
 
+// One in-order stream plus per-class fan-out streams: a mixed batch's classes
+// are each too small to fill 256 CUs alone, so untimed runs put every class's
+// kernel chain on its own stream, joined back before the scatter.
+struct Lane {
+  hipStream_t stream = nullptr;
+  hipStream_t cstream[NCLS] = {};
+  hipEvent_t ev_start = nullptr, ev_done[NCLS] = {};
+  void create() {
+    HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    for (int c = 1; c < NCLS; ++c) {
+      HIPCHK(hipStreamCreateWithFlags(&cstream[c], hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&ev_done[c], hipEventDisableTiming));
+    }
+    HIPCHK(hipEventCreateWithFlags(&ev_start, hipEventDisableTiming));
+  }
+  void sync() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (int c = 1; c < NCLS; ++c)
+      if (cstream[c]) (void)hipStreamSynchronize(cstream[c]);
+  }
+  void destroy() {
+    sync();
+    for (int c = 1; c < NCLS; ++c) {
+      if (cstream[c]) (void)hipStreamDestroy(cstream[c]);
+      if (ev_done[c]) (void)hipEventDestroy(ev_done[c]);
+      cstream[c] = nullptr;
+      ev_done[c] = nullptr;
+    }
+    if (ev_start) (void)hipEventDestroy(ev_start);
+    if (stream) (void)hipStreamDestroy(stream);
+    ev_start = nullptr;
+    stream = nullptr;
+  }
+};
+
+struct Bufs {
+  Grow arena, toks, perm, wave_key, sigw, dig, status, siglen, vpad, verdict, rows, pss, exc, exc_cnt;
+};
+
+// Host side of one staged chunk: the counting-sort layout.
+struct Plan {
+  int64_t ntok = 0, npad = 0;
+  ClassRange ranges[NCLS] = {};
+  int hash_mask[NCLS] = {};       // per class: bit 0 SHA-256 present, bit 1 SHA-384/512
+  int pss_any[NCLS] = {};         // per class: some token uses RSASSA-PSS (PS256/384/512)
+  int sig_rows = 1, scratch_rows = 1;
+  int64_t pss_tokens = 0;         // PSS scratch tokens: the RSA classes' ranges back to back
+  int64_t pss_off[NCLS] = {};
+};
+
+struct Ticket {
+  std::mutex m;
+  std::condition_variable cv;
+  size_t pending = 0;             // chunks not yet complete
+  int rc = 0;
+  std::string err;
+  void fail(int code, const std::string& e) {
+    std::lock_guard<std::mutex> g(m);
+    if (rc == 0) {
+      rc = code;
+      err = e;
+    }
+  }
+  void done_chunks(size_t k) {
+    std::lock_guard<std::mutex> g(m);
+    pending -= std::min(pending, k);
+    if (pending == 0) cv.notify_all();
+  }
+};
+
+// A pipeline slot: stream lane, device scratch, pinned host staging.
+struct Slot {
+  Lane lane;
+  Bufs bufs;
+  HGrow h_arena, h_toks, h_perm, h_wkey, h_verdict;
+  hipEvent_t done = nullptr;
+  hipEvent_t tr_a = nullptr, tr_b = nullptr, tr_c = nullptr;   // CAPJWT_PIPE_TRACE: H2D start / end, kernels end
+  double host_ms[3] = {};                                       // wait, plan, enqueue
+  int chunk_no = 0;
+  bool inflight = false;
+  std::shared_ptr<Ticket> ticket;
+  uint8_t* out = nullptr;
+  size_t n = 0;
+};
+
+struct Item {                     // one device's share of a submission
+  std::shared_ptr<Ticket> t;
+  const uint8_t* arena = nullptr;
+  size_t arena_len = 0;
+  const jg_tok* toks = nullptr;   // the caller's array, [lo, hi)
+  size_t lo = 0, hi = 0;
+  uint8_t* out = nullptr;         // the caller's verdicts (index space of toks)
+  uint64_t epoch = 0;
+  bool pinned = false;            // arena is page-locked (direct DMA)
+  size_t chunk = 0, nchunks = 0;
+};
+
 struct Device {
   int id = 0;
-  hipStream_t stream = nullptr;
+  Lane lane0;                     // resident batches, key loads, hashing
   uint32_t* gtab[NCLS] = {};
   uint32_t* btab = nullptr;
   std::shared_ptr<SharedTable> tab_ref[NCLS];   // keeps gtab / btab alive
-  // untimed runs with several classes: one stream per class so the classes'
-  // kernel chains overlap (a mixed batch's per-class ranges are each too small
-  // to fill 256 CUs alone); joined back into `stream` before the scatter
-  hipStream_t cstream[NCLS] = {};
-  hipEvent_t ev_start = nullptr, ev_done[NCLS] = {};
   // comb tables of the current key blob by key content (class, coordinates):
   // a reload (JWKS refresh) copies the tables of keys it already had instead
   // of rebuilding them (D2D copy ~0.2 ms vs ~80 ms per P-256 key)
@@ -132,12 +278,17 @@ struct Device {
   DevKey* dkeys = nullptr;
   uint32_t* dblob = nullptr;
   int32_t* didx = nullptr;
-  std::mutex mu;
-  std::unique_ptr<struct Bufs> sync_bufs;
-};
-
-struct Bufs {
-  Grow arena, toks, perm, wave_key, sigw, dig, status, siglen, vpad, verdict, rows, pss, exc, exc_cnt;
+  std::mutex mu;                  // device state + lane0 + slots
+  // streaming pipeline
+  Slot slots[NSLOT];
+  int next_slot = 0;
+  std::thread worker;
+  std::mutex qmu;
+  std::condition_variable qcv, idle_cv;
+  std::deque<Item> q;
+  bool stop = false, busy = false;
+  std::vector<uint8_t> tcls;      // worker scratch: class per job of a chunk
+  std::vector<int64_t> cnt, fill; // worker scratch: bucket counts / cursors
 };
 
 }  // namespace
@@ -145,16 +296,11 @@ struct Bufs {
 struct jg_batch {
   jg_ctx* ctx = nullptr;
   Device* dev = nullptr;
+  Lane* lane = nullptr;
   std::unique_ptr<Bufs> own;
   Bufs* b = nullptr;
-  int64_t ntok = 0, npad = 0;
+  Plan plan;
   size_t arena_len = 0;
-  int sig_rows = 0, scratch_rows = 0;
-  int64_t pss_tokens = 0;          // PSS scratch tokens: the RSA classes' ranges back to back
-  int64_t pss_off[NCLS] = {};
-  ClassRange ranges[NCLS] = {};
-  int hash_mask[NCLS] = {};       // per class: bit 0 SHA-256 present, bit 1 SHA-384/512
-  int pss_any[NCLS] = {};         // per class: some token uses RSASSA-PSS (PS256/384/512)
   uint64_t epoch = 0;
   bool timing = true;
   // timing marks of the most recent run: events are created once and
@@ -169,11 +315,19 @@ struct jg_batch {
   }
 };
 
+struct jg_ticket {
+  std::shared_ptr<Ticket> t;
+};
+
 struct jg_ctx {
   std::vector<std::unique_ptr<Device>> devs;
   std::vector<HostKey> keys;
+  std::vector<uint8_t> cls_tab;   // [key * NALG + alg] -> kernel class of the job
+  std::vector<int32_t> cls_keys[NCLS];   // keys of each class, in index order
+  bool failed = false;            // the last key load failed half-way: nothing verifies
+  std::atomic<size_t> chunk{chunk_jobs()};   // jobs per pipeline chunk
   uint64_t epoch = 0;
-  std::mutex key_mu;
+  std::shared_mutex key_mu;       // key table: exclusive in jg_keys_load, shared by submitters
   std::mutex err_mu;
   std::string err;
   void set_err(const std::string& s) {
@@ -217,22 +371,169 @@ int alg_family(int alg) {         // 1 RSA, 2 EC, 3 Ed, 0 none
   return 0;
 }
 
-int classify(const jg_ctx* ctx, const jg_tok& t) {
-  if (t.key_idx >= ctx->keys.size()) return -1;
-  const HostKey& k = ctx->keys[t.key_idx];
-  if (!k.valid || alg_family(t.alg) != k.kind) return CLS_REJECT;
-  return k.cls;
+// kernel class of a job (key_idx already range-checked)
+inline int classify(const jg_ctx* ctx, const jg_tok& t) {
+  return t.alg < NALG ? ctx->cls_tab[(size_t)t.key_idx * NALG + t.alg] : CLS_REJECT;
 }
 
+void rebuild_class_tables(jg_ctx* ctx) {
+  const size_t nk = ctx->keys.size();
+  ctx->cls_tab.assign(nk * NALG, (uint8_t)CLS_REJECT);
+  for (auto& v : ctx->cls_keys) v.clear();
+  for (size_t k = 0; k < nk; ++k) {
+    const HostKey& hk = ctx->keys[k];
+    if (hk.valid && hk.cls != CLS_REJECT) ctx->cls_keys[hk.cls].push_back((int32_t)k);
+    for (int a = 0; a < NALG; ++a)
+      if (hk.valid && alg_family(a) == hk.kind) ctx->cls_tab[k * NALG + a] = (uint8_t)hk.cls;
+  }
+}
+
+// Reject a job list that names a key outside the table or a byte span outside
+// the arena (the prep kernel reads the device copy at those offsets).
+bool check_jobs(const jg_ctx* ctx, size_t arena_len, const jg_tok* toks, size_t ntok, std::string* err) {
+  const size_t nk = ctx->keys.size();
+  for (size_t i = 0; i < ntok; ++i) {
+    const jg_tok& t = toks[i];
+    if (t.key_idx >= nk) {
+      *err = "jg_tok[" + std::to_string(i) + "].key_idx " + std::to_string(t.key_idx) +
+             " out of range of the loaded key table (" + std::to_string(nk) + " keys)";
+      return false;
+    }
+    if (t.off > arena_len || t.sig_in_len > arena_len - t.off ||
+        (uint64_t)t.sig_rel_off + t.sig_b64_len > arena_len - t.off) {
+      *err = "jg_tok[" + std::to_string(i) + "]: signing input or signature span past the arena (" +
+             std::to_string(arena_len) + " bytes)";
+      return false;
+    }
+  }
+  return true;
+}
+
+inline uint64_t tok_end(const jg_tok& t) {
+  return std::max<uint64_t>(t.off + t.sig_in_len, t.off + (uint64_t)t.sig_rel_off + t.sig_b64_len);
+}
+
+bool is_pinned(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();      // clear the sticky "invalid value" of pageable memory
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Counting sort of toks[0..ntok) by (class, key): classes 1..NCLS-1 key by key,
+// then the reject bucket; every bucket padded to whole waves.  `alloc(npad)`
+// returns (perm, wave_key) storage for npad / npad/WAVE entries.
+template <class Alloc>
+void make_plan(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, Plan& P, std::vector<uint8_t>& tcls,
+               std::vector<int64_t>& cnt, std::vector<int64_t>& fill, Alloc&& alloc) {
+  const size_t nk = ctx->keys.size();
+  const size_t RB = nk;                                  // reject bucket
+  cnt.assign(nk + 1, 0);
+  tcls.resize(ntok);
+  for (int c = 0; c < NCLS; ++c) P.hash_mask[c] = P.pss_any[c] = 0;
+  for (size_t i = 0; i < ntok; ++i) {
+    const jg_tok& t = toks[i];
+    const int c = classify(ctx, t);
+    tcls[i] = (uint8_t)c;
+    const int alg = t.alg;
+    P.hash_mask[c] |= (alg == JG_RS256 || alg == JG_PS256 || alg == JG_ES256) ? 1 : 2;
+    P.pss_any[c] |= alg >= JG_PS256 && alg <= JG_PS512;
+    cnt[c == CLS_REJECT ? RB : t.key_idx]++;
+  }
+  fill.assign(nk + 1, 0);
+  int64_t pos = 0;
+  for (int c = 1; c <= NCLS; ++c) {
+    const int cc = c % NCLS;
+    P.ranges[cc].begin = pos;
+    if (cc == CLS_REJECT) {
+      fill[RB] = pos;
+      pos += (cnt[RB] + WAVE - 1) / WAVE * WAVE;
+    } else {
+      for (int32_t k : ctx->cls_keys[cc]) {
+        fill[(size_t)k] = pos;
+        pos += (cnt[(size_t)k] + WAVE - 1) / WAVE * WAVE;
+      }
+    }
+    P.ranges[cc].end = pos;
+  }
+  P.npad = pos > 0 ? pos : WAVE;
+  P.ntok = (int64_t)ntok;
+  int32_t* perm;
+  int32_t* wkey;
+  alloc((size_t)P.npad, &perm, &wkey);
+  // padding lanes: the tail of each bucket's last wave
+  for (size_t b = 0; b <= nk; ++b) {
+    const int64_t e = fill[b] + cnt[b], pe = fill[b] + (cnt[b] + WAVE - 1) / WAVE * WAVE;
+    for (int64_t p = e; p < pe; ++p) perm[p] = -1;
+  }
+  if (pos == 0)
+    for (int64_t p = 0; p < WAVE; ++p) perm[p] = -1;
+  wkey[0] = 0;
+  for (size_t i = 0; i < ntok; ++i) {
+    const int c = tcls[i];
+    const size_t b = c == CLS_REJECT ? RB : toks[i].key_idx;
+    const int64_t p = fill[b]++;
+    perm[p] = (int32_t)i;
+    wkey[p / WAVE] = c == CLS_REJECT ? 0 : toks[i].key_idx;
+  }
+  P.sig_rows = 1;
+  P.scratch_rows = 1;
+  P.pss_tokens = 0;
+  for (int c = 1; c < NCLS; ++c) {
+    if (P.ranges[c].end <= P.ranges[c].begin) continue;
+    P.sig_rows = std::max(P.sig_rows, cls_rows_sig(c));
+    P.scratch_rows = std::max(P.scratch_rows, cls_rows_scratch(c));
+    if (c <= CLS_RSA4K) {
+      P.pss_off[c] = P.pss_tokens;
+      P.pss_tokens += P.ranges[c].end - P.ranges[c].begin;
+    }
+  }
+}
+
+// device scratch of a plan (inputs are copied by the caller)
+void size_bufs(Bufs* B, const Plan& P, size_t arena_bytes) {
+  const int64_t npad = P.npad;
+  const size_t ntok = std::max<size_t>((size_t)P.ntok, 1);
+  B->arena.get(arena_bytes + ARENA_SLACK);
+  B->toks.get(sizeof(jg_tok) * ntok);
+  B->perm.get(sizeof(int32_t) * npad);
+  B->wave_key.get(sizeof(int32_t) * (npad / WAVE));
+  B->sigw.get(sizeof(uint32_t) * P.sig_rows * npad);
+  B->dig.get(sizeof(uint32_t) * DIG_ROWS * npad);
+  B->status.get(npad);
+  B->siglen.get(sizeof(uint16_t) * npad);
+  B->vpad.get(npad);
+  B->verdict.get(ntok);
+  B->rows.get(sizeof(uint32_t) * (size_t)P.scratch_rows * npad);
+  B->pss.get((size_t)std::max<int64_t>(P.pss_tokens, 1) * 2048);
+  B->exc.get(sizeof(int32_t) * npad);
+  B->exc_cnt.get(sizeof(uint32_t) * NCLS);
+}
+
+void upload(Bufs* B, hipStream_t s, const Plan& P, const uint8_t* arena, size_t arena_bytes, const jg_tok* toks,
+            const int32_t* perm, const int32_t* wkey) {
+  size_bufs(B, P, arena_bytes);
+  uint8_t* da = (uint8_t*)B->arena.p;
+  if (arena_bytes && arena) HIPCHK(hipMemcpyAsync(da, arena, arena_bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(da + arena_bytes, 0, ARENA_SLACK, s));
+  if (P.ntok) HIPCHK(hipMemcpyAsync(B->toks.p, toks, sizeof(jg_tok) * P.ntok, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(B->perm.p, perm, sizeof(int32_t) * P.npad, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(B->wave_key.p, wkey, sizeof(int32_t) * (P.npad / WAVE), hipMemcpyHostToDevice, s));
+}
+
+// ---------------------------------------------------------------- timing marks
 void mark(jg_batch* b, const char* name) {
-  if (!b->timing) return;
+  if (!b || !b->timing) return;
   if (b->marks_used == b->mark_events.size()) {
     hipEvent_t e;
     HIPCHK(hipEventCreate(&e));
     b->mark_events.push_back(e);
     b->mark_names.emplace_back();
   }
-  HIPCHK(hipEventRecord(b->mark_events[b->marks_used], b->dev->stream));
+  HIPCHK(hipEventRecord(b->mark_events[b->marks_used], b->lane->stream));
   b->mark_names[b->marks_used] = name;
   ++b->marks_used;
 }
@@ -254,113 +555,26 @@ void mark_cb(void* p, const char* kname) {
 }
 
 Marker marker(jg_batch* b, int cls) {
-  g_mark_ctx = MarkCtx{b, cls};
   Marker mk;
+  if (!b || !b->timing) return mk;
+  g_mark_ctx = MarkCtx{b, cls};
   mk.ctx = &g_mark_ctx;
   mk.fn = mark_cb;
   return mk;
 }
 
-// Build the plan and upload everything for toks[0..ntok) (indices are the caller's).
-void stage(jg_ctx* ctx, jg_batch* b, const uint8_t* arena, size_t arena_len, const jg_tok* toks, size_t ntok) {
-  Device* d = b->dev;
-  HIPCHK(hipSetDevice(d->id));
-  const int nkeys = (int)ctx->keys.size();
-  const size_t nbuck = (size_t)NCLS * (nkeys > 0 ? nkeys : 1);
-  std::vector<int64_t> cnt(nbuck, 0);
-  std::vector<int> tcls(ntok);
-  for (int c = 0; c < NCLS; ++c) b->hash_mask[c] = b->pss_any[c] = 0;
-  for (size_t i = 0; i < ntok; ++i) {
-    const int c = classify(ctx, toks[i]);
-    if (c < 0) throw std::invalid_argument("jg_tok.key_idx out of range of the loaded key table");
-    tcls[i] = c;
-    const int alg = toks[i].alg;
-    b->hash_mask[c] |= (alg == JG_RS256 || alg == JG_PS256 || alg == JG_ES256) ? 1 : 2;
-    if (alg >= JG_PS256 && alg <= JG_PS512) b->pss_any[c] = 1;
-    cnt[(size_t)c * nkeys + (c == CLS_REJECT ? 0 : toks[i].key_idx)]++;
-  }
-  // bucket order: classes 1..NCLS-1 by key, then the reject bucket
-  std::vector<int64_t> off(nbuck, 0);
-  int64_t pos = 0;
-  for (int c = 1; c <= NCLS; ++c) {
-    const int cc = c % NCLS;
-    b->ranges[cc].begin = pos;
-    const int kmax = cc == CLS_REJECT ? 1 : nkeys;
-    for (int k = 0; k < kmax; ++k) {
-      const size_t i = (size_t)cc * nkeys + k;
-      off[i] = pos;
-      pos += (cnt[i] + WAVE - 1) / WAVE * WAVE;
-    }
-    b->ranges[cc].end = pos;
-  }
-  const int64_t npad = pos > 0 ? pos : WAVE;
-  b->npad = npad;
-  b->ntok = (int64_t)ntok;
-  std::vector<int32_t> perm((size_t)npad, -1);
-  std::vector<int32_t> wkey((size_t)(npad / WAVE), 0);
-  std::vector<int64_t> fill = off;
-  for (size_t i = 0; i < ntok; ++i) {
-    const int c = tcls[i];
-    const size_t bi = (size_t)c * nkeys + (c == CLS_REJECT ? 0 : toks[i].key_idx);
-    const int64_t p = fill[bi]++;
-    perm[(size_t)p] = (int32_t)i;
-    wkey[(size_t)(p / WAVE)] = c == CLS_REJECT ? 0 : toks[i].key_idx;
-  }
-  b->sig_rows = 1;
-  b->scratch_rows = 1;
-  b->pss_tokens = 0;
-  for (int c = 1; c < NCLS; ++c) {
-    if (b->ranges[c].end <= b->ranges[c].begin) continue;
-    b->sig_rows = std::max(b->sig_rows, cls_rows_sig(c));
-    b->scratch_rows = std::max(b->scratch_rows, cls_rows_scratch(c));
-    if (c <= CLS_RSA4K) {
-      b->pss_off[c] = b->pss_tokens;
-      b->pss_tokens += b->ranges[c].end - b->ranges[c].begin;
-    }
-  }
-  Bufs* B = b->b;
-  hipStream_t s = d->stream;
-  b->arena_len = arena_len;
-  uint8_t* da = (uint8_t*)B->arena.get(arena_len + ARENA_SLACK);
-  HIPCHK(hipMemcpyAsync(da, arena, arena_len, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemsetAsync(da + arena_len, 0, ARENA_SLACK, s));
-  HIPCHK(hipMemcpyAsync(B->toks.get(sizeof(jg_tok) * std::max<size_t>(ntok, 1)), toks, sizeof(jg_tok) * ntok,
-                        hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(B->perm.get(sizeof(int32_t) * npad), perm.data(), sizeof(int32_t) * npad,
-                        hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(B->wave_key.get(sizeof(int32_t) * wkey.size()), wkey.data(), sizeof(int32_t) * wkey.size(),
-                        hipMemcpyHostToDevice, s));
-  B->sigw.get(sizeof(uint32_t) * b->sig_rows * npad);
-  B->dig.get(sizeof(uint32_t) * DIG_ROWS * npad);
-  B->status.get(npad);
-  B->siglen.get(sizeof(uint16_t) * npad);
-  B->vpad.get(npad);
-  B->verdict.get(std::max<size_t>(ntok, 1));
-  B->rows.get(sizeof(uint32_t) * (size_t)b->scratch_rows * npad);
-  B->pss.get((size_t)std::max<int64_t>(b->pss_tokens, 1) * 2048);
-  B->exc.get(sizeof(int32_t) * npad);
-  B->exc_cnt.get(sizeof(uint32_t) * NCLS);
-  // the host vectors die here: the copies above must complete first
-  HIPCHK(hipStreamSynchronize(s));
-  b->epoch = ctx->epoch;
-}
-
-// timed: per-kernel HIP events (classes in sequence on the device stream);
-// untimed: classes on their own streams, overlapping.
-void run(jg_ctx* ctx, jg_batch* b, bool timed) {
-  Device* d = b->dev;
-  HIPCHK(hipSetDevice(d->id));
-  if (b->epoch != ctx->epoch) throw std::runtime_error("key table reloaded since this batch was staged");
-  Bufs* B = b->b;
-  hipStream_t s = d->stream;
-  b->timing = timed;
-  b->marks_used = 0;
+// Launch the verify kernels of a staged plan on lane L.  With `marks` (a
+// timed resident run) the classes run in sequence on L.stream with a HIP event
+// after each kernel; otherwise classes with work run on their own streams.
+void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
+  const bool timed = marks && marks->timing;
   int nact = 0;
-  for (int c = 1; c < NCLS; ++c) nact += b->ranges[c].end > b->ranges[c].begin;
+  for (int c = 1; c < NCLS; ++c) nact += P.ranges[c].end > P.ranges[c].begin;
   const bool conc = !timed && nact > 1;
-  const int64_t np = b->npad;
-  mark(b, "begin");
-  HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, s));
+  const int64_t np = P.npad;
+  const hipStream_t s0 = L->stream;
+  mark(marks, "begin");
+  HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, s0));
   PrepArgs pa{};
   pa.arena = (const uint8_t*)B->arena.p;
   pa.toks = (const jg_tok_dev*)B->toks.p;
@@ -374,36 +588,35 @@ void run(jg_ctx* ctx, jg_batch* b, bool timed) {
   pa.siglen = (uint16_t*)B->siglen.p;
   pa.npad = np;
   uint32_t* rows = (uint32_t*)B->rows.p;
-  if (conc) HIPCHK(hipEventRecord(d->ev_start, s));
-  const hipStream_t s0 = s;
+  if (conc) HIPCHK(hipEventRecord(L->ev_start, s0));
   for (int c = 1; c < NCLS; ++c) {
-    const ClassRange r = b->ranges[c];
+    const ClassRange r = P.ranges[c];
     if (r.end <= r.begin) continue;
     // every class reads and writes only columns [r.begin, r.end) of the shared
     // scratch rows, its own exception counter and its own PSS scratch
     hipStream_t s = s0;
     if (conc) {
-      s = d->cstream[c];
-      HIPCHK(hipStreamWaitEvent(s, d->ev_start, 0));
+      s = L->cstream[c];
+      HIPCHK(hipStreamWaitEvent(s, L->ev_start, 0));
     }
     pa.begin = r.begin;
     pa.end = r.end;
     pa.zrows = cls_rows_sig(c);
-    launch_prep(c, b->hash_mask[c], pa, s);
-    mark(b, (std::string(cls_name(c)) + "_prep").c_str());
+    launch_prep(c, P.hash_mask[c], pa, s);
+    mark(marks, (std::string(cls_name(c)) + "_prep").c_str());
     if (c <= CLS_RSA4K) {
       RsaArgs ra{};
       ra.toks = pa.toks; ra.perm = pa.perm; ra.wave_key = pa.wave_key; ra.keys = pa.keys; ra.keyblob = pa.keyblob;
       ra.sigw = pa.sigw; ra.dig = pa.dig;
-      const int L = rsa_limbs(c);
+      const int Lm = rsa_limbs(c);
       ra.xmw = rows;
-      ra.xlr = rows + (size_t)L * np;
-      ra.yw = rows + (size_t)2 * L * np;
+      ra.xlr = rows + (size_t)Lm * np;
+      ra.yw = rows + (size_t)2 * Lm * np;
       ra.status = pa.status; ra.siglen = pa.siglen; ra.verdict_pad = (uint8_t*)B->vpad.p;
-      ra.pss_scratch = (uint8_t*)B->pss.p + b->pss_off[c] * 2048;
-      ra.has_pss = b->pss_any[c];
+      ra.pss_scratch = (uint8_t*)B->pss.p + P.pss_off[c] * 2048;
+      ra.has_pss = P.pss_any[c];
       ra.npad = np; ra.begin = r.begin; ra.end = r.end;
-      launch_rsa(c, ra, s, marker(b, c));
+      launch_rsa(c, ra, s, marker(marks, c));
     } else if (c <= CLS_P521) {
       if (!d->gtab[c]) throw std::runtime_error("curve table missing");
       EcArgs ea{};
@@ -416,8 +629,9 @@ void run(jg_ctx* ctx, jg_batch* b, bool timed) {
       ea.exc_list = (int32_t*)B->exc.p + r.begin;
       ea.exc_count = (uint32_t*)B->exc_cnt.p + c;
       ea.npad = np; ea.begin = r.begin; ea.end = r.end;
-      launch_ec(c, ea, s, marker(b, c));
+      launch_ec(c, ea, s, marker(marks, c));
     } else {
+      if (!d->btab) throw std::runtime_error("Ed25519 base table missing");
       EdArgs ea{};
       ea.perm = pa.perm; ea.wave_key = pa.wave_key; ea.keys = pa.keys; ea.keyblob = pa.keyblob;
       ea.sigw = pa.sigw; ea.dig = pa.dig; ea.status = pa.status; ea.siglen = pa.siglen;
@@ -425,15 +639,15 @@ void run(jg_ctx* ctx, jg_batch* b, bool timed) {
       ea.xyz = rows;
       ea.btab = d->btab;
       ea.npad = np; ea.begin = r.begin; ea.end = r.end;
-      launch_ed(ea, s, marker(b, c));
+      launch_ed(ea, s, marker(marks, c));
     }
     if (conc) {
-      HIPCHK(hipEventRecord(d->ev_done[c], s));
-      HIPCHK(hipStreamWaitEvent(s0, d->ev_done[c], 0));
+      HIPCHK(hipEventRecord(L->ev_done[c], s));
+      HIPCHK(hipStreamWaitEvent(s0, L->ev_done[c], 0));
     }
   }
-  launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s);
-  mark(b, "scatter");
+  launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s0);
+  mark(marks, "scatter");
   HIPCHK(hipGetLastError());
 }
 
@@ -447,6 +661,180 @@ void collect_times(jg_batch* b) {
       b->tms.push_back(ms);
     }
   }
+}
+
+// ---------------------------------------------------------------- streaming pipeline
+// Complete the chunk held by slot S (its verdicts were copied to pinned
+// staging): hand the verdicts to the caller and count the chunk off its ticket.
+void finish_slot(Slot& S) {
+  if (!S.inflight) return;
+  const hipError_t e = hipEventSynchronize(S.done);
+  if (e != hipSuccess) S.ticket->fail(-2, std::string("verify chunk: ") + hipGetErrorString(e));
+  else if (S.n) std::memcpy(S.out, S.h_verdict.p, S.n);
+  if (pipe_trace() && e == hipSuccess && g_trace_ref) {
+    float a = 0, b = 0, c = 0, dn = 0;
+    (void)hipEventElapsedTime(&a, g_trace_ref, S.tr_a);
+    (void)hipEventElapsedTime(&b, g_trace_ref, S.tr_b);
+    (void)hipEventElapsedTime(&c, g_trace_ref, S.tr_c);
+    (void)hipEventElapsedTime(&dn, g_trace_ref, S.done);
+    std::fprintf(stderr, "[pipe] chunk %3d n=%7zu host wait %.3f plan %.3f enq %.3f | gpu h2d %.3f-%.3f kern-end %.3f done %.3f ms\n",
+                 S.chunk_no, S.n, S.host_ms[0], S.host_ms[1], S.host_ms[2], a, b, c, dn);
+  }
+  S.inflight = false;
+  auto t = std::move(S.ticket);
+  S.ticket.reset();
+  t->done_chunks(1);
+}
+
+bool slot_ready(Slot& S) {
+  if (!S.inflight) return true;
+  const hipError_t e = hipEventQuery(S.done);
+  if (e == hipErrorNotReady) return false;
+  if (e != hipSuccess) (void)hipGetLastError();
+  return true;
+}
+
+// Plan and enqueue one chunk toks[0..n) of an item on slot S.
+void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok* toks, size_t n, uint8_t* out) {
+  const auto t_start = std::chrono::steady_clock::now();
+  // arena span of the chunk's jobs; DMA it straight from a pinned caller
+  // arena when it is compact, else repack the jobs' bytes into pinned staging
+  uint64_t amin = UINT64_MAX, amax = 0, need = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t e = tok_end(toks[i]);
+    amin = std::min<uint64_t>(amin, toks[i].off);
+    amax = std::max<uint64_t>(amax, e);
+    need += e - toks[i].off;
+  }
+  if (n == 0) amin = amax = 0;
+  const uint64_t base = amin & ~uint64_t(255);
+  const uint64_t span = amax - base;
+  const bool compact = span <= 2 * need + 65536;
+  jg_tok* jt = (jg_tok*)S.h_toks.get(sizeof(jg_tok) * std::max<size_t>(n, 1));
+  const uint8_t* src;
+  size_t bytes;
+  if (compact) {
+    for (size_t i = 0; i < n; ++i) {
+      jt[i] = toks[i];
+      jt[i].off -= base;
+    }
+    bytes = (size_t)span;
+    if (it.pinned) {
+      src = it.arena + base;
+    } else {
+      uint8_t* h = (uint8_t*)S.h_arena.get(bytes);
+      std::memcpy(h, it.arena + base, bytes);
+      src = h;
+    }
+  } else {
+    uint8_t* h = (uint8_t*)S.h_arena.get((size_t)need + 4 * n);
+    uint64_t pos = 0;
+    for (size_t i = 0; i < n; ++i) {
+      const uint64_t len = tok_end(toks[i]) - toks[i].off;
+      std::memcpy(h + pos, it.arena + toks[i].off, len);
+      jt[i] = toks[i];
+      jt[i].off = pos;
+      pos += (len + 3) & ~uint64_t(3);
+    }
+    bytes = (size_t)pos;
+    src = h;
+  }
+  Plan P;
+  make_plan(ctx, jt, n, P, d->tcls, d->cnt, d->fill, [&](size_t npad, int32_t** perm, int32_t** wkey) {
+    *perm = (int32_t*)S.h_perm.get(sizeof(int32_t) * npad);
+    *wkey = (int32_t*)S.h_wkey.get(sizeof(int32_t) * (npad / WAVE));
+  });
+  const hipStream_t s = S.lane.stream;
+  const bool tr = pipe_trace();
+  S.host_ms[1] = tr ? ms_since(t_start) : 0.0;
+  const auto t_enq = std::chrono::steady_clock::now();
+  if (tr) HIPCHK(hipEventRecord(S.tr_a, s));
+  upload(&S.bufs, s, P, src, bytes, jt, (const int32_t*)S.h_perm.p, (const int32_t*)S.h_wkey.p);
+  if (tr) HIPCHK(hipEventRecord(S.tr_b, s));
+  run_plan(d, &S.lane, &S.bufs, P, nullptr);
+  if (tr) HIPCHK(hipEventRecord(S.tr_c, s));
+  uint8_t* hv = (uint8_t*)S.h_verdict.get(std::max<size_t>(n, 1));
+  if (n) HIPCHK(hipMemcpyAsync(hv, S.bufs.verdict.p, n, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipEventRecord(S.done, s));
+  if (tr) S.host_ms[2] = ms_since(t_enq);
+  S.ticket = it.t;
+  S.out = out;
+  S.n = n;
+  S.inflight = true;
+}
+
+void process_item(jg_ctx* ctx, Device* d, Item& it) {
+  size_t enq = 0;
+  try {
+    std::lock_guard<std::mutex> g(d->mu);
+    HIPCHK(hipSetDevice(d->id));
+    if (ctx->failed || ctx->epoch != it.epoch)
+      throw std::runtime_error("key table reloaded (or its load failed) while the batch was queued");
+    const size_t C = it.chunk;
+    if (pipe_trace()) {
+      if (!g_trace_ref) HIPCHK(hipEventCreate(&g_trace_ref));
+      HIPCHK(hipEventRecord(g_trace_ref, d->slots[d->next_slot].lane.stream));
+    }
+    for (size_t lo = it.lo; lo < it.hi; lo += C) {
+      const size_t hi = std::min(it.hi, lo + C);
+      Slot& S = d->slots[d->next_slot];
+      d->next_slot = (d->next_slot + 1) % NSLOT;
+      const auto tw = std::chrono::steady_clock::now();
+      finish_slot(S);                 // the slot's previous chunk (NSLOT chunks ago)
+      const double wait_ms = pipe_trace() ? ms_since(tw) : 0.0;
+      enqueue_chunk(ctx, d, S, it, it.toks + lo, hi - lo, it.out + lo);
+      S.host_ms[0] = wait_ms;
+      S.chunk_no = (int)enq;
+      ++enq;
+    }
+  } catch (const std::exception& e) {
+    it.t->fail(-2, e.what());
+    it.t->done_chunks(it.nchunks - enq);
+  }
+}
+
+void worker_loop(jg_ctx* ctx, Device* d) {
+  (void)hipSetDevice(d->id);
+  std::unique_lock<std::mutex> lk(d->qmu);
+  while (true) {
+    if (!d->q.empty()) {
+      Item it = std::move(d->q.front());
+      d->q.pop_front();
+      d->busy = true;
+      lk.unlock();
+      process_item(ctx, d, it);
+      lk.lock();
+      continue;
+    }
+    // queue empty: complete finished chunks, wait for in-flight ones (or new work)
+    bool any = false;
+    lk.unlock();
+    {
+      std::lock_guard<std::mutex> g(d->mu);
+      for (int k = 0; k < NSLOT; ++k) {
+        Slot& S = d->slots[(d->next_slot + k) % NSLOT];    // oldest first
+        if (!S.inflight) continue;
+        if (slot_ready(S)) finish_slot(S);
+        else any = true;
+      }
+    }
+    lk.lock();
+    if (any) {
+      d->qcv.wait_for(lk, std::chrono::microseconds(50));
+      continue;
+    }
+    if (d->q.empty()) {
+      d->busy = false;
+      d->idle_cv.notify_all();
+      if (d->stop) break;
+      d->qcv.wait(lk, [&] { return d->stop || !d->q.empty(); });
+    }
+  }
+}
+
+void wait_idle(Device* d) {
+  std::unique_lock<std::mutex> lk(d->qmu);
+  d->idle_cv.wait(lk, [&] { return d->q.empty() && !d->busy; });
 }
 
 // ---------------------------------------------------------------- keys
@@ -473,13 +861,16 @@ uint64_t blob_alloc(std::vector<uint32_t>& blob, size_t words) {
   return off;
 }
 
-void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
-  ctx->keys.assign((size_t)nkeys, HostKey{});
+// Host part of a key load.  Touches no context state (the caller commits `hk`
+// only after every device has loaded the new table); `warn` collects
+// informational messages for jg_last_error.
+void build_keys(const jg_key* keys, int nkeys, StagedKeys& S, std::vector<HostKey>& hks, std::string* warn) {
+  hks.assign((size_t)nkeys, HostKey{});
   S.dk.assign((size_t)nkeys, DevKey{});
   S.tab_id.assign((size_t)nkeys, std::string());
   for (int i = 0; i < nkeys; ++i) {
     const jg_key& k = keys[i];
-    HostKey& hk = ctx->keys[i];
+    HostKey& hk = hks[i];
     DevKey& K = S.dk[i];
     hk.kind = K.kind = k.kind;
     K.cls = CLS_REJECT;
@@ -494,8 +885,8 @@ void build_keys(jg_ctx* ctx, const jg_key* keys, int nkeys, StagedKeys& S) {
       int cls = bits <= rsa_limbs(CLS_RSA2K) * 28 - 2 ? CLS_RSA2K : bits <= 112 * 28 - 2 ? CLS_RSA3K : bits <= 148 * 28 - 2 ? CLS_RSA4K : -1;
       if (cls < 0) {
         ok = false;
-        ctx->set_err("RSA key " + std::to_string(i) + " has " + std::to_string(bits) +
-                     " bits; the GPU path supports up to 4142-bit moduli (key marked unusable)");
+        *warn = "RSA key " + std::to_string(i) + " has " + std::to_string(bits) +
+                " bits; the GPU path supports up to 4142-bit moduli (key marked unusable)";
         cls = CLS_RSA4K;
       }
       const int L = rsa_limbs(cls);
@@ -576,7 +967,7 @@ std::shared_ptr<SharedTable> shared_table(Device* d, int cls, size_t bytes, Buil
   HIPCHK(hipMalloc(&t->p, bytes));
   build(t->p);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(d->stream));
+  HIPCHK(hipStreamSynchronize(d->lane0.stream));
   g_tabs[key] = t;
   return t;
 }
@@ -586,20 +977,21 @@ void ensure_tables(Device* d, const StagedKeys& S) {
   for (int c = CLS_P256; c <= CLS_P521; ++c) {
     if (S.ec_idx[c].empty() || d->gtab[c]) continue;
     d->tab_ref[c] = shared_table(d, c, sizeof(uint32_t) * ec_table_words(c, true),
-                                 [&](uint32_t* t) { launch_ec_gtable(c, t, d->stream); });
+                                 [&](uint32_t* t) { launch_ec_gtable(c, t, d->lane0.stream); });
     d->gtab[c] = d->tab_ref[c]->p;
   }
   if (!S.ed_idx.empty() && !d->btab) {
     d->tab_ref[CLS_ED25519] = shared_table(d, CLS_ED25519, sizeof(uint32_t) * ed_table_words(true),
-                                           [&](uint32_t* t) { launch_ed_btable(t, d->stream); });
+                                           [&](uint32_t* t) { launch_ed_btable(t, d->lane0.stream); });
     d->btab = d->tab_ref[CLS_ED25519]->p;
   }
 }
 
 void load_keys_device(Device* d, const StagedKeys& S) {
   HIPCHK(hipSetDevice(d->id));
-  hipStream_t s = d->stream;
-  HIPCHK(hipStreamSynchronize(s));
+  hipStream_t s = d->lane0.stream;
+  d->lane0.sync();
+  for (auto& sl : d->slots) sl.lane.sync();
   if (d->dkeys) (void)hipFree(d->dkeys);
   if (d->didx) (void)hipFree(d->didx);
   d->dkeys = nullptr; d->didx = nullptr;
@@ -607,55 +999,119 @@ void load_keys_device(Device* d, const StagedKeys& S) {
   auto old_cache = std::move(d->tab_cache);
   d->tab_cache.clear();
   d->dblob = nullptr;
-  const size_t nk = std::max<size_t>(S.dk.size(), 1);
-  HIPCHK(hipMalloc(&d->dkeys, sizeof(DevKey) * nk));
-  HIPCHK(hipMalloc(&d->dblob, sizeof(uint32_t) * std::max<uint64_t>(S.blob.size() + S.tab_words, 4)));
-  if (!S.dk.empty()) HIPCHK(hipMemcpyAsync(d->dkeys, S.dk.data(), sizeof(DevKey) * S.dk.size(), hipMemcpyHostToDevice, s));
-  if (!S.blob.empty())
-    HIPCHK(hipMemcpyAsync(d->dblob, S.blob.data(), sizeof(uint32_t) * S.blob.size(), hipMemcpyHostToDevice, s));
-  // per table class: keys to stage (all) and keys whose tables must be built
-  // (the rest are copied from the previous blob, same key content)
-  auto split = [&](const std::vector<int32_t>& keys, uint64_t words, std::vector<int32_t>& build) {
-    for (int32_t i : keys) {
-      const std::string& id = S.tab_id[(size_t)i];
-      const uint64_t off = S.dk[(size_t)i].tab_off;
-      auto it = id.empty() ? old_cache.end() : old_cache.find(id);
-      if (old_blob && it != old_cache.end() && it->second.second == words) {
-        HIPCHK(hipMemcpyAsync(d->dblob + off, old_blob + it->second.first, sizeof(uint32_t) * words,
-                              hipMemcpyDeviceToDevice, s));
-      } else {
-        build.push_back(i);
+  try {
+    const size_t nk = std::max<size_t>(S.dk.size(), 1);
+    HIPCHK(hipMalloc(&d->dkeys, sizeof(DevKey) * nk));
+    HIPCHK(hipMalloc(&d->dblob, sizeof(uint32_t) * std::max<uint64_t>(S.blob.size() + S.tab_words, 4)));
+    if (!S.dk.empty()) HIPCHK(hipMemcpyAsync(d->dkeys, S.dk.data(), sizeof(DevKey) * S.dk.size(), hipMemcpyHostToDevice, s));
+    if (!S.blob.empty())
+      HIPCHK(hipMemcpyAsync(d->dblob, S.blob.data(), sizeof(uint32_t) * S.blob.size(), hipMemcpyHostToDevice, s));
+    // per table class: keys to stage (all) and keys whose tables must be built
+    // (the rest are copied from the previous blob, same key content)
+    auto split = [&](const std::vector<int32_t>& keys, uint64_t words, std::vector<int32_t>& build) {
+      for (int32_t i : keys) {
+        const std::string& id = S.tab_id[(size_t)i];
+        const uint64_t off = S.dk[(size_t)i].tab_off;
+        auto it = id.empty() ? old_cache.end() : old_cache.find(id);
+        if (old_blob && it != old_cache.end() && it->second.second == words) {
+          HIPCHK(hipMemcpyAsync(d->dblob + off, old_blob + it->second.first, sizeof(uint32_t) * words,
+                                hipMemcpyDeviceToDevice, s));
+        } else {
+          build.push_back(i);
+        }
+        if (!id.empty()) d->tab_cache[id] = {off, words};
       }
-      if (!id.empty()) d->tab_cache[id] = {off, words};
-    }
-  };
-  std::vector<int32_t> build_ec[NCLS], build_ed;
-  for (int c = CLS_P256; c <= CLS_P521; ++c) split(S.ec_idx[c], (uint64_t)ec_table_words(c, false), build_ec[c]);
-  split(S.ed_idx, (uint64_t)ed_table_words(false), build_ed);
-  // one index array: rsa | p256 | p384 | p521 | ed | builds p256 | p384 | p521 | ed
-  std::vector<int32_t> idx;
-  std::vector<size_t> at;
-  auto push = [&](const std::vector<int32_t>& v) { at.push_back(idx.size()); idx.insert(idx.end(), v.begin(), v.end()); };
-  push(S.rsa_idx);
-  for (int c = CLS_P256; c <= CLS_P521; ++c) push(S.ec_idx[c]);
-  push(S.ed_idx);
-  for (int c = CLS_P256; c <= CLS_P521; ++c) push(build_ec[c]);
-  push(build_ed);
-  HIPCHK(hipMalloc(&d->didx, sizeof(int32_t) * std::max<size_t>(idx.size(), 1)));
-  if (!idx.empty()) HIPCHK(hipMemcpyAsync(d->didx, idx.data(), sizeof(int32_t) * idx.size(), hipMemcpyHostToDevice, s));
-  ensure_tables(d, S);
-  if (!S.dk.empty()) launch_rsa_keyprep(d->dkeys, d->dblob, (int)S.dk.size(), s);
-  for (int c = CLS_P256; c <= CLS_P521; ++c)
-    launch_ec_keyprep(c, d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(),
-                      d->didx + at[5 + c - CLS_P256], (int)build_ec[c].size(), s);
-  launch_ed_keyprep(d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), d->didx + at[8],
-                    (int)build_ed.size(), s);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));
+    };
+    std::vector<int32_t> build_ec[NCLS], build_ed;
+    for (int c = CLS_P256; c <= CLS_P521; ++c) split(S.ec_idx[c], (uint64_t)ec_table_words(c, false), build_ec[c]);
+    split(S.ed_idx, (uint64_t)ed_table_words(false), build_ed);
+    // one index array: rsa | p256 | p384 | p521 | ed | builds p256 | p384 | p521 | ed
+    std::vector<int32_t> idx;
+    std::vector<size_t> at;
+    auto push = [&](const std::vector<int32_t>& v) { at.push_back(idx.size()); idx.insert(idx.end(), v.begin(), v.end()); };
+    push(S.rsa_idx);
+    for (int c = CLS_P256; c <= CLS_P521; ++c) push(S.ec_idx[c]);
+    push(S.ed_idx);
+    for (int c = CLS_P256; c <= CLS_P521; ++c) push(build_ec[c]);
+    push(build_ed);
+    HIPCHK(hipMalloc(&d->didx, sizeof(int32_t) * std::max<size_t>(idx.size(), 1)));
+    if (!idx.empty()) HIPCHK(hipMemcpyAsync(d->didx, idx.data(), sizeof(int32_t) * idx.size(), hipMemcpyHostToDevice, s));
+    ensure_tables(d, S);
+    if (!S.dk.empty()) launch_rsa_keyprep(d->dkeys, d->dblob, (int)S.dk.size(), s);
+    for (int c = CLS_P256; c <= CLS_P521; ++c)
+      launch_ec_keyprep(c, d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(),
+                        d->didx + at[5 + c - CLS_P256], (int)build_ec[c].size(), s);
+    launch_ed_keyprep(d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), d->didx + at[8],
+                      (int)build_ed.size(), s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+  } catch (...) {
+    (void)hipStreamSynchronize(s);
+    if (old_blob) (void)hipFree(old_blob);
+    d->tab_cache.clear();
+    throw;
+  }
   if (old_blob) (void)hipFree(old_blob);
 }
 
 thread_local std::string g_tls_err;
+
+// Split jobs [0, ntok) over the context's devices by the cost model and queue
+// each device's share.  Caller holds key_mu (shared) and has validated the jobs.
+std::shared_ptr<Ticket> submit_locked(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok* toks,
+                                      size_t ntok, uint8_t* out) {
+  auto t = std::make_shared<Ticket>();
+  const size_t nd = ctx->devs.size();
+  std::vector<size_t> cut(nd + 1, 0);
+  cut[nd] = ntok;
+  if (nd > 1) {
+    std::vector<double> pre(ntok + 1, 0.0);
+    for (size_t i = 0; i < ntok; ++i) pre[i + 1] = pre[i] + cls_cost(classify(ctx, toks[i]));
+    size_t j = 0;
+    for (size_t k = 1; k < nd; ++k) {
+      const double target = pre[ntok] * (double)k / (double)nd;
+      while (j < ntok && pre[j] < target) ++j;
+      cut[k] = j;
+    }
+  }
+  const bool pinned = is_pinned(arena);
+  const size_t C = ctx->chunk.load();
+  std::vector<Item> items;
+  for (size_t k = 0; k < nd; ++k) {
+    if (cut[k + 1] <= cut[k]) continue;
+    Item it;
+    it.t = t;
+    it.arena = arena;
+    it.arena_len = arena_len;
+    it.toks = toks;
+    it.lo = cut[k];
+    it.hi = cut[k + 1];
+    it.out = out;
+    it.epoch = ctx->epoch;
+    it.pinned = pinned;
+    it.chunk = C;
+    it.nchunks = (it.hi - it.lo + C - 1) / C;
+    t->pending += it.nchunks;
+    items.push_back(std::move(it));
+  }
+  for (size_t k = 0, i = 0; k < nd && i < items.size(); ++k) {
+    if (cut[k + 1] <= cut[k]) continue;
+    Device* d = ctx->devs[k].get();
+    {
+      std::lock_guard<std::mutex> g(d->qmu);
+      d->q.push_back(std::move(items[i++]));
+    }
+    d->qcv.notify_one();
+  }
+  return t;
+}
+
+int wait_ticket(jg_ctx* ctx, const std::shared_ptr<Ticket>& t) {
+  std::unique_lock<std::mutex> lk(t->m);
+  t->cv.wait(lk, [&] { return t->pending == 0; });
+  if (t->rc) ctx->set_err(t->err);
+  return t->rc;
+}
 
 }  // namespace
 
@@ -676,16 +1132,19 @@ jg_ctx* jg_create(const int* devices, int ndev) {
       auto d = std::make_unique<Device>();
       d->id = id;
       HIPCHK(hipSetDevice(id));
-      HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-      for (int c = 1; c < NCLS; ++c) {
-        HIPCHK(hipStreamCreateWithFlags(&d->cstream[c], hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&d->ev_done[c], hipEventDisableTiming));
+      d->lane0.create();
+      for (auto& s : d->slots) {
+        s.lane.create();
+        HIPCHK(hipEventCreateWithFlags(&s.done, pipe_trace() ? hipEventDefault : hipEventDisableTiming));
+        HIPCHK(hipEventCreate(&s.tr_a));
+        HIPCHK(hipEventCreate(&s.tr_b));
+        HIPCHK(hipEventCreate(&s.tr_c));
       }
-      HIPCHK(hipEventCreateWithFlags(&d->ev_start, hipEventDisableTiming));
-      d->sync_bufs = std::make_unique<Bufs>();
       ctx->devs.push_back(std::move(d));
     }
-    return ctx.release();
+    jg_ctx* c = ctx.release();
+    for (auto& d : c->devs) d->worker = std::thread(worker_loop, c, d.get());
+    return c;
   } catch (const std::exception& e) {
     g_tls_err = e.what();
     return nullptr;
@@ -695,20 +1154,27 @@ jg_ctx* jg_create(const int* devices, int ndev) {
 void jg_destroy(jg_ctx* ctx) {
   if (!ctx) return;
   for (auto& d : ctx->devs) {
+    {
+      std::lock_guard<std::mutex> g(d->qmu);
+      d->stop = true;
+    }
+    d->qcv.notify_all();
+    if (d->worker.joinable()) d->worker.join();
+  }
+  for (auto& d : ctx->devs) {
     (void)hipSetDevice(d->id);
-    (void)hipStreamSynchronize(d->stream);
-    d->sync_bufs.reset();
+    for (auto& s : d->slots) {
+      s.lane.destroy();
+      if (s.done) (void)hipEventDestroy(s.done);
+      for (hipEvent_t e : {s.tr_a, s.tr_b, s.tr_c})
+        if (e) (void)hipEventDestroy(e);
+    }
+    d->lane0.sync();
     for (auto& t : d->tab_ref) t.reset();         // shared fixed-base tables: last holder frees
     if (d->dkeys) (void)hipFree(d->dkeys);
     if (d->dblob) (void)hipFree(d->dblob);
     if (d->didx) (void)hipFree(d->didx);
-    for (int c = 1; c < NCLS; ++c) {
-      if (d->cstream[c]) (void)hipStreamSynchronize(d->cstream[c]);
-      if (d->cstream[c]) (void)hipStreamDestroy(d->cstream[c]);
-      if (d->ev_done[c]) (void)hipEventDestroy(d->ev_done[c]);
-    }
-    if (d->ev_start) (void)hipEventDestroy(d->ev_start);
-    (void)hipStreamDestroy(d->stream);
+    d->lane0.destroy();
   }
   delete ctx;
 }
@@ -717,31 +1183,87 @@ int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys) {
   if (!ctx || nkeys < 0 || (nkeys > 0 && !keys)) return -1;
   if (nkeys > 65535) { ctx->set_err("at most 65535 keys"); return -1; }
   try {
-    std::lock_guard<std::mutex> g(ctx->key_mu);
-    for (auto& d : ctx->devs) d->mu.lock();
+    std::unique_lock<std::shared_mutex> kl(ctx->key_mu);    // no new submissions
+    for (auto& d : ctx->devs) wait_idle(d.get());            // queued work runs against the old table
+    std::vector<std::unique_lock<std::mutex>> dl;
+    for (auto& d : ctx->devs) dl.emplace_back(d->mu);
     StagedKeys S;
-    build_keys(ctx, keys, nkeys, S);
+    std::vector<HostKey> hk;
+    std::string warn;
+    build_keys(keys, nkeys, S, hk, &warn);                  // throws before any device state changes
     try {
       for (auto& d : ctx->devs) load_keys_device(d.get(), S);
+      // device-side validity (on-curve, Ed25519 decoding) back into the host view
+      Device* d0 = ctx->devs[0].get();
+      std::vector<DevKey> back(S.dk.size());
+      if (!back.empty()) {
+        HIPCHK(hipSetDevice(d0->id));
+        HIPCHK(hipMemcpy(back.data(), d0->dkeys, sizeof(DevKey) * back.size(), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < back.size(); ++i) hk[i].valid = hk[i].valid && back[i].valid;
+      }
     } catch (...) {
-      for (auto& d : ctx->devs) d->mu.unlock();
+      // some device may hold part of the new table: nothing verifies until a
+      // load succeeds, and batches staged before now are stale
+      ctx->keys.clear();
+      rebuild_class_tables(ctx);
+      ctx->failed = true;
+      ++ctx->epoch;
       throw;
     }
-    // device-side validity (on-curve, Ed25519 decoding) back into the host view
-    Device* d0 = ctx->devs[0].get();
-    std::vector<DevKey> back(S.dk.size());
-    if (!back.empty()) {
-      HIPCHK(hipSetDevice(d0->id));
-      HIPCHK(hipMemcpy(back.data(), d0->dkeys, sizeof(DevKey) * back.size(), hipMemcpyDeviceToHost));
-      for (size_t i = 0; i < back.size(); ++i) ctx->keys[i].valid = ctx->keys[i].valid && back[i].valid;
-    }
+    ctx->keys = std::move(hk);
+    rebuild_class_tables(ctx);
+    ctx->failed = false;
     ++ctx->epoch;
-    for (auto& d : ctx->devs) d->mu.unlock();
+    if (!warn.empty()) ctx->set_err(warn);
     return 0;
   } catch (const std::exception& e) {
     ctx->set_err(e.what());
     return -2;
   }
+}
+
+int jg_submit(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok* toks, size_t ntok,
+              uint8_t* verdict_out, jg_ticket** out) {
+  if (!ctx || !out || (ntok > 0 && (!toks || !arena || !verdict_out))) return -1;
+  *out = nullptr;
+  if (ntok > (size_t)INT32_MAX / 2) { ctx->set_err("batch too large"); return -1; }
+  try {
+    if (ntok == 0) {                       // nothing to verify
+      *out = new jg_ticket{std::make_shared<Ticket>()};
+      return 0;
+    }
+    std::shared_lock<std::shared_mutex> kl(ctx->key_mu);
+    if (ctx->failed) { ctx->set_err("the last jg_keys_load failed; no key table is loaded"); return -2; }
+    std::string err;
+    if (!check_jobs(ctx, arena_len, toks, ntok, &err)) { ctx->set_err(err); return -1; }
+    auto t = submit_locked(ctx, arena, arena_len, toks, ntok, verdict_out);
+    *out = new jg_ticket{std::move(t)};
+    return 0;
+  } catch (const std::exception& e) {
+    ctx->set_err(e.what());
+    return -2;
+  }
+}
+
+int jg_wait(jg_ctx* ctx, jg_ticket* t) {
+  if (!ctx || !t) return -1;
+  const int rc = wait_ticket(ctx, t->t);
+  delete t;
+  return rc;
+}
+
+int jg_set_chunk(jg_ctx* ctx, size_t jobs) {
+  if (!ctx || jobs < 64) return -1;
+  ctx->chunk.store(jobs);
+  return 0;
+}
+
+int jg_verify_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
+                    const jg_tok* toks, size_t ntok, uint8_t* verdict_out) {
+  jg_ticket* t = nullptr;
+  const int rc = jg_submit(ctx, arena, arena_len, toks, ntok, verdict_out, &t);
+  if (rc != 0) return rc;
+  return jg_wait(ctx, t);
 }
 
 int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t arena_len,
@@ -750,33 +1272,60 @@ int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t ar
   if (device_slot < 0 || device_slot >= (int)ctx->devs.size()) return -1;
   if (ntok > (size_t)INT32_MAX / 2) { ctx->set_err("batch too large"); return -1; }
   try {
+    std::shared_lock<std::shared_mutex> kl(ctx->key_mu);
+    if (ctx->failed) { ctx->set_err("the last jg_keys_load failed; no key table is loaded"); return -2; }
+    std::string err;
+    if (!check_jobs(ctx, arena_len, toks, ntok, &err)) { ctx->set_err(err); return -1; }
     auto b = std::make_unique<jg_batch>();
     b->ctx = ctx;
     b->dev = ctx->devs[device_slot].get();
+    b->lane = &b->dev->lane0;
     b->own = std::make_unique<Bufs>();
     b->b = b->own.get();
     std::lock_guard<std::mutex> g(b->dev->mu);
-    stage(ctx, b.get(), arena, arena_len, toks, ntok);
+    HIPCHK(hipSetDevice(b->dev->id));
+    std::vector<uint8_t> tcls;
+    std::vector<int64_t> cnt, fill;
+    std::vector<int32_t> perm, wkey;
+    make_plan(ctx, toks, ntok, b->plan, tcls, cnt, fill, [&](size_t npad, int32_t** p, int32_t** w) {
+      perm.resize(npad);
+      wkey.resize(npad / WAVE);
+      *p = perm.data();
+      *w = wkey.data();
+    });
+    upload(b->b, b->lane->stream, b->plan, arena, arena_len, toks, perm.data(), wkey.data());
+    // the host vectors die here: the copies above must complete first
+    HIPCHK(hipStreamSynchronize(b->lane->stream));
+    b->arena_len = arena_len;
+    b->epoch = ctx->epoch;
     *out = b.release();
     return 0;
-  } catch (const std::invalid_argument& e) {
-    ctx->set_err(e.what());
-    return -1;
   } catch (const std::exception& e) {
     ctx->set_err(e.what());
     return -2;
   }
 }
 
+namespace {
+void run_resident(jg_ctx* ctx, jg_batch* b, bool timed) {
+  HIPCHK(hipSetDevice(b->dev->id));
+  if (b->epoch != ctx->epoch) throw std::runtime_error("key table reloaded since this batch was staged");
+  b->timing = timed;
+  b->marks_used = 0;
+  run_plan(b->dev, b->lane, b->b, b->plan, b);
+}
+}  // namespace
+
 int jg_batch_run(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out) {
   if (!ctx || !b) return -1;
   try {
     std::lock_guard<std::mutex> g(b->dev->mu);
-    run(ctx, b, true);
+    run_resident(ctx, b, true);
     if (verdict_out) {
-      if (b->ntok > 0)
-        HIPCHK(hipMemcpyAsync(verdict_out, b->b->verdict.p, (size_t)b->ntok, hipMemcpyDeviceToHost, b->dev->stream));
-      HIPCHK(hipStreamSynchronize(b->dev->stream));
+      if (b->plan.ntok > 0)
+        HIPCHK(hipMemcpyAsync(verdict_out, b->b->verdict.p, (size_t)b->plan.ntok, hipMemcpyDeviceToHost,
+                              b->lane->stream));
+      HIPCHK(hipStreamSynchronize(b->lane->stream));
       collect_times(b);
     }
     return 0;
@@ -790,9 +1339,10 @@ int jg_batch_enqueue(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out) {
   if (!ctx || !b) return -1;
   try {
     std::lock_guard<std::mutex> g(b->dev->mu);
-    run(ctx, b, false);
-    if (verdict_out && b->ntok > 0)
-      HIPCHK(hipMemcpyAsync(verdict_out, b->b->verdict.p, (size_t)b->ntok, hipMemcpyDeviceToHost, b->dev->stream));
+    run_resident(ctx, b, false);
+    if (verdict_out && b->plan.ntok > 0)
+      HIPCHK(hipMemcpyAsync(verdict_out, b->b->verdict.p, (size_t)b->plan.ntok, hipMemcpyDeviceToHost,
+                            b->lane->stream));
     return 0;
   } catch (const std::exception& e) {
     ctx->set_err(e.what());
@@ -804,7 +1354,7 @@ int jg_batch_sync(jg_ctx* ctx, jg_batch* b) {
   if (!ctx || !b) return -1;
   try {
     HIPCHK(hipSetDevice(b->dev->id));
-    HIPCHK(hipStreamSynchronize(b->dev->stream));
+    HIPCHK(hipStreamSynchronize(b->lane->stream));
     collect_times(b);
     return 0;
   } catch (const std::exception& e) {
@@ -817,7 +1367,7 @@ void jg_batch_free(jg_ctx* ctx, jg_batch* b) {
   (void)ctx;
   if (!b) return;
   (void)hipSetDevice(b->dev->id);
-  (void)hipStreamSynchronize(b->dev->stream);
+  (void)hipStreamSynchronize(b->lane->stream);
   delete b;
 }
 
@@ -831,65 +1381,25 @@ int jg_batch_kernel_times(jg_batch* b, const char** names, float* ms, int cap) {
   return n;
 }
 
-int jg_verify_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
-                    const jg_tok* toks, size_t ntok, uint8_t* verdict_out) {
-  if (!ctx || (ntok > 0 && (!toks || !arena || !verdict_out))) return -1;
-  if (ntok == 0) return 0;
-  // split over devices by the cost model
-  const size_t nd = ctx->devs.size();
-  std::vector<size_t> cut(nd + 1, 0);
-  cut[nd] = ntok;
-  if (nd > 1) {
-    std::vector<double> pre(ntok + 1, 0.0);
-    for (size_t i = 0; i < ntok; ++i) {
-      int c = classify(ctx, toks[i]);
-      pre[i + 1] = pre[i] + cls_cost(c < 0 ? 0 : c);
+int jg_batch_exceptions(jg_batch* b, uint32_t* counts, int cap) {
+  if (!b || !counts || cap < 0) return -1;
+  try {
+    HIPCHK(hipSetDevice(b->dev->id));
+    uint32_t c[NCLS] = {};
+    if (b->b->exc_cnt.p) {
+      HIPCHK(hipMemcpyAsync(c, b->b->exc_cnt.p, sizeof(c), hipMemcpyDeviceToHost, b->lane->stream));
+      HIPCHK(hipStreamSynchronize(b->lane->stream));
     }
-    size_t j = 0;
-    for (size_t k = 1; k < nd; ++k) {
-      const double target = pre[ntok] * (double)k / (double)nd;
-      while (j < ntok && pre[j] < target) ++j;
-      cut[k] = j;
+    for (int k = 0; k < cap && k < NCLS; ++k) {
+      // a class's counter is only meaningful when the batch has work of that class
+      const bool act = b->plan.ranges[k].end > b->plan.ranges[k].begin && k >= CLS_P256 && k <= CLS_P521;
+      counts[k] = act ? c[k] : 0u;
     }
+    return NCLS;
+  } catch (const std::exception& e) {
+    b->ctx->set_err(e.what());
+    return -2;
   }
-  std::vector<int> rc(nd, 0);
-  std::vector<std::string> errs(nd);
-  auto work = [&](size_t k) {
-    Device* d = ctx->devs[k].get();
-    const size_t lo = cut[k], hi = cut[k + 1];
-    if (hi <= lo) return;
-    try {
-      std::lock_guard<std::mutex> g(d->mu);
-      jg_batch b;
-      b.ctx = ctx;
-      b.dev = d;
-      b.b = d->sync_bufs.get();
-      b.timing = false;
-      stage(ctx, &b, arena, arena_len, toks + lo, hi - lo);
-      run(ctx, &b, false);
-      HIPCHK(hipMemcpyAsync(verdict_out + lo, b.b->verdict.p, hi - lo, hipMemcpyDeviceToHost, d->stream));
-      HIPCHK(hipStreamSynchronize(d->stream));
-    } catch (const std::invalid_argument& e) {
-      rc[k] = -1;
-      errs[k] = e.what();
-    } catch (const std::exception& e) {
-      rc[k] = -2;
-      errs[k] = e.what();
-    }
-  };
-  if (nd == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
-    for (auto& t : th) t.join();
-  }
-  for (size_t k = 0; k < nd; ++k)
-    if (rc[k]) {
-      ctx->set_err(errs[k]);
-      return rc[k];
-    }
-  return 0;
 }
 
 int jg_hash_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
@@ -907,18 +1417,19 @@ int jg_hash_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
     Device* d = ctx->devs[0].get();
     std::lock_guard<std::mutex> g(d->mu);
     HIPCHK(hipSetDevice(d->id));
+    const hipStream_t s = d->lane0.stream;
     Grow da, dj, dout;
     uint8_t* a = (uint8_t*)da.get(arena_len + ARENA_SLACK);
-    HIPCHK(hipMemsetAsync(a + arena_len, 0, ARENA_SLACK, d->stream));
-    if (arena_len) HIPCHK(hipMemcpyAsync(a, arena, arena_len, hipMemcpyHostToDevice, d->stream));
+    HIPCHK(hipMemsetAsync(a + arena_len, 0, ARENA_SLACK, s));
+    if (arena_len) HIPCHK(hipMemcpyAsync(a, arena, arena_len, hipMemcpyHostToDevice, s));
     jg_hjob* j = (jg_hjob*)dj.get(sizeof(jg_hjob) * njobs);
-    HIPCHK(hipMemcpyAsync(j, jobs, sizeof(jg_hjob) * njobs, hipMemcpyHostToDevice, d->stream));
+    HIPCHK(hipMemcpyAsync(j, jobs, sizeof(jg_hjob) * njobs, hipMemcpyHostToDevice, s));
     uint32_t* o = (uint32_t*)dout.get(64 * njobs);
-    launch_hash(a, j, (int64_t)njobs, o, d->stream);
+    launch_hash(a, j, (int64_t)njobs, o, s);
     HIPCHK(hipGetLastError());
     std::vector<uint32_t> w(16 * njobs);
-    HIPCHK(hipMemcpyAsync(w.data(), o, 64 * njobs, hipMemcpyDeviceToHost, d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));
+    HIPCHK(hipMemcpyAsync(w.data(), o, 64 * njobs, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     for (size_t k = 0; k < w.size(); ++k) {              // big-endian words -> digest bytes
       digest_out[4 * k] = (uint8_t)(w[k] >> 24);
       digest_out[4 * k + 1] = (uint8_t)(w[k] >> 16);
@@ -941,7 +1452,7 @@ const char* jg_last_error(jg_ctx* ctx) {
 
 void* jg_host_alloc(size_t bytes) {
   void* p = nullptr;
-  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
   return p;
 }
 
@@ -949,6 +1460,6 @@ void jg_host_free(void* p) {
   if (p) (void)hipHostFree(p);
 }
 
-const char* jg_version(void) { return "capjwt 0.1 (gfx950, HIP)"; }
+const char* jg_version(void) { return "capjwt 0.2 (gfx950, HIP)"; }
 
 }  // extern "C"

@@ -87,14 +87,41 @@ void jg_destroy(jg_ctx* ctx);
 /* Replace the key table (copied; may be reloaded on JWKS refresh).  Invalid
  * keys (off-curve EC point, Ed25519 point that does not decode, even or
  * unusable RSA modulus, e out of range) load fine and verify nothing -- the
- * same outcome Go produces per token.  Returns 0 or a negative error. */
+ * same outcome Go produces per token.  Returns 0, -1 on bad arguments, or -2
+ * when the table cannot be staged (e.g. more than 256 EC keys of one curve):
+ * the previous table then stays in force, unless a device failed half-way, in
+ * which case no table is loaded and verification returns -2 until a load
+ * succeeds. */
 int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys);
 
-/* Verify ntok jobs, blocking.  Host buffers; copied to the device(s).  Returns
- * 0 on success, <0 on an infrastructure error (see jg_last_error); per-token
- * outcomes are only in verdict_out[i] (JG_ACCEPT / JG_REJECT). */
+/* Verify ntok jobs, blocking (= jg_submit + jg_wait).  Host buffers; copied to
+ * the device(s) in chunks whose H2D copies overlap the kernels of the previous
+ * chunk (direct DMA when `arena` is pinned -- jg_host_alloc -- else through
+ * pinned staging).  Returns 0 on success, -1 on bad arguments (a key_idx
+ * outside the loaded table, a signing-input or signature span past
+ * arena_len), -2 on an infrastructure error (see jg_last_error); per-token
+ * outcomes are only in verdict_out[i] (JG_ACCEPT / JG_REJECT).  ntok == 0
+ * returns 0 without touching the buffers.
+ * Replaces the per-token loops of jwt/keyset.go:162-167 (staticKeySet) and
+ * jwt/keyset.go:127 (go-oidc remoteKeySet) for a whole batch. */
 int jg_verify_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
                     const jg_tok* toks, size_t ntok, uint8_t* verdict_out);
+
+/* Asynchronous form: jg_submit validates the jobs (same return codes), queues
+ * them on the context's devices and returns at once with a ticket; arena, toks
+ * and verdict_out must stay valid and unmodified until jg_wait(ticket)
+ * returns.  Consecutive submissions pipeline back to back on each device.
+ * jg_wait blocks until every verdict is written, frees the ticket and returns
+ * 0 or -2.  A batch runs entirely against the key table current at submit
+ * time: a jg_keys_load waits for queued work to drain first. */
+typedef struct jg_ticket jg_ticket;
+int jg_submit(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok* toks, size_t ntok,
+              uint8_t* verdict_out, jg_ticket** ticket);
+int jg_wait(jg_ctx* ctx, jg_ticket* ticket);
+
+/* Jobs per pipeline chunk of jg_submit / jg_verify_batch (default 131072, or
+ * CAPJWT_CHUNK; >= 64).  Applies to later submissions.  Returns 0 or -1. */
+int jg_set_chunk(jg_ctx* ctx, size_t jobs);
 
 const char* jg_last_error(jg_ctx* ctx);
 
@@ -121,6 +148,12 @@ void jg_batch_free(jg_ctx* ctx, jg_batch* b);
 /* Per-kernel device time (ms) of the last jg_batch_run, measured with HIP
  * events on the batch's stream.  names/ms arrays of length cap; returns count. */
 int jg_batch_kernel_times(jg_batch* b, const char** names, float* ms, int cap);
+
+/* Diagnostics of the last run of a resident batch: counts[c] = tokens of kernel
+ * class c (0 reject, 1-3 RSA-2K/3K/4K, 4-6 P-256/384/521, 7 Ed25519) whose
+ * ECDSA comb sum hit an exceptional case of the group law and were recomputed
+ * by the complete-formula path.  Returns the number of classes (8) or <0. */
+int jg_batch_exceptions(jg_batch* b, uint32_t* counts, int cap);
 
 /* ---- batched SHA-2 of byte strings ----
  * The hash of cap's OIDC hash-claim checks: oidc/id_token.go:121-135

@@ -1,0 +1,176 @@
+"""GPU checks of the runtime behind the C ABI (jg_runtime.cpp): argument and
+bounds errors, key-load failure handling, the chunked streaming pipeline
+(jg_submit / jg_wait), and the in-process multi-device split -- every verdict
+against the oracle."""
+import ctypes
+
+import pytest
+
+from tests import gpu_helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+def _mixed_arena(keys, toks, reps=1):
+    """Every golden token against every key (all seven kernel classes, wrong
+    families, bad signatures), `reps` times; returns (arena, oracle verdicts)."""
+    from cap_amd import _lib
+    from oracle import jws
+    okeys = [jws.Key.from_fixture(k) for k in keys]
+    arena = _lib.Arena()
+    want = []
+    cache = {}
+    for _ in range(reps):
+        for t in toks:
+            p = jws.parse_jws(t["token"])
+            if p is None or not p.crit_ok:
+                continue
+            sig_b64 = jws.b64url_encode(p.signature).encode()
+            for ki, k in enumerate(okeys):
+                arena.add(p.signing_input, sig_b64, p.alg, ki)
+                key = (t["name"], ki)
+                if key not in cache:
+                    cache[key] = int(jws.verify_sig(p, k))
+                want.append(cache[key])
+    return arena, want
+
+
+def test_abi_return_codes_zero_jobs_zero_keys():
+    """jg_verify_batch with zero jobs, with zero keys loaded, and with jobs
+    whose key or spans are out of range (SURVEY §8b error conventions)."""
+    from cap_amd import _lib
+    L = _lib.lib()
+    ctx = _lib.Context()
+    out = (ctypes.c_uint8 * 4)()
+    # no keys loaded yet, zero jobs: OK, nothing written
+    assert L.jg_verify_batch(ctx.h, None, 0, None, 0, None) == 0
+    assert L.jg_keys_load(ctx.h, None, 0) == 0                 # an empty key table is legal
+    assert L.jg_verify_batch(ctx.h, None, 0, None, 0, None) == 0
+    # a job naming key 0 of an empty table: bad argument
+    arena = b"a.b" + b"\0" * 8
+    tok = (_lib.JgTok * 1)()
+    tok[0].off, tok[0].sig_in_len, tok[0].sig_rel_off, tok[0].sig_b64_len, tok[0].key_idx, tok[0].alg = 0, 1, 2, 1, 0, 7
+    assert L.jg_verify_batch(ctx.h, arena, len(arena), tok, 1, out) == -1
+    assert "key_idx" in ctx.error()
+    keys, _ = H.golden()
+    ctx.load_keys([H.abi_key(k) for k in keys])
+    assert L.jg_verify_batch(ctx.h, arena, len(arena), tok, 1, out) == 0
+    assert out[0] == 0
+    # spans past the arena: rejected on the host before any upload
+    for fld, val in (("off", len(arena) + 1), ("sig_in_len", len(arena) + 1), ("sig_b64_len", len(arena)),
+                     ("sig_rel_off", 1 << 31)):
+        bad = (_lib.JgTok * 1)()
+        ctypes.memmove(bad, tok, ctypes.sizeof(bad))
+        setattr(bad[0], fld, val)
+        assert L.jg_verify_batch(ctx.h, arena, len(arena), bad, 1, out) == -1, fld
+        assert "past the arena" in ctx.error()
+        h = ctypes.c_void_p()
+        assert L.jg_batch_stage(ctx.h, 0, arena, len(arena), bad, 1, ctypes.byref(h)) == -1, fld
+    # null context / pointers
+    assert L.jg_verify_batch(None, arena, len(arena), tok, 1, out) == -1
+    assert L.jg_verify_batch(ctx.h, arena, len(arena), tok, 1, None) == -1
+    assert L.jg_keys_load(None, None, 0) == -1
+    assert L.jg_set_chunk(ctx.h, 8) == -1
+    ctx.close()
+
+
+def test_key_load_failure_keeps_table_and_does_not_hang():
+    """More P-256 keys than a comb-table budget allows: jg_keys_load returns -2,
+    the previous table stays in force (verification neither hangs nor changes)."""
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    sel = [t for t in toks if t["name"].startswith(("valid-ES256", "tamper-sig-ES256", "valid-RS256"))]
+    ctx = _lib.Context()
+    ctx.load_keys([H.abi_key(k) for k in keys])
+    arena, slots = H.jobs_from_tokens(sel, kid_index)
+    before = ctx.verify(arena)
+    p256 = next(k for k in keys if k["kid"] == "p256-a")
+    with pytest.raises(_lib.JgError, match="at most 256 keys"):
+        ctx.load_keys([H.abi_key(p256)] * 257)
+    assert ctx.verify(arena) == before                        # same table, no deadlock
+    assert [before[s] for s in slots] == [t["verdict"] for t in sel]
+    ctx.load_keys([H.abi_key(k) for k in keys])                # and a later load works
+    assert ctx.verify(arena) == before
+    ctx.close()
+
+
+def test_streaming_pipeline_chunks_and_overlapping_submits():
+    """jg_submit with small pipeline chunks (many chunks per device, all
+    NSLOT slots in flight) and several submissions in flight at once: every
+    verdict equals the oracle's and the synchronous path's."""
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    arena, want = _mixed_arena(keys, toks)
+    ctx = _lib.Context()
+    ctx.load_keys([H.abi_key(k) for k in keys])
+    ref = ctx.verify(arena)
+    assert list(ref) == want
+    for chunk in (64, 1000, 4096):
+        ctx.set_chunk(chunk)
+        pend = [ctx.submit(arena) for _ in range(3)]
+        for p in pend:
+            assert p.wait() == ref, chunk
+    ctx.close()
+
+
+def test_streaming_from_pinned_and_scattered_arenas():
+    """The pipeline's three arena routes: direct DMA from a pinned arena,
+    copy of a compact pageable span, and per-job repacking when the jobs of a
+    chunk are scattered far apart in the arena."""
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    arena, want = _mixed_arena(keys, toks)
+    L = _lib.lib()
+    ctx = _lib.Context()
+    ctx.load_keys([H.abi_key(k) for k in keys])
+    ctx.set_chunk(512)
+    n = len(arena.toks)
+    ta = arena.tok_array()
+    out = (ctypes.c_uint8 * n)()
+    # pinned
+    pa = _lib.PinnedBuffer(len(arena.buf))
+    ctypes.memmove(pa.ptr, bytes(arena.buf), len(arena.buf))
+    assert L.jg_verify_batch(ctx.h, pa.ptr, len(arena.buf), ta, n, out) == 0
+    assert list(out) == want
+    pa.free()
+    # scattered: every job's bytes on its own 4 KiB page (span >> bytes needed)
+    gap = 4096
+    buf = bytearray()
+    spread = (_lib.JgTok * n)()
+    for i in range(n):
+        t = ta[i]
+        end = max(t.off + t.sig_in_len, t.off + t.sig_rel_off + t.sig_b64_len)
+        buf += b"\0" * (gap - len(buf) % gap if len(buf) % gap else 0)
+        spread[i] = t
+        spread[i].off = len(buf)
+        buf += bytes(arena.buf[t.off:end])
+    out2 = (ctypes.c_uint8 * n)()
+    assert L.jg_verify_batch(ctx.h, bytes(buf), len(buf), spread, n, out2) == 0
+    assert list(out2) == want
+    ctx.close()
+
+
+def test_multi_device_split_on_two_slots():
+    """A context with two device slots on the same GPU ({0, 0}): the batch is
+    split by the cost model, each slot stages only its share's arena span
+    (rebased), and the verdicts equal the oracle's -- the in-process
+    multi-device path without a second GPU."""
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    arena, want = _mixed_arena(keys, toks, reps=3)
+    ctx = _lib.Context([0, 0])
+    ctx.load_keys([H.abi_key(k) for k in keys])
+    assert list(ctx.verify(arena)) == want
+    ctx.set_chunk(700)
+    pend = [ctx.submit(arena) for _ in range(2)]
+    for p in pend:
+        assert list(p.wait()) == want
+    # a key reload between batches reaches both slots
+    order = keys[::-1]
+    ctx.load_keys([H.abi_key(k) for k in order])
+    kid_index = {k["kid"]: i for i, k in enumerate(order)}
+    arena2, slots = H.jobs_from_tokens(toks, kid_index)
+    out = ctx.verify(arena2)
+    assert [0 if s is None else out[s] for s in slots] == [t["verdict"] for t in toks]
+    ctx.close()

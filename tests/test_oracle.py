@@ -102,3 +102,18 @@ def test_oracle_rsa_keys_above_4096_bits():
     for t in d["tokens"]:
         p = jws.parse_jws(t["token"])
         assert int(jws.verify_sig(p, keys[t["key"]])) == t["want"], t["name"]
+
+
+def test_oracle_matches_crafted_ec_edge_fixtures():
+    """tests/golden/ec_edge.json (make_ec_edge_fixtures.py: verdicts from plain
+    affine big-integer arithmetic under the Go rule R22): exceptional comb
+    sums, x(R) >= n, an ES256 token on a P-521 key, the reference's example
+    token -- the C oracle agrees on every one."""
+    import json
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ec_edge.json")))
+    keys = {k["kid"]: jws.Key.from_fixture(k) for k in d["keys"]}
+    assert len(d["tokens"]) >= 20
+    for t in d["tokens"]:
+        p = jws.parse_jws(t["token"])
+        assert int(jws.verify_sig(p, keys[t["key"]])) == t["verdict"], t["name"]
+    assert sum(t["verdict"] for t in d["tokens"]) >= 7
