@@ -40,6 +40,7 @@ COLL_DEVICE = "cuda"            # device of the timing all-reduce (RCCL); "cpu" 
 # statement (no hazard padding), profiles/r01_int_rates2.json -- i.e. one
 # wave64 VALU instruction per 4 cycles per SIMD, the chip's full VALU issue rate.
 MAD_PEAK_T = 36.98
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 
 JG_TOK = np.dtype([("off", "<u8"), ("sig_in_len", "<u4"), ("sig_rel_off", "<u4"), ("sig_b64_len", "<u4"),
                    ("key_idx", "<u2"), ("alg", "u1"), ("flags", "u1")])
@@ -67,16 +68,59 @@ def p256_point_mads_per_token():
     return (adds - 1) * madd + madd_z1 + sqr + 2 * mul
 
 
+def ec_point_mads_per_token(L, red_mul, red_sqr, fold, wg, wq, bits, red_generic):
+    """Multiply-accumulates of a comb point kernel (k_ec_point) per token:
+    products are L^2 (mul) or L(L+1)/2 (sqr) partial products + the
+    reduction's MADs (red_*: L rows x the non-zero reduction constants); a
+    mixed addition is 8 mul + 3 sqr + 2 value folds (`fold` MADs each); the
+    first addition is an assignment, the second lands on Z == 1 (4 mul + 2 sqr
+    + 2 folds); the final check is 1 sqr + 2 mul with the generic reduction."""
+    mul, sqr = L * L + red_mul, L * (L + 1) // 2 + red_sqr
+    madd = 8 * mul + 3 * sqr + 2 * fold
+    madd_z1 = 4 * mul + 2 * sqr + 2 * fold
+    ng, nq = (bits + 1 + wg - 1) // wg, (bits + 1 + wq - 1) // wq
+    adds = ng * (1 - 2.0 ** -wg) + nq * (1 - 2.0 ** -wq) - 1
+    gmul, gsqr = L * L + red_generic, L * (L + 1) // 2 + red_generic
+    return (adds - 1) * madd + madd_z1 + gsqr + 2 * gmul
+
+
+def p384_point_mads_per_token():
+    """P-384 (ecdsa.hpp: L = 15 28-bit limbs, G W = 20 / key W = 20/16): the hot
+    loop's mulf / sqrf use the special-form reduction, 4 signed MADs per row
+    (mp.hpp mont_reduce_p384); value folds through freduce (5 non-zero
+    constants of 2^384 mod p); final check with m+1's 12 non-zero limbs."""
+    return ec_point_mads_per_token(15, 15 * 4, 15 * 4, 5, 20, 16, 384, 15 * 12)
+
+
+def ed25519_point_mads_per_token():
+    """k_ed_point: 13 + 16 comb windows (B W = 20, key W = 16), each a Niels
+    addition of 7 field products (ed25519.hip add_niels); p = 2^255 - 19 is
+    reduced with 2 MADs per row (mp.hpp mont_reduce_25519): a product is
+    L^2 + 2L = 120 MADs.  Plus k = H mod L (one reduction + one product mod L)."""
+    L = 10
+    mul = L * L + 2 * L
+    adds = 13 * (1 - 2.0 ** -20) + 16 * (1 - 2.0 ** -16)
+    return adds * 7 * mul + 220
+
+
 def rsa_modexp_mads_per_token(limbs, lanes):
     """k_rsa_modexp (e = 65537): 18 Montgomery products on L 28-bit limbs held
     by `lanes` lanes per token (H = L / lanes each; RSA-2048: L = 74 on 2 lanes,
-    RSA-4096: 148 on 4).  To-Montgomery and the final multiply (mont_mul) are
-    2 L^2 multiply-accumulates each; the 16 squarings (mont_sqr) issue each limb
-    product once -- lanes^2 * H(H+1)/2 for the square (L(L+1)/2 plus the
-    diagonal blocks' duplicated diagonal) + L^2 for the reduction."""
+    RSA-3072: 112 on 4, RSA-4096: 148 on 4).  To-Montgomery and the final
+    multiply (mont_mul) are 2 L^2 multiply-accumulates each; the 16 squarings
+    (mont_sqr) issue each limb product once -- lanes^2 * H(H+1)/2 for the
+    square (L(L+1)/2 plus the diagonal blocks' duplicated diagonal) + L^2 for
+    the reduction."""
     h = limbs // lanes
     sqr = lanes * lanes * h * (h + 1) // 2 + limbs * limbs
     return 2 * 2 * limbs * limbs + 16 * sqr
+
+
+def prep_bytes_per_token(token_bytes, sig_rows):
+    """Algorithmic HBM bytes of k_prep per token: the token's signing input and
+    signature read once, the 24-B job + 4-B plan entry, the decoded signature
+    rows (4 B each), 16 digest words, status + signature length."""
+    return token_bytes + 28 + 4 * sig_rows + 64 + 3
 
 
 # ---------------------------------------------------------------- inputs
@@ -219,7 +263,7 @@ def h2d_bandwidth(nbytes, iters=5):
     return nbytes / best
 
 
-def measure_pcie(ctx, arena, toks, iters=3, chunks=(65536, 131072, 262144)):
+def measure_pcie(ctx, arena, toks, iters=3, chunks=(16384, 32768, 65536)):
     """jg_verify_batch end to end from PINNED host buffers: H2D of arena + jobs
     (chunked, copies overlapping the previous chunk's kernels), planning,
     kernels, verdict D2H.  Reported beside `value`, never as it."""
@@ -239,7 +283,7 @@ def measure_pcie(ctx, arena, toks, iters=3, chunks=(65536, 131072, 262144)):
                 raise RuntimeError(ctx.error())
             best = min(best, time.perf_counter() - t0)
         per_chunk[ch] = best
-    ctx.set_chunk(131072)
+    ctx.set_chunk(32768)
     pa.free()
     ch, best = min(per_chunk.items(), key=lambda kv: kv[1])
     bw = h2d_bandwidth(len(arena))
@@ -282,8 +326,35 @@ def measure_e2e(pool, kids_jwk, total, threads):
                     "on host_threads cores + one jg_verify_batch (H2D included); not the headline value"}
 
 
-def cpu_baseline(pool, alg, okeys, threads, seconds, keyidx=None):
-    """The C oracle (oracle/jws_oracle.c) on the host's cores over a bounded sample."""
+def cpu_info():
+    """The host CPUs this process may use: nproc (cgroup-aware), the affinity
+    mask, the cgroup v2 CPU quota, and the lscpu model."""
+    import math
+    info = {"os_cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        info["nproc"] = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+    except (OSError, ValueError):
+        info["nproc"] = None
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpu_quota"] = quota
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True).stdout
+        info["model"] = next((ln.split(":", 1)[1].strip() for ln in out.splitlines() if ln.startswith("Model name")), None)
+    except OSError:
+        info["model"] = None
+    info["cores_used"] = max(1, min(info["affinity"], math.ceil(quota) if quota else info["affinity"]))
+    return info
+
+
+def cpu_baseline(pool, alg, okeys, threads, seconds, keyidx=None, max_tokens=None, cpu=None):
+    """The C oracle (oracle/jws_oracle.c) on the host's cores over a bounded
+    sample (the whole pool when max_tokens is given and fits)."""
     from oracle import jws
     L = jws.lib()
 
@@ -320,13 +391,16 @@ def cpu_baseline(pool, alg, okeys, threads, seconds, keyidx=None):
             else:
                 j.key_kind, j.x = 2, buf(k.x)
         return jobs
-    # calibrate on 64 tokens single-threaded, then size the sample for `seconds` of wall time
-    probe = make_jobs(64)
-    out = (ctypes.c_uint8 * 64)()
-    t0 = time.perf_counter()
-    L.or_verify_many(probe, 64, 1, out)
-    per = (time.perf_counter() - t0) / 64
-    n = int(max(256, min(len(pool), seconds * threads / per)))
+    if max_tokens:
+        n = max_tokens
+    else:
+        # calibrate on 64 tokens single-threaded, then size the sample for `seconds` of wall time
+        probe = make_jobs(64)
+        out = (ctypes.c_uint8 * 64)()
+        t0 = time.perf_counter()
+        L.or_verify_many(probe, 64, 1, out)
+        per = (time.perf_counter() - t0) / 64
+        n = int(max(256, min(len(pool), seconds * threads / per)))
     jobs = make_jobs(n)
     out = (ctypes.c_uint8 * n)()
     t0 = time.perf_counter()
@@ -334,10 +408,40 @@ def cpu_baseline(pool, alg, okeys, threads, seconds, keyidx=None):
     el = time.perf_counter() - t0
     ok = sum(out)
     name = alg if isinstance(alg, str) else "mixed"
-    return {"value": n / el, "unit": "verified JWTs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} {name} tokens from the benchmark pool verified by the C oracle "
-                      f"(oracle/jws_oracle.c, a restatement of Go crypto/*, not Go itself) "
-                      f"on {threads} host threads; {ok}/{n} accepted; {el:.2f} s wall"}
+    res = {"value": n / el, "unit": "verified JWTs/s", "cores": threads, "kind": "port",
+           "sample": f"{n} {name} tokens from the benchmark pool verified by the C oracle "
+                     f"(oracle/jws_oracle.c, a restatement of Go crypto/*, not Go itself) "
+                     f"on {threads} host threads (all cores available to the process); {ok}/{n} accepted; "
+                     f"{el:.2f} s wall", "accepted": ok, "tokens": n}
+    if cpu:
+        res["cpu"] = cpu
+    return res
+
+
+CPUVERIFY = os.path.join(ROOT, "tools", "cpuverify", "cpuverify")
+
+
+def openssl_baseline(pool, alg, keypaths, threads, seconds):
+    """All-core OpenSSL libcrypto verification of the same tokens
+    (tools/cpuverify): a closer stand-in for Go's assembly-backed crypto than
+    the clarity-first C oracle.  Token i is verified with key i % len(keypaths),
+    as tools/tokgen signed it."""
+    if not os.path.exists(CPUVERIFY):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(CPUVERIFY)], check=True)
+    path = os.path.join("/tmp", f"capjwt_cpuverify_{alg}_{os.getpid()}.txt")
+    with open(path, "wb") as f:
+        f.write(b"\n".join(pool) + b"\n")
+    try:
+        r = subprocess.run([CPUVERIFY, alg, str(threads), str(seconds), path] + list(keypaths),
+                           capture_output=True, text=True, check=True)
+    finally:
+        os.unlink(path)
+    d = json.loads(r.stdout)
+    return {"value": d["per_second"], "unit": "verified JWTs/s", "cores": threads, "kind": "openssl",
+            "sample": f"{d['tokens']} {alg} tokens (the benchmark pool) verified {d['verified']} times in total "
+                      f"by {d['openssl']} (tools/cpuverify, EVP_DigestVerify) on {threads} threads for "
+                      f"{d['seconds']:.1f} s; {d['accepted']}/{d['verified']} accepted. Not Go.",
+            "accepted": d["accepted"], "verified": d["verified"]}
 
 
 def golden_oracle_keys(kids):
@@ -380,8 +484,26 @@ def tamper(pool, algs, keyidx, keys_meta, frac, seed=1):
     return pool, algs, keyidx, good
 
 
+def roofline_line(kernel_ms, per_gpu, kernels):
+    """{kernel: roofline} for each (key, mads-per-token | ('hbm', bytes-per-token))."""
+    out = {}
+    for key, work in kernels.items():
+        if key not in kernel_ms:
+            continue
+        sec = kernel_ms[key] * 1e-3
+        if isinstance(work, tuple):               # ("hbm", bytes per token)
+            ach = work[1] * per_gpu / sec / 1e9
+            out[key] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": ach / HBM_PEAK_GBPS, "bytes_per_token": work[1]}
+        else:
+            ach = work * per_gpu / sec / 1e12
+            out[key] = {"bound": "valu", "achieved": ach, "peak": MAD_PEAK_T, "unit": "TMAD/s",
+                        "frac": ach / MAD_PEAK_T, "mads_per_token": work}
+    return out
+
+
 def config_line(ctx, name, workload, pool, algs, keyidx, expected_good, per_gpu, steps, warmup, dist, world,
-                kernel_key=None, mads=None):
+                kernels=None):
     arena, toks = pack(pool, algs, keyidx, per_gpu)
     el, acc, kms, v = measure(ctx, arena, toks, steps, warmup, dist)
     reps = (per_gpu + len(pool) - 1) // len(pool)
@@ -391,10 +513,25 @@ def config_line(ctx, name, workload, pool, algs, keyidx, expected_good, per_gpu,
             "accepted": acc, "expected_accepted": want, "kernel_ms": kms}
     if acc != want:
         line["error"] = f"accepted {acc} != expected {want}"
-    if kernel_key and mads and kernel_key in kms:
-        ach = mads * per_gpu / (kms[kernel_key] * 1e-3) / 1e12
-        line["roofline"] = {"bound": "valu", "kernel": kernel_key, "achieved": ach, "peak": MAD_PEAK_T,
-                            "unit": "TMAD/s", "frac": ach / MAD_PEAK_T}
+    if kernels:
+        # per-class token counts: a mixed batch's class kernels see only their share
+        share = {}
+        for key in kernels:
+            cls = key.split("_")[0]
+            share[key] = cls
+        counts = {}
+        aid = np.asarray(algs)
+        for key, cls in share.items():
+            fam = {"p256": (7,), "p384": (8,), "p521": (9,), "ed25519": (10,), "rsa2048": (1, 2, 3, 4, 5, 6),
+                   "rsa3072": (1, 2, 3, 4, 5, 6), "rsa4096": (1, 2, 3, 4, 5, 6)}[cls]
+            frac = float(np.isin(aid, fam).mean()) if cls not in ("rsa2048", "rsa3072", "rsa4096") else None
+            counts[key] = frac
+        rl = {}
+        for key, work in kernels.items():
+            frac = counts[key]
+            n = per_gpu * (frac if frac is not None else 1.0)
+            rl.update(roofline_line(kms, n, {key: work}))
+        line["roofline"] = rl
     return line
 
 
@@ -406,7 +543,9 @@ def run_configs(ctx, args, threads, rank, world, dist):
     out["ps512_rsa4096"] = config_line(
         ctx, "ps512_rsa4096", "PS512 RSA-4096 (PSS/MGF1-SHA512), 1M tokens / 8 GPUs = 131072 per GPU (configs[2])",
         pool, [ALG_IDS["PS512"]] * len(pool), [0] * len(pool), np.ones(len(pool), bool), 131072,
-        max(1, args.steps // 2), 1, dist, world, "rsa4096_modexp", rsa_modexp_mads_per_token(148, 4))
+        max(1, args.steps // 2), 1, dist, world,
+        kernels={"rsa4096_modexp": rsa_modexp_mads_per_token(148, 4),
+                 "rsa4096_prep": ("hbm", prep_bytes_per_token(939, 132))})
     # configs[3]: EdDSA Ed25519 + ES384 P-384 mixed, 1M tokens per GPU
     ctx.load_keys(abi_keys(["ed-a", "p384-a"]))
     pe = gen_tokens("EdDSA", 8192, golden_keypaths(["ed-a"]), threads, f"c3r{rank}")
@@ -415,7 +554,10 @@ def run_configs(ctx, args, threads, rank, world, dist):
     algs = [ALG_IDS["EdDSA"], ALG_IDS["ES384"]] * len(pe)
     out["eddsa_es384_mixed"] = config_line(
         ctx, "eddsa_es384_mixed", "EdDSA Ed25519 + ES384 P-384 50/50 mixed batch, 1M tokens per GPU (configs[3])",
-        pool, algs, [0, 1] * len(pe), np.ones(len(pool), bool), 1 << 20, max(1, args.steps // 2), 1, dist, world)
+        pool, algs, [0, 1] * len(pe), np.ones(len(pool), bool), 1 << 20, max(1, args.steps // 2), 1, dist, world,
+        kernels={"p384_point": p384_point_mads_per_token(), "ed25519_point": ed25519_point_mads_per_token(),
+                 "p384_prep": ("hbm", prep_bytes_per_token(384, 49)),
+                 "ed25519_prep": ("hbm", prep_bytes_per_token(342, 16))})
     # configs[4]: all 10 algs, 32 kids, ~5 % tampered; the 10M stream in 256k-token chunks (one chunk per step)
     meta = bench_keys()
     ctx.load_keys([m[3] for m in meta])
@@ -454,7 +596,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--tokens", type=int, default=1 << 20, help="tokens per GPU per step")
-    ap.add_argument("--pool", type=int, default=1 << 17, help="unique signed tokens (replicated)")
+    ap.add_argument("--pool", type=int, default=0, help="unique signed ES256 tokens (default: all unique)")
+    ap.add_argument("--rs-pool", type=int, default=100000, help="unique RS256 tokens (BASELINE configs[0]: 100k)")
+    ap.add_argument("--no-ab", action="store_true", help="skip the replicated-pool A/B line")
     ap.add_argument("--no-rs256", action="store_true")
     ap.add_argument("--no-configs", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -480,14 +624,15 @@ def main():
         td.init_process_group("nccl" if COLL_DEVICE == "cuda" else "gloo")
     from cap_amd import _lib
 
-    host_threads = max(1, min(16, os.cpu_count() or 1))
+    cpu = cpu_info()
+    host_threads = cpu["cores_used"]          # every core this process may use (cgroup quota, affinity)
     ctx = _lib.Context([dev])
 
-    # ---- ES256, P-256 JWKS with 4 kids (configs[1])
+    # ---- ES256, P-256 JWKS with 4 kids (configs[1]): 1M unique OpenSSL-signed tokens
     kids = ["p256-a", "p256-b", "p256-c", "p256-d"]
     ctx.load_keys(abi_keys(kids))
-    pool = gen_tokens("ES256", min(args.pool, args.tokens), golden_keypaths(kids), host_threads, f"r{rank}")
-    npool = len(pool)
+    npool = min(args.pool or args.tokens, args.tokens)
+    pool = gen_tokens("ES256", npool, golden_keypaths(kids), host_threads, f"r{rank}")
     arena, toks = pack(pool, [ALG_IDS["ES256"]] * npool, np.arange(npool) % len(kids), args.tokens)
     el, acc, kms, _ = measure(ctx, arena, toks, args.steps, args.warmup, dist)
     ntok = len(toks)
@@ -508,10 +653,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32 (28-bit limbs, 64-bit v_mad_u64_u32 accumulators)",
-        "data": f"synthetic: OpenSSL-signed ES256 JWTs (testJWTClaims shape), {npool}-token unique pool "
-                f"replicated to {ntok} per GPU, no verdict caching",
+        "data": f"synthetic: OpenSSL-signed ES256 JWTs (testJWTClaims shape), {npool} unique tokens"
+                + (f" replicated to {ntok}" if npool < ntok else "") + " per GPU, no verdict caching",
         "config": {"workload": "ES256 P-256 JWKS with 4 kids, 1M tokens batch-verified per MI355X (BASELINE configs[1])",
-                   "tokens_per_gpu": ntok, "kids": 4, "parallelism": f"independent shards x{world}"},
+                   "tokens_per_gpu": ntok, "unique_tokens": npool, "kids": 4,
+                   "parallelism": f"independent shards x{world}"},
         "accepted": acc,
         "roofline": {"bound": "valu", "kernel": "k_ec_point<P256>",
                      "achieved": achieved, "peak": MAD_PEAK_T, "unit": "TMAD/s",
@@ -519,19 +665,31 @@ def main():
                      "note": "integer multiply-add roofline (SURVEY §8d): algorithmic 32x32->64 MADs "
                              f"per token {p256_point_mads_per_token():.0f} x tokens / HIP-event kernel time; "
                              "peak = measured v_mad_u64_u32 rate; traffic = HBM bytes per launch from the "
-                             "rocprofv3 --pmc pass in profiles/r01_s7_pmc_traffic.json"},
+                             f"rocprofv3 --pmc passes in {os.path.relpath(TRAFFIC, ROOT)}"},
+        "roofline_other": roofline_line(kms, ntok, {"p256_prep": ("hbm", prep_bytes_per_token(342, 49))}),
         "kernel_ms": kms,
+        "cpu": cpu,
     }
     if acc != ntok:
         result["error"] = f"only {acc}/{ntok} valid tokens accepted"
     if rank == 0 and world == 1:
         result["pcie"] = measure_pcie(ctx, arena, toks)
     del arena, toks
+    # A/B: the same batch built from a 131072-token pool replicated 8x (round-1 default)
+    if not args.no_ab and npool > (1 << 17):
+        sub = pool[:1 << 17]
+        a2, t2 = pack(sub, [ALG_IDS["ES256"]] * len(sub), np.arange(len(sub)) % len(kids), args.tokens)
+        el2, acc2, kms2, _ = measure(ctx, a2, t2, max(1, args.steps // 2), 1, dist)
+        result["pool_ab"] = {"replicated_pool": len(sub), "value": world * len(t2) * max(1, args.steps // 2) / el2,
+                             "kernel_ms": kms2, "accepted": acc2,
+                             "note": "same 1M-token batch from a 131072-token pool replicated 8x; `value` above "
+                                     "uses unique tokens"}
+        del a2, t2
 
-    # ---- RS256 RSA-2048 (second half of the metric)
+    # ---- RS256 RSA-2048 (second half of the metric; BASELINE configs[0]'s 100k-token pool)
     if not args.no_rs256:
         ctx.load_keys(abi_keys(["rsa2048-a"]))
-        rpool = gen_tokens("RS256", min(1 << 15, args.tokens), golden_keypaths(["rsa2048-a"]), host_threads,
+        rpool = gen_tokens("RS256", min(args.rs_pool, args.tokens), golden_keypaths(["rsa2048-a"]), host_threads,
                            f"r{rank}")
         rarena, rtoks = pack(rpool, [ALG_IDS["RS256"]] * len(rpool), [0] * len(rpool), args.tokens)
         rsteps = max(1, args.steps // 2)
@@ -540,11 +698,13 @@ def main():
         rach = rsa_modexp_mads_per_token(74, 2) * len(rtoks) / (mexp * 1e-3) / 1e12
         result["rs256"] = {"value": world * len(rtoks) * rsteps / rel, "unit": "verified JWTs/s",
                            "ms_per_step": rel * 1000.0 / rsteps, "tokens_per_gpu": len(rtoks),
-                           "accepted": racc, "kernel_ms": rkms,
+                           "unique_tokens": len(rpool), "accepted": racc, "kernel_ms": rkms,
                            "roofline": {"bound": "valu", "kernel": "k_rsa_modexp<37,2,8>", "achieved": rach,
                                         "peak": MAD_PEAK_T, "unit": "TMAD/s", "frac": rach / MAD_PEAK_T,
                                         "mads_per_token": rsa_modexp_mads_per_token(74, 2),
-                                        "traffic": load_traffic("rsa2048_modexp")}}
+                                        "traffic": load_traffic("rsa2048_modexp")},
+                           "roofline_other": roofline_line(rkms, len(rtoks),
+                                                           {"rsa2048_prep": ("hbm", prep_bytes_per_token(598, 66))})}
         if racc != len(rtoks):
             result["rs256"]["error"] = f"only {racc}/{len(rtoks)} valid tokens accepted"
         del rarena, rtoks
@@ -559,12 +719,26 @@ def main():
         jwk = [{"kty": "EC", "kid": f"kid-{i:02d}", "crv": "P-256", **xy} for i, xy in enumerate(p256_jwk_xy(kids))]
         result["e2e"] = measure_e2e(pool, jwk, args.tokens, host_threads)
 
-    # ---- CPU baseline (rank 0, N = 1 only)
+    # ---- CPU baselines (rank 0, N = 1 only): the C oracle ("port", the
+    # contract's cpu_baseline) and OpenSSL libcrypto, both on every core
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(pool, "ES256", golden_oracle_keys(kids), host_threads, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(pool, "ES256", golden_oracle_keys(kids), host_threads,
+                                              args.cpu_seconds, cpu=cpu)
+        result["cpu_baseline_openssl"] = {"es256": openssl_baseline(pool[:1 << 16], "ES256", golden_keypaths(kids),
+                                                                    host_threads, 5.0)}
+        speed = {"es256_vs_port": value / result["cpu_baseline"]["value"],
+                 "es256_vs_openssl": value / result["cpu_baseline_openssl"]["es256"]["value"]}
         if not args.no_rs256:
+            # BASELINE configs[0]: RS256 RSA-2048 StaticKeySet, 100k tokens, all cores
             result["cpu_baseline_rs256"] = cpu_baseline(rpool, "RS256", golden_oracle_keys(["rsa2048-a"]),
-                                                        host_threads, args.cpu_seconds / 2)
+                                                        host_threads, 0, max_tokens=len(rpool), cpu=cpu)
+            result["cpu_baseline_openssl"]["rs256"] = openssl_baseline(rpool, "RS256", golden_keypaths(["rsa2048-a"]),
+                                                                       host_threads, 3.0)
+            speed["rs256_vs_port"] = result["rs256"]["value"] / result["cpu_baseline_rs256"]["value"]
+            speed["rs256_vs_openssl"] = result["rs256"]["value"] / result["cpu_baseline_openssl"]["rs256"]["value"]
+        speed["note"] = ("GPU value / all-core CPU rate on the same tokens; neither CPU leg is Go (absent on the GPU "
+                         "box): 'port' = the repo's C oracle, 'openssl' = OpenSSL libcrypto")
+        result["speedup_vs_cpu"] = speed
     if rank == 0:
         print(json.dumps(result))
     if dist:

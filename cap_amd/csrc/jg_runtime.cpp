@@ -13,12 +13,14 @@
 //
 // Streaming path (jg_submit / jg_wait / jg_verify_batch): a batch
 // is split over the devices by the per-alg cost model, and each device's part
-// runs through a ring of NSLOT pipeline slots in chunks of CHUNK jobs.  Every
-// slot owns a stream (+ per-class fan-out streams), device scratch and pinned
-// host staging, so the host plan and the H2D copy of chunk k+1 overlap the
-// kernels of chunk k.  One worker thread per device drains a FIFO of submitted
+// runs in chunks of CHUNK jobs through a ring of NSLOT buffer sets (device
+// scratch + pinned host staging).  The H2D copies of all chunks run back to
+// back on one copy stream (the link stays busy while the host plans ahead);
+// each chunk's kernels run on one of NLANE compute streams (+ per-class
+// fan-out streams) once its copy event fires, overlapping the next copies.  One worker thread per device drains a FIFO of submitted
 // work, so chunks of consecutive submissions overlap as well.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -29,6 +31,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -47,16 +50,15 @@
 #include "kernels/prep.hpp"
 #include "kernels/rsa.hpp"
 
-static_assert(sizeof(jg_tok) == sizeof(jg_tok_dev), "jg_tok layout");
-static_assert(offsetof(jg_tok, key_idx) == offsetof(jg_tok_dev, key_idx), "jg_tok layout");
-static_assert(offsetof(jg_tok, alg) == offsetof(jg_tok_dev, alg), "jg_tok layout");
+static_assert(sizeof(jg_tok) == 24 && sizeof(jgk::JobDev) == 16, "job layouts");
 
 using namespace jgk;
 
 namespace {
 
 constexpr size_t ARENA_SLACK = 256;   // aligned SHA word reads may run past the last string
-constexpr int NSLOT = 3;              // pipeline depth per device
+constexpr int NLANE = 3;              // compute streams per device (HW queues 1..3; the copy stream has 0)
+constexpr int NSLOT = 8;              // chunk buffer sets per device (pipeline depth)
 constexpr int NALG = 16;              // alg ids 0..15 in the class table (jg_alg <= 10)
 
 #define HIPCHK(x)                                                                   \
@@ -70,7 +72,6 @@ bool pipe_trace() {
   return on;
 }
 hipEvent_t g_trace_ref = nullptr;     // first chunk's H2D start (trace only)
-std::chrono::steady_clock::time_point g_trace_t0;
 
 double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -82,9 +83,23 @@ size_t chunk_jobs() {
       const long v = std::atol(e);
       if (v >= 64) return (size_t)v;
     }
-    return (size_t)131072;
+    return (size_t)32768;
   }();
   return n;
+}
+
+// Chunk boundaries of jobs [lo, hi) for a pipeline of C-job chunks: the first
+// chunks ramp up from 4096 jobs (the copy engine starts after a short host
+// plan) and the tail ends in a quarter-size chunk (little kernel time left
+// exposed after the last copy).
+std::vector<size_t> chunk_cuts(size_t lo, size_t hi, size_t C) {
+  std::vector<size_t> cut{lo};
+  for (size_t ramp = std::min<size_t>(C, 4096); cut.back() < hi; ramp = std::min(C, 2 * ramp))
+    cut.push_back(std::min(hi, cut.back() + ramp));
+  const size_t tail = C / 4;
+  if (cut.size() > 2 && tail >= 1024 && cut.back() - cut[cut.size() - 2] > tail)
+    cut.insert(cut.end() - 1, cut.back() - tail);
+  return cut;
 }
 
 int cls_rows_sig(int c) {
@@ -137,15 +152,17 @@ struct Grow {                     // grow-only device allocation
 
 struct HGrow {                    // grow-only pinned host allocation
   void* p = nullptr;
+  void* dp = nullptr;             // the same memory as kernels address it
   size_t cap = 0;
   void* get(size_t n) {
     if (n == 0) n = 16;
     if (n > cap) {
       if (p) (void)hipHostFree(p);
-      p = nullptr;
+      p = dp = nullptr;
       cap = 0;
       const size_t want = std::max(n, cap + cap / 2);
-      HIPCHK(hipHostMalloc(&p, want, hipHostMallocPortable));
+      HIPCHK(hipHostMalloc(&p, want, hipHostMallocPortable | hipHostMallocMapped));
+      HIPCHK(hipHostGetDevicePointer(&dp, p, 0));
       cap = want;
     }
     return p;
@@ -175,8 +192,12 @@ struct Lane {
   hipStream_t stream = nullptr;
   hipStream_t cstream[NCLS] = {};
   hipEvent_t ev_start = nullptr, ev_done[NCLS] = {};
-  void create() {
-    HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  // Streams are bound to the process's hardware queues round-robin in
+  // creation order (GPU_MAX_HW_QUEUES, 4 by default): the device creates
+  // every lane's main stream first so the pipeline slots land on distinct
+  // queues and really overlap, then the per-class fan-out streams.
+  void create_main() { HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); }
+  void create_fanout() {
     for (int c = 1; c < NCLS; ++c) {
       HIPCHK(hipStreamCreateWithFlags(&cstream[c], hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&ev_done[c], hipEventDisableTiming));
@@ -204,7 +225,10 @@ struct Lane {
 };
 
 struct Bufs {
-  Grow arena, toks, perm, wave_key, sigw, dig, status, siglen, vpad, verdict, rows, pss, exc, exc_cnt;
+  // jobs: the plan's padded JobDev array; perm (resident batches only): padded
+  // index -> caller index, for the device-side verdict scatter (pipeline
+  // chunks scatter on the host from their staged perm instead)
+  Grow arena, jobs, perm, meta, sigw, dig, status, siglen, vpad, verdict, rows, pss, exc, exc_cnt;
 };
 
 // Host side of one staged chunk: the counting-sort layout.
@@ -216,6 +240,11 @@ struct Plan {
   int sig_rows = 1, scratch_rows = 1;
   int64_t pss_tokens = 0;         // PSS scratch tokens: the RSA classes' ranges back to back
   int64_t pss_off[NCLS] = {};
+};
+
+struct PlanScratch {              // reused across chunks
+  std::vector<uint8_t> tcls;      // class per job (host fill only)
+  std::vector<int64_t> start, total;   // per bucket [nkeys + 1]
 };
 
 struct Ticket {
@@ -238,14 +267,15 @@ struct Ticket {
   }
 };
 
-// A pipeline slot: stream lane, device scratch, pinned host staging.
+// A pipeline slot: the device scratch and pinned host staging of one chunk
+// in flight (its kernels run on one of the device's NLANE compute lanes).
 struct Slot {
-  Lane lane;
   Bufs bufs;
-  HGrow h_arena, h_toks, h_perm, h_wkey, h_verdict;
-  hipEvent_t done = nullptr;
+  HGrow h_arena, h_meta, h_verdict;   // pinned staging: arena repack, plan block (H2D), verdicts (D2H)
+  hipEvent_t done = nullptr;       // slot stream: verdicts copied back
+  hipEvent_t copied = nullptr;     // copy stream: the chunk's inputs are on the device
   hipEvent_t tr_a = nullptr, tr_b = nullptr, tr_c = nullptr;   // CAPJWT_PIPE_TRACE: H2D start / end, kernels end
-  double host_ms[3] = {};                                       // wait, plan, enqueue
+  double host_ms[4] = {};                                       // wait, plan, enqueue, of which H2D calls
   int chunk_no = 0;
   bool inflight = false;
   std::shared_ptr<Ticket> ticket;
@@ -261,8 +291,9 @@ struct Item {                     // one device's share of a submission
   size_t lo = 0, hi = 0;
   uint8_t* out = nullptr;         // the caller's verdicts (index space of toks)
   uint64_t epoch = 0;
-  bool pinned = false;            // arena is page-locked (direct DMA)
+  const uint8_t* dev_arena = nullptr;   // device view of a page-locked arena (kernels read it over PCIe)
   size_t chunk = 0, nchunks = 0;
+  std::vector<size_t> cuts;       // chunk boundaries (chunk_cuts)
 };
 
 struct Device {
@@ -279,16 +310,20 @@ struct Device {
   uint32_t* dblob = nullptr;
   int32_t* didx = nullptr;
   std::mutex mu;                  // device state + lane0 + slots
-  // streaming pipeline
+  // streaming pipeline: H2D copies of every chunk back to back on one copy
+  // stream (full link bandwidth, no sharing between slots), each slot's
+  // kernels on its own stream once its copy event fires
+  hipStream_t copy = nullptr;
+  Lane lanes[NLANE];
   Slot slots[NSLOT];
-  int next_slot = 0;
+  int next_slot = 0, next_lane = 0;
   std::thread worker;
   std::mutex qmu;
   std::condition_variable qcv, idle_cv;
   std::deque<Item> q;
   bool stop = false, busy = false;
-  std::vector<uint8_t> tcls;      // worker scratch: class per job of a chunk
-  std::vector<int64_t> cnt, fill; // worker scratch: bucket counts / cursors
+  PlanScratch plan;               // worker scratch of the host plan
+  uint8_t* dcls = nullptr;        // device copy of the context's class table (k_plan_fill)
 };
 
 }  // namespace
@@ -390,18 +425,19 @@ void rebuild_class_tables(jg_ctx* ctx) {
 
 // Reject a job list that names a key outside the table or a byte span outside
 // the arena (the prep kernel reads the device copy at those offsets).
-bool check_jobs(const jg_ctx* ctx, size_t arena_len, const jg_tok* toks, size_t ntok, std::string* err) {
+bool check_jobs(const jg_ctx* ctx, size_t arena_len, const jg_tok* toks, size_t ntok, std::string* err,
+                size_t base = 0) {
   const size_t nk = ctx->keys.size();
   for (size_t i = 0; i < ntok; ++i) {
     const jg_tok& t = toks[i];
     if (t.key_idx >= nk) {
-      *err = "jg_tok[" + std::to_string(i) + "].key_idx " + std::to_string(t.key_idx) +
+      *err = "jg_tok[" + std::to_string(base + i) + "].key_idx " + std::to_string(t.key_idx) +
              " out of range of the loaded key table (" + std::to_string(nk) + " keys)";
       return false;
     }
     if (t.off > arena_len || t.sig_in_len > arena_len - t.off ||
         (uint64_t)t.sig_rel_off + t.sig_b64_len > arena_len - t.off) {
-      *err = "jg_tok[" + std::to_string(i) + "]: signing input or signature span past the arena (" +
+      *err = "jg_tok[" + std::to_string(base + i) + "]: signing input or signature span past the arena (" +
              std::to_string(arena_len) + " bytes)";
       return false;
     }
@@ -413,72 +449,97 @@ inline uint64_t tok_end(const jg_tok& t) {
   return std::max<uint64_t>(t.off + t.sig_in_len, t.off + (uint64_t)t.sig_rel_off + t.sig_b64_len);
 }
 
-bool is_pinned(const void* p) {
-  if (!p) return false;
+// The device-visible address of page-locked host memory (hipHostMalloc /
+// hipHostRegister), or nullptr for pageable memory.
+const uint8_t* device_view(const void* p) {
+  if (!p) return nullptr;
   hipPointerAttribute_t a{};
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();      // clear the sticky "invalid value" of pageable memory
-    return false;
+    return nullptr;
   }
-  return a.type == hipMemoryTypeHost;
+  if (a.type != hipMemoryTypeHost) return nullptr;
+  if (a.devicePointer && a.hostPointer)        // attributes describe the allocation base
+    return (const uint8_t*)a.devicePointer + ((const uint8_t*)p - (const uint8_t*)a.hostPointer);
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, const_cast<void*>(p), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return (const uint8_t*)dp;
 }
 
-// Counting sort of toks[0..ntok) by (class, key): classes 1..NCLS-1 key by key,
-// then the reject bucket; every bucket padded to whole waves.  `alloc(npad)`
-// returns (perm, wave_key) storage for npad / npad/WAVE entries.
-template <class Alloc>
-void make_plan(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, Plan& P, std::vector<uint8_t>& tcls,
-               std::vector<int64_t>& cnt, std::vector<int64_t>& fill, Alloc&& alloc) {
-  const size_t nk = ctx->keys.size();
-  const size_t RB = nk;                                  // reject bucket
-  cnt.assign(nk + 1, 0);
-  tcls.resize(ntok);
-  for (int c = 0; c < NCLS; ++c) P.hash_mask[c] = P.pss_any[c] = 0;
+// Dispatch plan of toks[0..ntok): a counting sort by (class, key) --
+// classes 1..NCLS-1 key by key, then the reject bucket; every bucket padded
+// to whole waves.  plan_layout counts (the per-job host work of a pipeline
+// chunk) and fills X.start / X.total per bucket; the placement is done either
+// on the host (plan_fill_host: resident batches) or on the device
+// (k_plan_fill: pipeline chunks).
+// per-job part of plan_layout (one pass; `visit(i)` runs on every job too):
+// bucket counts into X.total, (class, alg) pairs seen into *seen (bit c*16+alg)
+template <class Visit>
+void plan_count(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, PlanScratch& X, bool keep_cls, uint64_t* seen,
+                Visit&& visit) {
+  const size_t nk = ctx->keys.size(), NB = nk + 1, RB = nk;
+  X.total.assign(NB, 0);
+  if (keep_cls) X.tcls.resize(ntok);
+  const uint8_t* ctab = ctx->cls_tab.data();
+  int64_t* tot = X.total.data();
+  uint64_t lo = 0, hi = 0;
   for (size_t i = 0; i < ntok; ++i) {
-    const jg_tok& t = toks[i];
-    const int c = classify(ctx, t);
-    tcls[i] = (uint8_t)c;
-    const int alg = t.alg;
-    P.hash_mask[c] |= (alg == JG_RS256 || alg == JG_PS256 || alg == JG_ES256) ? 1 : 2;
-    P.pss_any[c] |= alg >= JG_PS256 && alg <= JG_PS512;
-    cnt[c == CLS_REJECT ? RB : t.key_idx]++;
+    const jg_tok& tk = toks[i];
+    visit(i);
+    const unsigned alg = tk.alg;
+    const unsigned c = alg < NALG ? ctab[(size_t)tk.key_idx * NALG + alg] : CLS_REJECT;
+    if (keep_cls) X.tcls[i] = (uint8_t)c;
+    const unsigned combo = c * 16 + (alg & 15u);
+    if (combo < 64) lo |= 1ull << combo;
+    else hi |= 1ull << (combo - 64);
+    tot[c == CLS_REJECT ? RB : tk.key_idx]++;
   }
-  fill.assign(nk + 1, 0);
+  seen[0] = lo;
+  seen[1] = hi;
+}
+
+void plan_layout(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, Plan& P, PlanScratch& X, bool keep_cls,
+                 const uint64_t* seen_in = nullptr) {
+  const size_t nk = ctx->keys.size();
+  const size_t NB = nk + 1, RB = nk;
+  uint64_t seen[2];
+  if (seen_in) {
+    seen[0] = seen_in[0];
+    seen[1] = seen_in[1];
+  } else {
+    plan_count(ctx, toks, ntok, X, keep_cls, seen, [](size_t) {});
+  }
+  X.start.assign(NB, 0);
+  const int64_t* tot = X.total.data();
+  for (int c = 0; c < NCLS; ++c) {
+    P.hash_mask[c] = P.pss_any[c] = 0;
+    for (int alg = 0; alg < 16; ++alg) {
+      const unsigned combo = (unsigned)c * 16 + alg;
+      if (!((seen[combo >> 6] >> (combo & 63)) & 1)) continue;
+      P.hash_mask[c] |= (alg == JG_RS256 || alg == JG_PS256 || alg == JG_ES256) ? 1 : 2;
+      P.pss_any[c] |= alg >= JG_PS256 && alg <= JG_PS512;
+    }
+  }
   int64_t pos = 0;
   for (int c = 1; c <= NCLS; ++c) {
     const int cc = c % NCLS;
     P.ranges[cc].begin = pos;
     if (cc == CLS_REJECT) {
-      fill[RB] = pos;
-      pos += (cnt[RB] + WAVE - 1) / WAVE * WAVE;
+      X.start[RB] = pos;
+      pos += (tot[RB] + WAVE - 1) / WAVE * WAVE;
     } else {
       for (int32_t k : ctx->cls_keys[cc]) {
-        fill[(size_t)k] = pos;
-        pos += (cnt[(size_t)k] + WAVE - 1) / WAVE * WAVE;
+        X.start[(size_t)k] = pos;
+        pos += (tot[(size_t)k] + WAVE - 1) / WAVE * WAVE;
       }
     }
     P.ranges[cc].end = pos;
   }
   P.npad = pos > 0 ? pos : WAVE;
   P.ntok = (int64_t)ntok;
-  int32_t* perm;
-  int32_t* wkey;
-  alloc((size_t)P.npad, &perm, &wkey);
-  // padding lanes: the tail of each bucket's last wave
-  for (size_t b = 0; b <= nk; ++b) {
-    const int64_t e = fill[b] + cnt[b], pe = fill[b] + (cnt[b] + WAVE - 1) / WAVE * WAVE;
-    for (int64_t p = e; p < pe; ++p) perm[p] = -1;
-  }
-  if (pos == 0)
-    for (int64_t p = 0; p < WAVE; ++p) perm[p] = -1;
-  wkey[0] = 0;
-  for (size_t i = 0; i < ntok; ++i) {
-    const int c = tcls[i];
-    const size_t b = c == CLS_REJECT ? RB : toks[i].key_idx;
-    const int64_t p = fill[b]++;
-    perm[p] = (int32_t)i;
-    wkey[p / WAVE] = c == CLS_REJECT ? 0 : toks[i].key_idx;
-  }
   P.sig_rows = 1;
   P.scratch_rows = 1;
   P.pss_tokens = 0;
@@ -493,14 +554,44 @@ void make_plan(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, Plan& P, std:
   }
 }
 
+// padding lanes of bucket b: [lo, hi); the empty plan is one wave of padding
+inline std::pair<int64_t, int64_t> pad_range(const PlanScratch& X, size_t b, const Plan& P, size_t RB) {
+  if (P.npad == WAVE && X.start[RB] == 0 && b == RB) {
+    int64_t any = 0;
+    for (int64_t t : X.total) any += t;
+    if (any == 0) return {0, WAVE};
+  }
+  return {X.start[b] + X.total[b], X.start[b] + (X.total[b] + WAVE - 1) / WAVE * WAVE};
+}
+
+// Host placement (resident batches): JobDev array + perm in padded order.
+void plan_fill_host(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, const Plan& P, PlanScratch& X, JobDev* jobs,
+                    int32_t* perm) {
+  const size_t nk = ctx->keys.size(), NB = nk + 1, RB = nk;
+  for (size_t b = 0; b < NB; ++b) {
+    const auto r = pad_range(X, b, P, RB);
+    const JobDev pad{0, 0, 0, job_pack(b == RB ? 0u : (uint32_t)b, JOB_PAD, 0)};
+    for (int64_t p = r.first; p < r.second; ++p) {
+      jobs[p] = pad;
+      perm[p] = -1;
+    }
+  }
+  std::vector<int64_t> cur = X.start;
+  for (size_t i = 0; i < ntok; ++i) {
+    const jg_tok& tk = toks[i];
+    const int c = X.tcls[i];
+    const int64_t p = cur[c == CLS_REJECT ? RB : tk.key_idx]++;
+    jobs[p] = JobDev{(uint32_t)tk.off, tk.sig_in_len, (uint32_t)(tk.off + tk.sig_rel_off),
+                     job_pack(c == CLS_REJECT ? 0u : tk.key_idx, tk.alg, tk.sig_b64_len)};
+    perm[p] = (int32_t)i;
+  }
+}
+
 // device scratch of a plan (inputs are copied by the caller)
-void size_bufs(Bufs* B, const Plan& P, size_t arena_bytes) {
+void size_scratch(Bufs* B, const Plan& P, size_t arena_bytes) {
   const int64_t npad = P.npad;
   const size_t ntok = std::max<size_t>((size_t)P.ntok, 1);
   B->arena.get(arena_bytes + ARENA_SLACK);
-  B->toks.get(sizeof(jg_tok) * ntok);
-  B->perm.get(sizeof(int32_t) * npad);
-  B->wave_key.get(sizeof(int32_t) * (npad / WAVE));
   B->sigw.get(sizeof(uint32_t) * P.sig_rows * npad);
   B->dig.get(sizeof(uint32_t) * DIG_ROWS * npad);
   B->status.get(npad);
@@ -513,16 +604,30 @@ void size_bufs(Bufs* B, const Plan& P, size_t arena_bytes) {
   B->exc_cnt.get(sizeof(uint32_t) * NCLS);
 }
 
-void upload(Bufs* B, hipStream_t s, const Plan& P, const uint8_t* arena, size_t arena_bytes, const jg_tok* toks,
-            const int32_t* perm, const int32_t* wkey) {
-  size_bufs(B, P, arena_bytes);
+// resident batch: arena (slack zeroed), jobs and perm placed by the host
+void upload(Bufs* B, hipStream_t s, const Plan& P, const uint8_t* arena, size_t arena_bytes, const JobDev* jobs,
+            const int32_t* perm) {
+  size_scratch(B, P, arena_bytes);
+  B->jobs.get(sizeof(JobDev) * P.npad);
+  B->perm.get(sizeof(int32_t) * P.npad);
   uint8_t* da = (uint8_t*)B->arena.p;
   if (arena_bytes && arena) HIPCHK(hipMemcpyAsync(da, arena, arena_bytes, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(da + arena_bytes, 0, ARENA_SLACK, s));
-  if (P.ntok) HIPCHK(hipMemcpyAsync(B->toks.p, toks, sizeof(jg_tok) * P.ntok, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(B->jobs.p, jobs, sizeof(JobDev) * P.npad, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(B->perm.p, perm, sizeof(int32_t) * P.npad, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(B->wave_key.p, wkey, sizeof(int32_t) * (P.npad / WAVE), hipMemcpyHostToDevice, s));
 }
+
+// Plan block of a pipeline chunk (pinned staging and its device copy alike):
+// bucket cursors | padding ranges | the chunk's jg_tok jobs in caller order.
+struct PlanBlock {
+  size_t cur_off, pad_off, toks_off, bytes;
+  PlanBlock(size_t nbuckets, size_t n) {
+    cur_off = 0;
+    pad_off = sizeof(uint64_t) * nbuckets;
+    toks_off = (pad_off + 2 * sizeof(int64_t) * nbuckets + 63) & ~size_t(63);
+    bytes = toks_off + sizeof(jg_tok) * std::max<size_t>(n, 1);
+  }
+};
 
 // ---------------------------------------------------------------- timing marks
 void mark(jg_batch* b, const char* name) {
@@ -577,9 +682,7 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
   HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, s0));
   PrepArgs pa{};
   pa.arena = (const uint8_t*)B->arena.p;
-  pa.toks = (const jg_tok_dev*)B->toks.p;
-  pa.perm = (const int32_t*)B->perm.p;
-  pa.wave_key = (const int32_t*)B->wave_key.p;
+  pa.jobs = (const JobDev*)B->jobs.p;
   pa.keys = d->dkeys;
   pa.keyblob = d->dblob;
   pa.sigw = (uint32_t*)B->sigw.p;
@@ -606,7 +709,7 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
     mark(marks, (std::string(cls_name(c)) + "_prep").c_str());
     if (c <= CLS_RSA4K) {
       RsaArgs ra{};
-      ra.toks = pa.toks; ra.perm = pa.perm; ra.wave_key = pa.wave_key; ra.keys = pa.keys; ra.keyblob = pa.keyblob;
+      ra.jobs = pa.jobs; ra.keys = pa.keys; ra.keyblob = pa.keyblob;
       ra.sigw = pa.sigw; ra.dig = pa.dig;
       const int Lm = rsa_limbs(c);
       ra.xmw = rows;
@@ -620,7 +723,7 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
     } else if (c <= CLS_P521) {
       if (!d->gtab[c]) throw std::runtime_error("curve table missing");
       EcArgs ea{};
-      ea.toks = pa.toks; ea.perm = pa.perm; ea.wave_key = pa.wave_key; ea.keys = pa.keys; ea.keyblob = pa.keyblob;
+      ea.jobs = pa.jobs; ea.keys = pa.keys; ea.keyblob = pa.keyblob;
       ea.sigw = pa.sigw; ea.dig = pa.dig; ea.status = pa.status; ea.verdict_pad = (uint8_t*)B->vpad.p;
       ea.digs = rows;
       ea.u1w = rows + (size_t)ec_digit_rows(c) * np;
@@ -633,7 +736,7 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
     } else {
       if (!d->btab) throw std::runtime_error("Ed25519 base table missing");
       EdArgs ea{};
-      ea.perm = pa.perm; ea.wave_key = pa.wave_key; ea.keys = pa.keys; ea.keyblob = pa.keyblob;
+      ea.jobs = pa.jobs; ea.keys = pa.keys; ea.keyblob = pa.keyblob;
       ea.sigw = pa.sigw; ea.dig = pa.dig; ea.status = pa.status; ea.siglen = pa.siglen;
       ea.verdict_pad = (uint8_t*)B->vpad.p;
       ea.xyz = rows;
@@ -677,8 +780,8 @@ void finish_slot(Slot& S) {
     (void)hipEventElapsedTime(&b, g_trace_ref, S.tr_b);
     (void)hipEventElapsedTime(&c, g_trace_ref, S.tr_c);
     (void)hipEventElapsedTime(&dn, g_trace_ref, S.done);
-    std::fprintf(stderr, "[pipe] chunk %3d n=%7zu host wait %.3f plan %.3f enq %.3f | gpu h2d %.3f-%.3f kern-end %.3f done %.3f ms\n",
-                 S.chunk_no, S.n, S.host_ms[0], S.host_ms[1], S.host_ms[2], a, b, c, dn);
+    std::fprintf(stderr, "[pipe] chunk %3d n=%7zu host wait %.3f plan %.3f enq %.3f (h2d calls %.3f) | gpu h2d %.3f-%.3f kern-end %.3f done %.3f ms\n",
+                 S.chunk_no, S.n, S.host_ms[0], S.host_ms[1], S.host_ms[2], S.host_ms[3], a, b, c, dn);
   }
   S.inflight = false;
   auto t = std::move(S.ticket);
@@ -686,75 +789,108 @@ void finish_slot(Slot& S) {
   t->done_chunks(1);
 }
 
-bool slot_ready(Slot& S) {
-  if (!S.inflight) return true;
-  const hipError_t e = hipEventQuery(S.done);
-  if (e == hipErrorNotReady) return false;
-  if (e != hipSuccess) (void)hipGetLastError();
-  return true;
-}
 
 // Plan and enqueue one chunk toks[0..n) of an item on slot S.
 void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok* toks, size_t n, uint8_t* out) {
   const auto t_start = std::chrono::steady_clock::now();
-  // arena span of the chunk's jobs; DMA it straight from a pinned caller
-  // arena when it is compact, else repack the jobs' bytes into pinned staging
-  uint64_t amin = UINT64_MAX, amax = 0, need = 0;
-  for (size_t i = 0; i < n; ++i) {
-    const uint64_t e = tok_end(toks[i]);
-    amin = std::min<uint64_t>(amin, toks[i].off);
+  // One pass over the caller's jobs: the arena span they use, the bucket
+  // counts of the plan, and their copy into the pinned plan block.  The span
+  // is DMAed straight from a pinned caller arena when it is compact, else
+  // repacked job by job into pinned staging.
+  const size_t NB = ctx->keys.size() + 1;
+  const PlanBlock L(NB, n);
+  uint8_t* hb = (uint8_t*)S.h_meta.get(L.bytes);
+  jg_tok* ht = (jg_tok*)(hb + L.toks_off);
+  uint64_t amin = UINT64_MAX, amax = 0, need = 0, seen[2];
+  plan_count(ctx, toks, n, d->plan, false, seen, [&](size_t i) {
+    const jg_tok& t = toks[i];
+    const uint64_t e = tok_end(t);
+    amin = std::min<uint64_t>(amin, t.off);
     amax = std::max<uint64_t>(amax, e);
-    need += e - toks[i].off;
-  }
+    need += e - t.off;
+    ht[i] = t;
+  });
   if (n == 0) amin = amax = 0;
   const uint64_t base = amin & ~uint64_t(255);
   const uint64_t span = amax - base;
-  const bool compact = span <= 2 * need + 65536;
-  jg_tok* jt = (jg_tok*)S.h_toks.get(sizeof(jg_tok) * std::max<size_t>(n, 1));
+  // JobDev offsets are 32-bit: a span that does not fit is repacked
+  const bool compact = span <= 2 * need + 65536 && span < (uint64_t(1) << 32) - ARENA_SLACK;
   const uint8_t* src;
   size_t bytes;
+  uint64_t dbase;                                  // subtracted from job offsets on the device
   if (compact) {
-    for (size_t i = 0; i < n; ++i) {
-      jt[i] = toks[i];
-      jt[i].off -= base;
-    }
     bytes = (size_t)span;
-    if (it.pinned) {
-      src = it.arena + base;
+    dbase = base;
+    if (it.dev_arena) {
+      src = it.dev_arena + base;
     } else {
       uint8_t* h = (uint8_t*)S.h_arena.get(bytes);
       std::memcpy(h, it.arena + base, bytes);
-      src = h;
+      src = (const uint8_t*)S.h_arena.dp;
     }
   } else {
+    if (need + 4 * n >= (uint64_t(1) << 32) - ARENA_SLACK)
+      throw std::runtime_error("a pipeline chunk's jobs span 4 GiB or more of arena: lower jg_set_chunk");
     uint8_t* h = (uint8_t*)S.h_arena.get((size_t)need + 4 * n);
     uint64_t pos = 0;
     for (size_t i = 0; i < n; ++i) {
       const uint64_t len = tok_end(toks[i]) - toks[i].off;
       std::memcpy(h + pos, it.arena + toks[i].off, len);
-      jt[i] = toks[i];
-      jt[i].off = pos;
+      ht[i].off = pos;
       pos += (len + 3) & ~uint64_t(3);
     }
     bytes = (size_t)pos;
-    src = h;
+    dbase = 0;
+    src = (const uint8_t*)S.h_arena.dp;
   }
   Plan P;
-  make_plan(ctx, jt, n, P, d->tcls, d->cnt, d->fill, [&](size_t npad, int32_t** perm, int32_t** wkey) {
-    *perm = (int32_t*)S.h_perm.get(sizeof(int32_t) * npad);
-    *wkey = (int32_t*)S.h_wkey.get(sizeof(int32_t) * (npad / WAVE));
-  });
-  const hipStream_t s = S.lane.stream;
+  plan_layout(ctx, ht, n, P, d->plan, false, seen);
+  uint64_t* cur = (uint64_t*)(hb + L.cur_off);
+  int64_t* pad = (int64_t*)(hb + L.pad_off);
+  for (size_t k = 0; k < NB; ++k) {
+    const auto r = pad_range(d->plan, k, P, NB - 1);
+    cur[k] = (uint64_t)d->plan.start[k];
+    pad[2 * k] = r.first;
+    pad[2 * k + 1] = r.second;
+  }
+  Lane& LN = d->lanes[d->next_lane];
+  d->next_lane = (d->next_lane + 1) % NLANE;
+  const hipStream_t s = LN.stream;
   const bool tr = pipe_trace();
   S.host_ms[1] = tr ? ms_since(t_start) : 0.0;
   const auto t_enq = std::chrono::steady_clock::now();
+  // Everything of the chunk on one compute lane, no DMA-engine copies: the
+  // arena span and the plan block's cursors are pulled from pinned host
+  // memory by a copy kernel, k_plan_fill reads the jobs straight from the
+  // pinned plan block, and the verdicts go back by a copy kernel.
+  size_scratch(&S.bufs, P, bytes);
+  S.bufs.jobs.get(sizeof(JobDev) * P.npad);
+  S.bufs.perm.get(sizeof(int32_t) * P.npad);
+  uint8_t* dm = (uint8_t*)S.bufs.meta.get(L.toks_off);
+  const uint8_t* hbd = (const uint8_t*)S.h_meta.dp;
   if (tr) HIPCHK(hipEventRecord(S.tr_a, s));
-  upload(&S.bufs, s, P, src, bytes, jt, (const int32_t*)S.h_perm.p, (const int32_t*)S.h_wkey.p);
+  launch_copy(src, S.bufs.arena.p, bytes, s);
+  launch_copy(hbd, dm, L.toks_off, s);
   if (tr) HIPCHK(hipEventRecord(S.tr_b, s));
-  run_plan(d, &S.lane, &S.bufs, P, nullptr);
+  if (tr) S.host_ms[3] = ms_since(t_enq);
+  {
+    PlanFillArgs fa{};
+    fa.toks = (const jg_tok*)(hbd + L.toks_off);
+    fa.n = (int64_t)n;
+    fa.base = dbase;
+    fa.cls_tab = d->dcls;
+    fa.nkeys = (int32_t)(NB - 1);
+    fa.cursor = (unsigned long long*)(dm + L.cur_off);
+    fa.pad = (const int64_t*)(dm + L.pad_off);
+    fa.jobs = (JobDev*)S.bufs.jobs.p;
+    fa.perm = (int32_t*)S.bufs.perm.p;
+    launch_plan_fill(fa, s);
+  }
+  run_plan(d, &LN, &S.bufs, P, nullptr);
   if (tr) HIPCHK(hipEventRecord(S.tr_c, s));
-  uint8_t* hv = (uint8_t*)S.h_verdict.get(std::max<size_t>(n, 1));
-  if (n) HIPCHK(hipMemcpyAsync(hv, S.bufs.verdict.p, n, hipMemcpyDeviceToHost, s));
+  S.h_verdict.get(std::max<size_t>(n, 1));
+  launch_copy(S.bufs.verdict.p, S.h_verdict.dp, n, s);
+  HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(S.done, s));
   if (tr) S.host_ms[2] = ms_since(t_enq);
   S.ticket = it.t;
@@ -770,13 +906,17 @@ void process_item(jg_ctx* ctx, Device* d, Item& it) {
     HIPCHK(hipSetDevice(d->id));
     if (ctx->failed || ctx->epoch != it.epoch)
       throw std::runtime_error("key table reloaded (or its load failed) while the batch was queued");
-    const size_t C = it.chunk;
     if (pipe_trace()) {
       if (!g_trace_ref) HIPCHK(hipEventCreate(&g_trace_ref));
-      HIPCHK(hipEventRecord(g_trace_ref, d->slots[d->next_slot].lane.stream));
+      HIPCHK(hipEventRecord(g_trace_ref, d->lanes[d->next_lane].stream));
     }
-    for (size_t lo = it.lo; lo < it.hi; lo += C) {
-      const size_t hi = std::min(it.hi, lo + C);
+    for (size_t c = 0; c + 1 < it.cuts.size(); ++c) {
+      const size_t lo = it.cuts[c], hi = it.cuts[c + 1];
+      std::string bad;
+      if (!check_jobs(ctx, it.arena_len, it.toks + lo, hi - lo, &bad, lo)) {
+        it.t->fail(-1, bad);
+        break;
+      }
       Slot& S = d->slots[d->next_slot];
       d->next_slot = (d->next_slot + 1) % NSLOT;
       const auto tw = std::chrono::steady_clock::now();
@@ -787,6 +927,7 @@ void process_item(jg_ctx* ctx, Device* d, Item& it) {
       S.chunk_no = (int)enq;
       ++enq;
     }
+    if (enq < it.nchunks) it.t->done_chunks(it.nchunks - enq);
   } catch (const std::exception& e) {
     it.t->fail(-2, e.what());
     it.t->done_chunks(it.nchunks - enq);
@@ -806,7 +947,8 @@ void worker_loop(jg_ctx* ctx, Device* d) {
       lk.lock();
       continue;
     }
-    // queue empty: complete finished chunks, wait for in-flight ones (or new work)
+    // queue empty: complete the in-flight chunks oldest first (blocking on
+    // each; a submission arriving meanwhile is picked up after that chunk)
     bool any = false;
     lk.unlock();
     {
@@ -814,15 +956,13 @@ void worker_loop(jg_ctx* ctx, Device* d) {
       for (int k = 0; k < NSLOT; ++k) {
         Slot& S = d->slots[(d->next_slot + k) % NSLOT];    // oldest first
         if (!S.inflight) continue;
-        if (slot_ready(S)) finish_slot(S);
-        else any = true;
+        finish_slot(S);
+        any = true;
+        break;
       }
     }
     lk.lock();
-    if (any) {
-      d->qcv.wait_for(lk, std::chrono::microseconds(50));
-      continue;
-    }
+    if (any) continue;
     if (d->q.empty()) {
       d->busy = false;
       d->idle_cv.notify_all();
@@ -991,7 +1131,8 @@ void load_keys_device(Device* d, const StagedKeys& S) {
   HIPCHK(hipSetDevice(d->id));
   hipStream_t s = d->lane0.stream;
   d->lane0.sync();
-  for (auto& sl : d->slots) sl.lane.sync();
+  if (d->copy) (void)hipStreamSynchronize(d->copy);
+  for (auto& ln : d->lanes) ln.sync();
   if (d->dkeys) (void)hipFree(d->dkeys);
   if (d->didx) (void)hipFree(d->didx);
   d->dkeys = nullptr; d->didx = nullptr;
@@ -1056,6 +1197,7 @@ void load_keys_device(Device* d, const StagedKeys& S) {
 
 thread_local std::string g_tls_err;
 
+
 // Split jobs [0, ntok) over the context's devices by the cost model and queue
 // each device's share.  Caller holds key_mu (shared) and has validated the jobs.
 std::shared_ptr<Ticket> submit_locked(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok* toks,
@@ -1066,7 +1208,9 @@ std::shared_ptr<Ticket> submit_locked(jg_ctx* ctx, const uint8_t* arena, size_t 
   cut[nd] = ntok;
   if (nd > 1) {
     std::vector<double> pre(ntok + 1, 0.0);
-    for (size_t i = 0; i < ntok; ++i) pre[i + 1] = pre[i] + cls_cost(classify(ctx, toks[i]));
+    const size_t nk = ctx->keys.size();
+    for (size_t i = 0; i < ntok; ++i)
+      pre[i + 1] = pre[i] + (toks[i].key_idx < nk ? cls_cost(classify(ctx, toks[i])) : 0.0);
     size_t j = 0;
     for (size_t k = 1; k < nd; ++k) {
       const double target = pre[ntok] * (double)k / (double)nd;
@@ -1074,7 +1218,7 @@ std::shared_ptr<Ticket> submit_locked(jg_ctx* ctx, const uint8_t* arena, size_t 
       cut[k] = j;
     }
   }
-  const bool pinned = is_pinned(arena);
+  const uint8_t* dview = device_view(arena);
   const size_t C = ctx->chunk.load();
   std::vector<Item> items;
   for (size_t k = 0; k < nd; ++k) {
@@ -1088,9 +1232,10 @@ std::shared_ptr<Ticket> submit_locked(jg_ctx* ctx, const uint8_t* arena, size_t 
     it.hi = cut[k + 1];
     it.out = out;
     it.epoch = ctx->epoch;
-    it.pinned = pinned;
+    it.dev_arena = dview;
     it.chunk = C;
-    it.nchunks = (it.hi - it.lo + C - 1) / C;
+    it.cuts = chunk_cuts(it.lo, it.hi, C);
+    it.nchunks = it.cuts.size() - 1;
     t->pending += it.nchunks;
     items.push_back(std::move(it));
   }
@@ -1132,10 +1277,14 @@ jg_ctx* jg_create(const int* devices, int ndev) {
       auto d = std::make_unique<Device>();
       d->id = id;
       HIPCHK(hipSetDevice(id));
-      d->lane0.create();
+      HIPCHK(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
+      for (auto& l : d->lanes) l.create_main();
+      d->lane0.create_main();
+      for (auto& l : d->lanes) l.create_fanout();
+      d->lane0.create_fanout();
       for (auto& s : d->slots) {
-        s.lane.create();
         HIPCHK(hipEventCreateWithFlags(&s.done, pipe_trace() ? hipEventDefault : hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
         HIPCHK(hipEventCreate(&s.tr_a));
         HIPCHK(hipEventCreate(&s.tr_b));
         HIPCHK(hipEventCreate(&s.tr_c));
@@ -1163,17 +1312,22 @@ void jg_destroy(jg_ctx* ctx) {
   }
   for (auto& d : ctx->devs) {
     (void)hipSetDevice(d->id);
+    for (auto& l : d->lanes) l.destroy();
     for (auto& s : d->slots) {
-      s.lane.destroy();
       if (s.done) (void)hipEventDestroy(s.done);
-      for (hipEvent_t e : {s.tr_a, s.tr_b, s.tr_c})
+      for (hipEvent_t e : {s.tr_a, s.tr_b, s.tr_c, s.copied})
         if (e) (void)hipEventDestroy(e);
     }
     d->lane0.sync();
+    if (d->copy) {
+      (void)hipStreamSynchronize(d->copy);
+      (void)hipStreamDestroy(d->copy);
+    }
     for (auto& t : d->tab_ref) t.reset();         // shared fixed-base tables: last holder frees
     if (d->dkeys) (void)hipFree(d->dkeys);
     if (d->dblob) (void)hipFree(d->dblob);
     if (d->didx) (void)hipFree(d->didx);
+    if (d->dcls) (void)hipFree(d->dcls);
     d->lane0.destroy();
   }
   delete ctx;
@@ -1212,6 +1366,14 @@ int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys) {
     }
     ctx->keys = std::move(hk);
     rebuild_class_tables(ctx);
+    for (auto& d : ctx->devs) {
+      HIPCHK(hipSetDevice(d->id));
+      if (d->dcls) (void)hipFree(d->dcls);
+      d->dcls = nullptr;
+      HIPCHK(hipMalloc(&d->dcls, std::max<size_t>(ctx->cls_tab.size(), 16)));
+      if (!ctx->cls_tab.empty())
+        HIPCHK(hipMemcpy(d->dcls, ctx->cls_tab.data(), ctx->cls_tab.size(), hipMemcpyHostToDevice));
+    }
     ctx->failed = false;
     ++ctx->epoch;
     if (!warn.empty()) ctx->set_err(warn);
@@ -1234,8 +1396,8 @@ int jg_submit(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok*
     }
     std::shared_lock<std::shared_mutex> kl(ctx->key_mu);
     if (ctx->failed) { ctx->set_err("the last jg_keys_load failed; no key table is loaded"); return -2; }
-    std::string err;
-    if (!check_jobs(ctx, arena_len, toks, ntok, &err)) { ctx->set_err(err); return -1; }
+    // jobs are validated chunk by chunk by the device workers, ahead of each
+    // chunk's upload (a bad job fails the ticket with -1 from jg_wait)
     auto t = submit_locked(ctx, arena, arena_len, toks, ntok, verdict_out);
     *out = new jg_ticket{std::move(t)};
     return 0;
@@ -1284,16 +1446,18 @@ int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t ar
     b->b = b->own.get();
     std::lock_guard<std::mutex> g(b->dev->mu);
     HIPCHK(hipSetDevice(b->dev->id));
-    std::vector<uint8_t> tcls;
-    std::vector<int64_t> cnt, fill;
-    std::vector<int32_t> perm, wkey;
-    make_plan(ctx, toks, ntok, b->plan, tcls, cnt, fill, [&](size_t npad, int32_t** p, int32_t** w) {
-      perm.resize(npad);
-      wkey.resize(npad / WAVE);
-      *p = perm.data();
-      *w = wkey.data();
-    });
-    upload(b->b, b->lane->stream, b->plan, arena, arena_len, toks, perm.data(), wkey.data());
+    PlanScratch X;
+    if (arena_len >= (uint64_t(1) << 32) - ARENA_SLACK) {
+      ctx->set_err("a resident batch's arena must be smaller than 4 GiB");
+      return -1;
+    }
+    std::vector<JobDev> jobs;
+    std::vector<int32_t> perm;
+    plan_layout(ctx, toks, ntok, b->plan, X, true);
+    jobs.resize(b->plan.npad);
+    perm.resize(b->plan.npad);
+    plan_fill_host(ctx, toks, ntok, b->plan, X, jobs.data(), perm.data());
+    upload(b->b, b->lane->stream, b->plan, arena, arena_len, jobs.data(), perm.data());
     // the host vectors die here: the copies above must complete first
     HIPCHK(hipStreamSynchronize(b->lane->stream));
     b->arena_len = arena_len;

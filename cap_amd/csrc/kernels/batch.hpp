@@ -3,4 +3,31 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "../../../include/jg.h"
+#include "common.hpp"
+
 void launch_scatter(const int32_t* perm, const uint8_t* verdict_pad, uint8_t* verdict, int64_t npad, hipStream_t s);
+
+// Device half of a pipeline chunk's dispatch plan.  The host counts jobs per
+// bucket (kernel class x key; the reject bucket last) and sends the bucket
+// cursors and padding ranges; this kernel places every caller job into the
+// padded (class, key)-sorted order as a 16-byte JobDev and writes perm.
+struct PlanFillArgs {
+  const jg_tok* toks;               // the chunk's jobs in caller order
+  int64_t n;
+  uint64_t base;                    // arena offset of the chunk's device copy
+  const uint8_t* cls_tab;           // [key * 16 + alg] -> kernel class (0 = reject)
+  int32_t nkeys;
+  unsigned long long* cursor;       // [nkeys + 1]: next padded index of each bucket
+  const int64_t* pad;               // [nkeys + 1][2]: padding lanes [lo, hi) of each bucket
+  jgk::JobDev* jobs;
+  int32_t* perm;
+};
+void launch_plan_fill(const PlanFillArgs& a, hipStream_t s);
+
+// Stream `bytes` from src to dst with a kernel (16 B per lane where both ends
+// are 16-byte aligned, bytes otherwise): the pipeline moves every chunk
+// between pinned host memory and HBM this way, through the kernel's own PCIe
+// reads / writes, not through the DMA engines (whose command queue stalled
+// the host for ~1 ms every few chunks, profiles/r02_pipe_*).
+void launch_copy(const void* src, void* dst, size_t bytes, hipStream_t s);

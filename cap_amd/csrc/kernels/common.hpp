@@ -29,6 +29,27 @@ constexpr int SIGW_ROWS = 132;      // decoded signature, up to 528 bytes (RSA-4
 constexpr int EC_S_ROW = 32;        // ECDSA: s starts at row 32 (r at row 0)
 constexpr int DIG_ROWS = 16;        // digest, big-endian 32-bit words
 
+// One (token, key) verification job as the kernels read it: in the padded,
+// (class, key)-sorted order of the dispatch plan, so lane p of a launch reads
+// jobs[p] (coalesced) and every wave's jobs share one key.  Padding lanes
+// carry alg JOB_PAD and the wave's key.  Offsets are byte offsets into the
+// device copy of the batch's (or chunk's) arena.
+constexpr uint32_t JOB_PAD = 15;      // alg of a padding lane (jg_alg ids are 0..10)
+constexpr uint32_t JOB_SIGLEN_MAX = 4095;   // longer signatures are clamped (rejected either way)
+struct JobDev {
+  uint32_t off;          // signing input
+  uint32_t sig_in_len;   // bytes hashed
+  uint32_t sig_off;      // base64url signature
+  uint32_t meta;         // bits 0-15 key index, 16-19 alg, 20-31 signature length (chars)
+};
+__host__ __device__ inline uint32_t job_pack(uint32_t key, uint32_t alg, uint32_t siglen) {
+  return (key & 0xffffu) | ((alg & 15u) << 16) | ((siglen < JOB_SIGLEN_MAX ? siglen : JOB_SIGLEN_MAX) << 20);
+}
+__host__ __device__ inline int job_key(const JobDev& j) { return (int)(j.meta & 0xffffu); }
+__host__ __device__ inline int job_alg(const JobDev& j) { return (int)((j.meta >> 16) & 15u); }
+__host__ __device__ inline uint32_t job_siglen(const JobDev& j) { return j.meta >> 20; }
+__host__ __device__ inline bool job_live(const JobDev& j) { return job_alg(j) != (int)JOB_PAD; }
+
 // Device view of one loaded key (arrays live in the key blob, word offsets).
 struct DevKey {
   int32_t kind;        // jg_key_kind

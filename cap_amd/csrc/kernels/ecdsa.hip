@@ -62,15 +62,15 @@ __device__ __forceinline__ bool ec_scalar_inputs(const EcArgs& a, int64_t p, uin
   constexpr int L = Fn::L;
   constexpr int CB = CV::C::BYTES;
   const int64_t np = a.npad;
-  const int32_t t = a.perm[p];
-  if (t < 0) {
+  const JobDev jb = a.jobs[p];
+  if (!job_live(jb)) {
 #pragma unroll
     for (int j = 0; j < L; ++j) { r[j] = 0; e[j] = 0; s[j] = j == 0 ? 1u : 0u; }
     return false;
   }
-  const int kidx = a.wave_key[p / WAVE];
+  const int kidx = job_key(jb);
   bool ok = a.status[p] == ST_OK && a.keys[kidx].valid;
-  const int alg = a.toks[t].alg;
+  const int alg = job_alg(jb);
   uint32_t rw[17], sw[17];
 #pragma unroll
   for (int q = 0; q < 17; ++q) {
@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(64) k_ec_scalar_batch(EcArgs a, int B) {
     if (p >= a.end) break;
     uint32_t r[L], s[L], e[L], sm[L];
     const bool ok = ec_scalar_inputs<CV>(a, p, r, s, e);
-    if (!ok && a.perm[p] >= 0) a.status[p] = ST_REJECT;
+    if (!ok && job_live(a.jobs[p])) a.status[p] = ST_REJECT;
     mp::to_mont<Fn>(sm, s);
     mp::mul<Fn>(acc, acc, sm);
 #pragma unroll
@@ -291,10 +291,10 @@ __global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
   constexpr int NWIN = NG > NQ ? NG : NQ;
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
-  const int32_t t = a.perm[p];
-  if (t < 0) return;
+  const JobDev jb = a.jobs[p];
+  if (!job_live(jb)) return;
   if (a.status[p] != ST_OK) { a.verdict_pad[p] = 0; return; }
-  const int kidx = __builtin_amdgcn_readfirstlane(a.wave_key[p / WAVE]);
+  const int kidx = __builtin_amdgcn_readfirstlane(job_key(jb));
   const uint32_t* __restrict__ qtab = a.keyblob + a.keys[kidx].tab_off;
   const uint32_t* __restrict__ gtab = a.gtab;
 
@@ -435,7 +435,7 @@ __global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
     const int64_t p = a.exc_list[i];
     const int64_t np = a.npad;
-    const int kidx = a.wave_key[p / WAVE];
+    const int kidx = job_key(a.jobs[p]);
     const uint32_t* aux = a.keyblob + a.keys[kidx].aux_off;
     uint32_t u1[L], u2[L];
 #pragma unroll

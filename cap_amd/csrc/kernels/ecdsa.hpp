@@ -7,9 +7,7 @@
 #include "prep.hpp"
 
 struct EcArgs {
-  const jg_tok_dev* toks;
-  const int32_t* perm;
-  const int32_t* wave_key;
+  const jgk::JobDev* jobs;
   const jgk::DevKey* keys;
   const uint32_t* keyblob;
   const uint32_t* sigw;       // r at rows 0.., s at rows EC_S_ROW.. (LE words)

@@ -98,9 +98,9 @@ __device__ __forceinline__ void recode(int* dg, const uint32_t* s) {
 __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
-  const int32_t t = a.perm[p];
-  if (t < 0) return;
-  const int kidx = __builtin_amdgcn_readfirstlane(a.wave_key[p / WAVE]);
+  const JobDev jb = a.jobs[p];
+  if (!job_live(jb)) return;
+  const int kidx = __builtin_amdgcn_readfirstlane(job_key(jb));
   const DevKey& K = a.keys[kidx];
   bool ok = a.status[p] == ST_OK && K.valid && a.siglen[p] == 64;
   // S: canonical, and sig[63] & 0xE0 == 0
@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(64) k_ed_finish(EdArgs a, int B) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= S) return;
   uint32_t* pre = a.xyz + (int64_t)3 * L * np;
-  auto live = [&](int64_t p) { return a.perm[p] >= 0 && a.status[p] == ST_OK; };
+  auto live = [&](int64_t p) { return job_live(a.jobs[p]) && a.status[p] == ST_OK; };
   auto load_z = [&](int64_t p, uint32_t* Z) {
     if (live(p)) {
 #pragma unroll
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(64) k_ed_finish(EdArgs a, int B) {
     load_z(p, Z);
     mp::mul<Fp>(zi, inv, cprev);                 // Z_j^-1 (Montgomery)
     mp::mul<Fp>(inv, inv, Z);
-    if (a.perm[p] < 0) continue;
+    if (!job_live(a.jobs[p])) continue;
     if (a.status[p] != ST_OK) { a.verdict_pad[p] = 0; continue; }
     uint32_t X[L], Y[L], x[L], y[L], tt[L];
 #pragma unroll

@@ -7,8 +7,7 @@
 #include "prep.hpp"
 
 struct EdArgs {
-  const int32_t* perm;
-  const int32_t* wave_key;
+  const jgk::JobDev* jobs;
   const jgk::DevKey* keys;
   const uint32_t* keyblob;
   const uint32_t* sigw;       // R at rows 0..7, S at rows 8..15 (LE words)

@@ -93,19 +93,17 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   const int lane = threadIdx.x;
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + lane;
   const int64_t np = a.npad;
-  const int32_t t = a.perm[p];
-  const bool valid = t >= 0;
+  const JobDev jb = a.jobs[p];
+  const bool valid = job_live(jb);
   uint32_t* sigw = a.sigw;
   uint32_t* dig = a.dig;
   const uint32_t* arena_w = reinterpret_cast<const uint32_t*>(a.arena);
   const uint32_t* my = slots + lane * SLOT;
-  jg_tok_dev tk{};
-  if (valid) tk = a.toks[t];
-  const int alg = tk.alg;
+  const int alg = valid ? job_alg(jb) : 0;
   uint8_t st = valid ? ST_OK : ST_REJECT;
 
   // ---- base64url decode of the signature segment
-  const uint32_t n = tk.sig_b64_len;
+  const uint32_t n = valid ? job_siglen(jb) : 0u;
   uint32_t D;
   if ((n & 3u) == 1u) { st = ST_REJECT; D = 0; }
   else D = (n >> 2) * 3u + ((n & 3u) == 2u ? 1u : (n & 3u) == 3u ? 2u : 0u);
@@ -148,7 +146,7 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   b64tab[128 + lane] = (int8_t)b64val(128u + lane);
   b64tab[192 + lane] = (int8_t)b64val(192u + lane);    // made visible by stage()'s first barrier
 
-  const uint64_t sbyte = tk.off + tk.sig_rel_off;
+  const uint64_t sbyte = valid ? jb.sig_off : 0u;
   const uint64_t sw0 = sbyte >> 2;                     // arena dword of the segment's first char
   const uint32_t first = (uint32_t)(sbyte & 3ull);
   const uint32_t nchars = (valid && D) ? n : 0u;
@@ -255,9 +253,9 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   //   SHA-512/384: one 128-byte block per window.  Ed25519 hashes R || A || M:
   //   block 0 = the 64-byte register prefix + message words 0..15, block
   //   c >= 1 = message words 32c-16 ..
-  const uint64_t mw0 = tk.off >> 2;
-  const uint32_t mshift = (uint32_t)(tk.off & 3ull);
-  const uint32_t len = tk.sig_in_len;
+  const uint64_t mw0 = valid ? jb.off >> 2 : 0u;
+  const uint32_t mshift = valid ? jb.off & 3u : 0u;
+  const uint32_t len = valid ? jb.sig_in_len : 0u;
   const int hb_alg = alg_hash_bits(alg);
   const int hb = CLS == CLS_ED25519 ? 512
                  : HM == 1          ? 256
@@ -266,7 +264,7 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   uint32_t pre[16];
   uint32_t pw = 0;
   if (CLS == CLS_ED25519 && valid) {
-    const uint32_t* A = a.keyblob + a.keys[a.wave_key[p / WAVE]].aux_off;
+    const uint32_t* A = a.keyblob + a.keys[__builtin_amdgcn_readfirstlane(job_key(jb))].aux_off;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       pre[k] = sha2::bswap32(R_le[k]);

@@ -5,22 +5,9 @@
 
 #include "common.hpp"
 
-// device mirror of jg_tok (include/jg.h); layout checked by static_assert in the runtime
-struct jg_tok_dev {
-  uint64_t off;
-  uint32_t sig_in_len;
-  uint32_t sig_rel_off;
-  uint32_t sig_b64_len;
-  uint16_t key_idx;
-  uint8_t alg;
-  uint8_t flags;
-};
-
 struct PrepArgs {
   const uint8_t* arena;
-  const jg_tok_dev* toks;
-  const int32_t* perm;        // padded index -> token index (-1 = padding)
-  const int32_t* wave_key;    // per wave: key index
+  const jgk::JobDev* jobs;    // padded, (class, key)-sorted jobs
   const jgk::DevKey* keys;
   const uint32_t* keyblob;
   uint32_t* sigw;             // SIGW_ROWS x npad

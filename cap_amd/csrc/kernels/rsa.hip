@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
   const int64_t pbase = a.begin + (int64_t)blockIdx.x * TPW;
   const int64_t p = pbase + tl;
   const int64_t np = a.npad;
-  const int kidx = __builtin_amdgcn_readfirstlane(a.wave_key[pbase / WAVE]);
+  const int kidx = __builtin_amdgcn_readfirstlane(job_key(a.jobs[pbase]));
   const DevKey K = a.keys[kidx];
   const uint32_t* __restrict__ N = a.keyblob + K.n_off;
   const uint32_t* __restrict__ RR = a.keyblob + K.rr_off;
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
 #pragma unroll
   for (int j = 0; j < H; ++j) n[j] = N[g * H + j];
 
-  bool act = a.perm[p] >= 0 && a.status[p] == ST_OK && a.siglen[p] == (uint16_t)K.kbytes && K.valid;
+  bool act = job_live(a.jobs[p]) && a.status[p] == ST_OK && a.siglen[p] == (uint16_t)K.kbytes && K.valid;
 
   const uint32_t loff = (uint32_t)((int64_t)g * H * np + p);
   uint32_t v[H];
@@ -483,14 +483,14 @@ template <bool PSS>
 __global__ void __launch_bounds__(64) k_rsa_pad(RsaArgs a) {
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
-  const int32_t t = a.perm[p];
-  if (t < 0) return;
+  const JobDev jb = a.jobs[p];
+  if (!job_live(jb)) return;
   uint8_t verdict = 0;
   if (a.status[p] == ST_OK) {
-    const int kidx = a.wave_key[p / WAVE];
+    const int kidx = job_key(jb);
     const DevKey K = a.keys[kidx];
     const int k = K.kbytes;
-    const int alg = a.toks[t].alg;
+    const int alg = job_alg(jb);
     const int hb = (alg == 1 || alg == 4) ? 256 : (alg == 2 || alg == 5) ? 384 : 512;
     const int hlen = hb / 8;
     if (alg <= 3) {

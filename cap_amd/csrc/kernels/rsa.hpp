@@ -7,9 +7,7 @@
 #include "prep.hpp"
 
 struct RsaArgs {
-  const jg_tok_dev* toks;
-  const int32_t* perm;
-  const int32_t* wave_key;
+  const jgk::JobDev* jobs;
   const jgk::DevKey* keys;
   const uint32_t* keyblob;
   const uint32_t* sigw;       // decoded signature integer, LE words, SoA rows

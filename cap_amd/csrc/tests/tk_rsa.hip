@@ -59,25 +59,24 @@ extern "C" int tk_rsa_modexp(int cls, const uint32_t* n_le, int n_words, uint64_
   std::vector<uint32_t> sigw((size_t)SIGW_ROWS * np, 0);
   for (int p = 0; p < ntok; ++p)
     for (int q = 0; q < n_words; ++q) sigw[(size_t)q * np + p] = s_le[(size_t)p * n_words + q];
-  std::vector<int32_t> perm(np), wave_key(np / WAVE, 0);
-  for (int64_t p = 0; p < np; ++p) perm[p] = p < ntok ? (int32_t)p : -1;
+  std::vector<JobDev> jobs(np);
+  for (int64_t p = 0; p < np; ++p) jobs[p] = JobDev{0, 0, 0, job_pack(0, p < ntok ? 1u : JOB_PAD, 0)};
   std::vector<uint16_t> siglen(np, (uint16_t)K.kbytes);
   std::vector<uint8_t> status(np, ST_OK);
 
   DevKey* dk = dev_upload(std::vector<DevKey>{K});
   uint32_t* dblob = dev_upload(blob);
   uint32_t* dsig = dev_upload(sigw);
-  int32_t* dperm = dev_upload(perm);
-  int32_t* dwk = dev_upload(wave_key);
+  JobDev* djobs = dev_upload(jobs);
   uint16_t* dlen = dev_upload(siglen);
   uint8_t* dst = dev_upload(status);
   std::vector<uint32_t> zero((size_t)(2 * L + SIGW_ROWS) * np, 0);
   uint32_t* rows = dev_upload(zero);
-  int rc = (dk && dblob && dsig && dperm && dwk && dlen && dst && rows) ? 0 : -1;
+  int rc = (dk && dblob && dsig && djobs && dlen && dst && rows) ? 0 : -1;
   if (rc == 0) {
     launch_rsa_keyprep(dk, dblob, 1, 0);
     RsaArgs a{};
-    a.perm = dperm; a.wave_key = dwk; a.keys = dk; a.keyblob = dblob; a.sigw = dsig;
+    a.jobs = djobs; a.keys = dk; a.keyblob = dblob; a.sigw = dsig;
     a.xmw = rows; a.xlr = rows + (size_t)L * np; a.yw = rows + (size_t)2 * L * np;
     a.status = dst; a.siglen = dlen; a.npad = np; a.begin = 0; a.end = np;
     const unsigned waves = (unsigned)(np / WAVE);
@@ -97,7 +96,7 @@ extern "C" int tk_rsa_modexp(int cls, const uint32_t* n_le, int n_words, uint64_
       for (int q = 0; q < n_words; ++q) y_le[(size_t)p * n_words + q] = yw[(size_t)q * np + p];
     }
   }
-  for (void* ptr : {(void*)dk, (void*)dblob, (void*)dsig, (void*)dperm, (void*)dwk, (void*)dlen, (void*)dst, (void*)rows})
+  for (void* ptr : {(void*)dk, (void*)dblob, (void*)dsig, (void*)djobs, (void*)dlen, (void*)dst, (void*)rows})
     if (ptr) (void)hipFree(ptr);
   return rc;
 }
