@@ -83,7 +83,7 @@ size_t chunk_jobs() {
       const long v = std::atol(e);
       if (v >= 64) return (size_t)v;
     }
-    return (size_t)32768;
+    return (size_t)65536;
   }();
   return n;
 }
@@ -822,11 +822,11 @@ void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok
     bytes = (size_t)span;
     dbase = base;
     if (it.dev_arena) {
-      src = it.dev_arena + base;
+      src = it.arena + base;                       // page-locked: DMA straight from the caller
     } else {
       uint8_t* h = (uint8_t*)S.h_arena.get(bytes);
       std::memcpy(h, it.arena + base, bytes);
-      src = (const uint8_t*)S.h_arena.dp;
+      src = h;
     }
   } else {
     if (need + 4 * n >= (uint64_t(1) << 32) - ARENA_SLACK)
@@ -841,7 +841,7 @@ void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok
     }
     bytes = (size_t)pos;
     dbase = 0;
-    src = (const uint8_t*)S.h_arena.dp;
+    src = h;
   }
   Plan P;
   plan_layout(ctx, ht, n, P, d->plan, false, seen);
@@ -859,20 +859,24 @@ void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok
   const bool tr = pipe_trace();
   S.host_ms[1] = tr ? ms_since(t_start) : 0.0;
   const auto t_enq = std::chrono::steady_clock::now();
-  // Everything of the chunk on one compute lane, no DMA-engine copies: the
-  // arena span and the plan block's cursors are pulled from pinned host
-  // memory by a copy kernel, k_plan_fill reads the jobs straight from the
-  // pinned plan block, and the verdicts go back by a copy kernel.
+  // The arena span goes over PCIe on the copy stream's DMA engine (spans of
+  // consecutive chunks back to back); the rest of the chunk runs on a compute
+  // lane once that copy lands: a copy kernel pulls the plan block's cursors
+  // from pinned host memory, k_plan_fill reads the jobs straight from it
+  // (zero-copy), and a copy kernel writes the verdicts back to pinned memory.
   size_scratch(&S.bufs, P, bytes);
   S.bufs.jobs.get(sizeof(JobDev) * P.npad);
   S.bufs.perm.get(sizeof(int32_t) * P.npad);
   uint8_t* dm = (uint8_t*)S.bufs.meta.get(L.toks_off);
   const uint8_t* hbd = (const uint8_t*)S.h_meta.dp;
-  if (tr) HIPCHK(hipEventRecord(S.tr_a, s));
-  launch_copy(src, S.bufs.arena.p, bytes, s);
-  launch_copy(hbd, dm, L.toks_off, s);
-  if (tr) HIPCHK(hipEventRecord(S.tr_b, s));
+  const hipStream_t cs = d->copy;
+  if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
+  if (bytes) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, cs));
+  HIPCHK(hipEventRecord(S.copied, cs));
+  if (tr) HIPCHK(hipEventRecord(S.tr_b, cs));
   if (tr) S.host_ms[3] = ms_since(t_enq);
+  HIPCHK(hipStreamWaitEvent(s, S.copied, 0));
+  launch_copy(hbd, dm, L.toks_off, s);
   {
     PlanFillArgs fa{};
     fa.toks = (const jg_tok*)(hbd + L.toks_off);
@@ -908,7 +912,7 @@ void process_item(jg_ctx* ctx, Device* d, Item& it) {
       throw std::runtime_error("key table reloaded (or its load failed) while the batch was queued");
     if (pipe_trace()) {
       if (!g_trace_ref) HIPCHK(hipEventCreate(&g_trace_ref));
-      HIPCHK(hipEventRecord(g_trace_ref, d->lanes[d->next_lane].stream));
+      HIPCHK(hipEventRecord(g_trace_ref, d->copy));
     }
     for (size_t c = 0; c + 1 < it.cuts.size(); ++c) {
       const size_t lo = it.cuts[c], hi = it.cuts[c + 1];

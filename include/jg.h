@@ -119,7 +119,7 @@ int jg_submit(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok*
               uint8_t* verdict_out, jg_ticket** ticket);
 int jg_wait(jg_ctx* ctx, jg_ticket* ticket);
 
-/* Jobs per pipeline chunk of jg_submit / jg_verify_batch (default 32768, or
+/* Jobs per pipeline chunk of jg_submit / jg_verify_batch (default 65536, or
  * CAPJWT_CHUNK; >= 64).  Applies to later submissions.  Returns 0 or -1. */
 int jg_set_chunk(jg_ctx* ctx, size_t jobs);
 
