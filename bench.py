@@ -51,33 +51,34 @@ ALG_IDS = {"RS256": 1, "RS384": 2, "RS512": 3, "PS256": 4, "PS384": 5, "PS512": 
 
 # ---------------------------------------------------------------- algorithmic work
 def p256_point_mads_per_token():
-    """32x32->64 multiply-accumulates the P-256 comb kernel (k_ec_point) issues per
-    token: 28-bit limbs, L = 10; Montgomery product = L^2 (mul) or L(L+1)/2 (sqr)
-    + L * 4 for the reduction (p + 1 has 4 non-zero limbs above limb 0, mp.hpp);
-    mixed addition = 8 mul + 3 sqr + 3 value folds (6 non-zero limbs of
-    2^256 mod p); signed comb digits (ecdsa.hpp ec_comb_w): 11 windows of 24
-    bits for u1 (generator table) and 13 of 20 bits for u2 (key table), each
-    non-zero w.p. 1 - 2^-W (the top windows never carry), the first addition an
-    assignment and the second onto Z == 1 (madd_z1: 4 mul + 2 sqr); final check
-    1 sqr + 2 mul."""
-    L, red, fold = 10, 10 * 4, 6
-    mul, sqr = L * L + red, L * (L + 1) // 2 + red
-    madd = 8 * mul + 3 * sqr + 2 * fold
-    madd_z1 = 4 * mul + 2 * sqr + 2 * fold
-    adds = 11 * (1 - 2.0 ** -24) + 13 * (1 - 2.0 ** -20) - 1
-    return (adds - 1) * madd + madd_z1 + sqr + 2 * mul
+    """Algorithmic 32x32->64 multiply-accumulates the P-256 comb kernel
+    (k_ec_point) issues per token: 28-bit limbs, L = 10; a product is L^2 (mul)
+    or L(L+1)/2 (sqr) partial products, a Montgomery reduction L * 4 (p + 1 has
+    4 non-zero limbs above limb 0, mp.hpp).  Mixed addition = 8 mul + 3 sqr
+    under 10 reductions (Y3 = r t - Y1 hhh sums two products under one,
+    ecdsa.hip y3_from) + one value fold of X3 (6 non-zero limbs of 2^256 mod p).
+    The carry MADs of the unmasked reduction rows (hi32 * 16, mp.hpp
+    mont_reduce) are carries, not partial products, and are not counted.
+    Signed comb digits (ecdsa.hpp ec_comb_w): 11 windows of 24 bits for u1
+    (generator table) and 13 of 20 bits for u2 (key table), each non-zero w.p.
+    1 - 2^-W, the first addition an assignment and the second onto Z == 1
+    (madd_z1: 4 mul + 2 sqr under 5 reductions); final check 1 sqr + 2 mul."""
+    return ec_point_mads_per_token(10, 4, 6, 24, 20, 256, 10 * 4, merged=True)
 
 
-def ec_point_mads_per_token(L, red_mul, red_sqr, fold, wg, wq, bits, red_generic):
-    """Multiply-accumulates of a comb point kernel (k_ec_point) per token:
-    products are L^2 (mul) or L(L+1)/2 (sqr) partial products + the
-    reduction's MADs (red_*: L rows x the non-zero reduction constants); a
-    mixed addition is 8 mul + 3 sqr + 2 value folds (`fold` MADs each); the
-    first addition is an assignment, the second lands on Z == 1 (4 mul + 2 sqr
-    + 2 folds); the final check is 1 sqr + 2 mul with the generic reduction."""
-    mul, sqr = L * L + red_mul, L * (L + 1) // 2 + red_sqr
-    madd = 8 * mul + 3 * sqr + 2 * fold
-    madd_z1 = 4 * mul + 2 * sqr + 2 * fold
+def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged):
+    """Algorithmic multiply-accumulates of a comb point kernel (k_ec_point) per
+    token: products are L^2 (mul) or L(L+1)/2 (sqr) partial products, a
+    reduction is L rows x `red_row` non-zero reduction constants; a mixed
+    addition is 8 mul + 3 sqr under 11 reductions and 2 value folds (`fold`
+    MADs each), or under 10 reductions and 1 fold where Y3's two products share
+    one reduction (`merged`, ecdsa.hip sum_ok); the first addition is an
+    assignment, the second lands on Z == 1 (4 mul + 2 sqr); the final check is
+    1 sqr + 2 mul with the generic reduction."""
+    red = L * red_row
+    nred, nfold = (10, 1) if merged else (11, 2)
+    madd = 8 * L * L + 3 * L * (L + 1) // 2 + nred * red + nfold * fold
+    madd_z1 = 4 * L * L + 2 * L * (L + 1) // 2 + (nred - 5) * red + nfold * fold
     ng, nq = (bits + 1 + wg - 1) // wg, (bits + 1 + wq - 1) // wq
     adds = ng * (1 - 2.0 ** -wg) + nq * (1 - 2.0 ** -wq) - 1
     gmul, gsqr = L * L + red_generic, L * (L + 1) // 2 + red_generic
@@ -89,7 +90,7 @@ def p384_point_mads_per_token():
     loop's mulf / sqrf use the special-form reduction, 4 signed MADs per row
     (mp.hpp mont_reduce_p384); value folds through freduce (5 non-zero
     constants of 2^384 mod p); final check with m+1's 12 non-zero limbs."""
-    return ec_point_mads_per_token(15, 15 * 4, 15 * 4, 5, 20, 16, 384, 15 * 12)
+    return ec_point_mads_per_token(15, 4, 5, 20, 16, 384, 15 * 12, merged=False)
 
 
 def ed25519_point_mads_per_token():

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "common.hpp"
 #include "ecdsa.hpp"
@@ -198,17 +199,59 @@ __global__ void __launch_bounds__(64) k_ec_scalar_batch(EcArgs a, int B) {
 }
 
 // ------------------------------------------------------------------ point ops
+// Y3 = r t - Y1 hhh.  Fields with the column headroom (sum_ok) take both
+// products under ONE Montgomery reduction: (r t + (KSUB - Y1) hhh) / R, with
+// r, t < 3*2^28 limbs and KSUB - Y1 < 2^29, hhh < 2^28 (values < 6m, 6m, 4m,
+// 2m: the sum is < 44 m^2, far below R m), so Y3 comes out normalized with no
+// subtraction and no value fold.  P-384 keeps two special-form products.
+template <class Fp>
+constexpr bool sum_ok() {
+  if constexpr (std::is_same<Fp, P384P>::value) {
+    return false;
+  } else {
+    uint32_t kmax = 0;
+    for (int j = 0; j < Fp::L; ++j) kmax = Fp::KSUB[j] > kmax ? Fp::KSUB[j] : kmax;
+    double red = 0;
+    if constexpr (Fp::NP1)
+      for (int j = 1; j < Fp::L; ++j) red += (double)Fp::M1[j] / 16777216.0;
+    else
+      red = 16.0 * Fp::L;
+    return 9.0 * Fp::L + Fp::L * (double)kmax / 268435456.0 + red + 1.0 < 256.0;
+  }
+}
+
+template <class Fp>
+__device__ __forceinline__ void y3_from(uint32_t* Y, const uint32_t* r, const uint32_t* t, const uint32_t* y1,
+                                        const uint32_t* hhh) {
+  constexpr int L = Fp::L;
+  if constexpr (sum_ok<Fp>()) {
+    uint32_t ny1[L];
+    mp::neg<Fp>(ny1, y1);
+    uint64_t T[2 * L];
+    mp::prod<Fp>(T, r, t);
+    mp::prod_acc<Fp>(T, ny1, hhh);
+    mp::mont_reduce<Fp>(Y, T);
+  } else {
+    uint32_t u[L];
+    mp::mulf<Fp>(Y, r, t);
+    mp::mulf<Fp>(u, y1, hhh);
+    mp::sub<Fp>(Y, Y, u); mp::freduce_lazy<Fp>(Y);
+  }
+}
+
 // Mixed addition P1 (Jacobian, normalized < 2p) += P2 (affine x2, y2).
-// 8M + 3S, lazy; X3, Y3 value-reduced (freduce) so they can be subtrahends.
+// 8M + 3S, lazy; X3, Y3 value-reduced so they can be subtrahends.
 // Products go through mulf / sqrf (P-384: special-form reduction, which needs
 // one operand with 28-bit limbs per product -- h and r are normalised for it).
+// Z1Z1 is semi-normalized where the field allows (mp::sqr_semi): both its
+// consumers multiply it by an operand with 28-bit limbs (x2, Z).
 // An exceptional pair (P1 == +-P2) yields H == 0 and so Z3 == 0, which is
 // absorbing in later additions and is detected at the end.
 template <class Fp>
 __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, const uint32_t* x2, const uint32_t* y2) {
   constexpr int L = Fp::L;
   uint32_t z1z1[L], u2[L], t[L], s2[L], h[L], r[L], hh[L], hhh[L], v[L];
-  mp::sqrf<Fp>(z1z1, Z);
+  mp::sqr_semi<Fp>(z1z1, Z);
   mp::mulf<Fp>(u2, x2, z1z1);
   mp::mulf<Fp>(t, Z, z1z1);
   mp::mulf<Fp>(s2, y2, t);
@@ -229,9 +272,7 @@ __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, cons
   mp::sub<Fp>(X, r2, hhh); mp::sub<Fp>(X, X, v); mp::sub<Fp>(X, X, v); mp::freduce_lazy<Fp>(X);
   // Y3 = r (v - X3) - Y1 hhh
   mp::sub<Fp>(t, v, X);
-  mp::mulf<Fp>(Y, r, t);
-  mp::mulf<Fp>(t, y1, hhh);
-  mp::sub<Fp>(Y, Y, t); mp::freduce_lazy<Fp>(Y);
+  y3_from<Fp>(Y, r, t, y1, hhh);
 }
 
 // madd with Z1 == 1 (P1 affine: the accumulator after its first assignment):
@@ -243,7 +284,7 @@ __device__ __forceinline__ void madd_z1(uint32_t* X, uint32_t* Y, uint32_t* Z, c
   mp::sub<Fp>(h, x2, X);
   mp::sub<Fp>(r, y2, Y);
   mp::norm<Fp>(h);                           // Z3 = h: 28-bit limbs (mulf operand), value < 6m
-  mp::norm_for_mulf<Fp>(r);
+  mp::norm<Fp>(r);                           // y2 may be negated (limbs < 2^29): keep r^2's columns in range
   mp::sqrf<Fp>(hh, h);
   mp::mulf<Fp>(hhh, h, hh);
   mp::mulf<Fp>(v, X, hh);
@@ -252,9 +293,7 @@ __device__ __forceinline__ void madd_z1(uint32_t* X, uint32_t* Y, uint32_t* Z, c
   mp::copy<Fp>(y1, Y);
   mp::sub<Fp>(X, r2, hhh); mp::sub<Fp>(X, X, v); mp::sub<Fp>(X, X, v); mp::freduce_lazy<Fp>(X);
   mp::sub<Fp>(t, v, X);
-  mp::mulf<Fp>(Y, r, t);
-  mp::mulf<Fp>(t, y1, hhh);
-  mp::sub<Fp>(Y, Y, t); mp::freduce_lazy<Fp>(Y);
+  y3_from<Fp>(Y, r, t, y1, hhh);
 }
 
 // Z1ONE: the accumulator, if not empty, holds exactly one table entry (Z == 1)

@@ -107,13 +107,80 @@ MPD void mont_reduce_25519(uint32_t* r, uint64_t* t) {
   }
 }
 
+// Unmasked Montgomery digits (NP1 fields whose columns have the headroom):
+// rows 0..L-2 take q = the low 32 bits of t[i] instead of its low 28.  Then
+// t[i] + q m = (t[i] - q) + q (m+1) leaves hi32(t[i]) 2^32 = 16 hi32(t[i]) 2^28
+// in column i, so the carry into column i+1 is ONE mad (hi * 16) -- no mask,
+// no 64-bit shift, no 64-bit add.  The top row keeps a 28-bit digit, so
+// Q = sum q_i 2^(28 i) < (1 + 2^-24) R and the output stays below
+// T/R + (1 + 2^-24) m (was T/R + m); every caller's T/R is far below m/2.
+// Column headroom, in units of 2^56: L * 9 for a product of limbs < 3*2^28
+// (mp.hpp bounds; 2 L * 9 for the two-product sums of prod_acc callers is
+// checked there) plus sum_j M1[j] 2^32 / 2^56 from the reduction rows.
 template <class F>
+constexpr bool unmasked_rows() {
+  if constexpr (!F::NP1) {
+    return false;
+  } else {
+    double red = 0;
+    for (int j = 1; j < F::L; ++j) red += (double)F::M1[j] / 16777216.0;
+    return 9.0 * F::L + red + 1.0 < 256.0;
+  }
+}
+
+// SEMI: the output keeps 32-bit limbs ("semi-normalized": value as usual,
+// limbs < 2^32): the final chain moves only hi32 of each column up (one mad
+// per limb instead of add + mask + 64-bit shift).  Only valid as an operand of
+// a product whose other operand has limbs < 2^28 and only where L 2^60 plus
+// the reduction rows fits a column (see semi_ok); the top column's hi32 is 0
+// because the value is < 2^(28(L-1)+32).
+template <class F>
+constexpr bool semi_ok() {
+  if constexpr (!F::NP1) {
+    return false;
+  } else {
+    double red = 0;
+    for (int j = 1; j < F::L; ++j) red += (double)F::M1[j] / 16777216.0;
+    return 16.0 * F::L + red + 1.0 < 256.0;
+  }
+}
+
+template <class F, bool SEMI = false>
 MPD void mont_reduce(uint32_t* r, uint64_t* t) {
   constexpr int L = F::L;
   if constexpr (std::is_same<F, ED25519P>::value) {
     mont_reduce_25519(r, t);
     return;
   }
+  if constexpr (unmasked_rows<F>()) {
+    const uint32_t c16 = (uint32_t)opaque_sgpr(16);
+#pragma unroll
+    for (int i = 0; i < L - 1; ++i) {
+      red_row<F, 0>(t + i, (uint32_t)t[i]);
+      t[i + 1] += (uint64_t)(uint32_t)(t[i] >> 32) * c16;
+    }
+    red_row<F, 0>(t + L - 1, (uint32_t)t[L - 1] & MP_MASK);
+    t[L] += t[L - 1] >> MP_W;
+    if constexpr (SEMI) {
+      static_assert(semi_ok<F>(), "semi-normalized output needs column headroom");
+#pragma unroll
+      for (int j = 0; j < L - 1; ++j) {
+        r[j] = (uint32_t)t[L + j];
+        t[L + j + 1] += (uint64_t)(uint32_t)(t[L + j] >> 32) * c16;
+      }
+      r[L - 1] = (uint32_t)t[2 * L - 1];
+      return;
+    }
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const uint64_t v = t[L + j] + c;
+      r[j] = (uint32_t)v & MP_MASK;
+      c = v >> MP_W;
+    }
+    return;
+  }
+  static_assert(!SEMI || unmasked_rows<F>(), "semi-normalized output needs unmasked rows");
 #pragma unroll
   for (int i = 0; i < L; ++i) {
     // NP1: m = -1 mod 2^28 => NP = 1, q = t[i] mod 2^28 and q*m = q*(m+1) - q:
@@ -145,6 +212,16 @@ MPD void prod(uint64_t* t, const uint32_t* a, const uint32_t* b) {
       if (i == 0 || j == L - 1) mul64c(t[i + j], a[i], b[j]);
       else mad64c(t[i + j], a[i], b[j]);
     }
+}
+
+// t += a*b (all 2L-1 columns accumulate; for sums of products under ONE reduction)
+template <class F>
+MPD void prod_acc(uint64_t* t, const uint32_t* a, const uint32_t* b) {
+  constexpr int L = F::L;
+#pragma unroll
+  for (int i = 0; i < L; ++i)
+#pragma unroll
+    for (int j = 0; j < L; ++j) mad64c(t[i + j], a[i], b[j]);
 }
 
 // t = a^2  (cross products once, doubled operand)
@@ -182,6 +259,8 @@ MPD void sqr(uint32_t* r, const uint32_t* a) {
   sqprod<F>(t, a);
   mont_reduce<F>(r, t);
 }
+
+
 
 // P-384's special form: p + 1 = 2^384 - 2^128 - 2^96 + 2^32, i.e. per
 // reduction row +q*2^4 at limb i+1, -q*2^12 at i+3, -q*2^16 at i+4 and
@@ -239,6 +318,20 @@ MPD void sqrf(uint32_t* r, const uint32_t* a) {
     sqr<F>(r, a);
   }
 }
+
+// r = a^2/R mod m with a semi-normalized result (limbs < 2^32) where the field
+// allows it (semi_ok), else sqrf's normalized result
+template <class F>
+MPD void sqr_semi(uint32_t* r, const uint32_t* a) {
+  if constexpr (semi_ok<F>()) {
+    uint64_t t[2 * F::L];
+    sqprod<F>(t, a);
+    mont_reduce<F, true>(r, t);
+  } else {
+    sqrf<F>(r, a);
+  }
+}
+
 template <class F>
 MPD void add(uint32_t* r, const uint32_t* a, const uint32_t* b) {
 #pragma unroll
