@@ -56,14 +56,15 @@ def p256_point_mads_per_token():
     or L(L+1)/2 (sqr) partial products, a Montgomery reduction L * 4 (p + 1 has
     4 non-zero limbs above limb 0, mp.hpp).  Mixed addition = 8 mul + 3 sqr
     under 10 reductions (Y3 = r t - Y1 hhh sums two products under one,
-    ecdsa.hip y3_from) + one value fold of X3 (6 non-zero limbs of 2^256 mod p).
-    The carry MADs of the unmasked reduction rows (hi32 * 16, mp.hpp
-    mont_reduce) are carries, not partial products, and are not counted.
-    Signed comb digits (ecdsa.hpp ec_comb_w): 11 windows of 24 bits for u1
+    ecdsa.hip y3_from; X3's subtractions ride in r^2's columns, x3_from, so no
+    value fold).  The carry MADs of the unmasked reduction rows (hi32 * 16,
+    mp.hpp mont_reduce) and the column adds of x3_from are carries / additions,
+    not partial products, and are not counted.
+    Signed comb digits (ecdsa.hpp ec_comb_w): 10 windows of 26 bits for u1
     (generator table) and 13 of 20 bits for u2 (key table), each non-zero w.p.
     1 - 2^-W, the first addition an assignment and the second onto Z == 1
     (madd_z1: 4 mul + 2 sqr under 5 reductions); final check 1 sqr + 2 mul."""
-    return ec_point_mads_per_token(10, 4, 6, 24, 20, 256, 10 * 4, merged=True)
+    return ec_point_mads_per_token(10, 4, 0, 26, 20, 256, 10 * 4, merged=True)
 
 
 def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged):
@@ -72,7 +73,8 @@ def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged)
     reduction is L rows x `red_row` non-zero reduction constants; a mixed
     addition is 8 mul + 3 sqr under 11 reductions and 2 value folds (`fold`
     MADs each), or under 10 reductions and 1 fold where Y3's two products share
-    one reduction (`merged`, ecdsa.hip sum_ok); the first addition is an
+    one reduction (`merged`, ecdsa.hip sum_ok; fold = 0 where X3 needs none);
+    the first addition is an
     assignment, the second lands on Z == 1 (4 mul + 2 sqr); the final check is
     1 sqr + 2 mul with the generic reduction."""
     red = L * red_row

@@ -239,7 +239,47 @@ __device__ __forceinline__ void y3_from(uint32_t* Y, const uint32_t* r, const ui
   }
 }
 
-// Mixed addition P1 (Jacobian, normalized < 2p) += P2 (affine x2, y2).
+// X3 = r^2 - hhh - 2v.  Fields with a column constant KX3 (P-256,
+// tools/gen_field_consts.py XCOL) subtract inside r^2's high columns:
+// (r^2 + (KX3 - hhh - 2v) R) / R, where KX3 = 8m has every limb >= 3(2^28-1),
+// so KX3 - hhh - 2v >= 0 limb by limb.  X3 then comes out of the reduction
+// with 28-bit limbs and value < 8m + r^2/R + (1 + 2^-24) m < 10m: no value
+// fold.  Subtractions with X as the subtrahend use KSUBX (16m, covers < 10m).
+template <class Fp, class = void>
+struct has_kx3 : std::false_type {};
+template <class Fp>
+struct has_kx3<Fp, std::void_t<decltype(Fp::KX3)>> : std::true_type {};
+
+template <class Fp>
+__device__ __forceinline__ void x3_from(uint32_t* X, const uint32_t* r, const uint32_t* hhh, const uint32_t* v) {
+  constexpr int L = Fp::L;
+  if constexpr (has_kx3<Fp>::value) {
+    uint64_t T[2 * L];
+    mp::sqprod<Fp>(T, r);
+    const uint32_t c1 = (uint32_t)mp::opaque_sgpr(1);
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[L + j] += (uint64_t)(Fp::KX3[j] - (hhh[j] + 2 * v[j])) * c1;
+    mp::mont_reduce<Fp>(X, T);
+  } else {
+    uint32_t r2[L];
+    mp::sqrf<Fp>(r2, r);
+    mp::sub<Fp>(X, r2, hhh); mp::sub<Fp>(X, X, v); mp::sub<Fp>(X, X, v); mp::freduce_lazy<Fp>(X);
+  }
+}
+
+// a - X for an X produced by x3_from (value < 10m on KX3 fields)
+template <class Fp>
+__device__ __forceinline__ void sub_x(uint32_t* r, const uint32_t* a, const uint32_t* x) {
+  if constexpr (has_kx3<Fp>::value) {
+#pragma unroll
+    for (int j = 0; j < Fp::L; ++j) r[j] = a[j] + Fp::KSUBX[j] - x[j];
+  } else {
+    mp::sub<Fp>(r, a, x);
+  }
+}
+
+// Mixed addition P1 (Jacobian; X < 10m on KX3 fields, else < 2m; Y, Z < 2m,
+// 28-bit limbs) += P2 (affine x2, y2).
 // 8M + 3S, lazy; X3, Y3 value-reduced so they can be subtrahends.
 // Products go through mulf / sqrf (P-384: special-form reduction, which needs
 // one operand with 28-bit limbs per product -- h and r are normalised for it).
@@ -255,7 +295,7 @@ __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, cons
   mp::mulf<Fp>(u2, x2, z1z1);
   mp::mulf<Fp>(t, Z, z1z1);
   mp::mulf<Fp>(s2, y2, t);
-  mp::sub<Fp>(h, u2, X);
+  sub_x<Fp>(h, u2, X);
   mp::sub<Fp>(r, s2, Y);
   mp::norm_for_mulf<Fp>(h);                  // P-384: h, r are squared (mulf precondition)
   mp::norm_for_mulf<Fp>(r);
@@ -263,15 +303,11 @@ __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, cons
   mp::mulf<Fp>(hhh, h, hh);
   mp::mulf<Fp>(v, X, hh);
   mp::mulf<Fp>(Z, Z, h);
-  // X3 = r^2 - hhh - v - v: three lazy subtractions of normalized products
-  // (limbs < 7 * 2^28, value < 14m) and one single-chain value fold
-  uint32_t r2[L];
-  mp::sqrf<Fp>(r2, r);
   uint32_t y1[L];
   mp::copy<Fp>(y1, Y);
-  mp::sub<Fp>(X, r2, hhh); mp::sub<Fp>(X, X, v); mp::sub<Fp>(X, X, v); mp::freduce_lazy<Fp>(X);
+  x3_from<Fp>(X, r, hhh, v);
   // Y3 = r (v - X3) - Y1 hhh
-  mp::sub<Fp>(t, v, X);
+  sub_x<Fp>(t, v, X);
   y3_from<Fp>(Y, r, t, y1, hhh);
 }
 
@@ -280,7 +316,7 @@ __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, cons
 template <class Fp>
 __device__ __forceinline__ void madd_z1(uint32_t* X, uint32_t* Y, uint32_t* Z, const uint32_t* x2, const uint32_t* y2) {
   constexpr int L = Fp::L;
-  uint32_t h[L], r[L], hh[L], hhh[L], v[L], t[L], r2[L], y1[L];
+  uint32_t h[L], r[L], hh[L], hhh[L], v[L], t[L], y1[L];
   mp::sub<Fp>(h, x2, X);
   mp::sub<Fp>(r, y2, Y);
   mp::norm<Fp>(h);                           // Z3 = h: 28-bit limbs (mulf operand), value < 6m
@@ -289,10 +325,9 @@ __device__ __forceinline__ void madd_z1(uint32_t* X, uint32_t* Y, uint32_t* Z, c
   mp::mulf<Fp>(hhh, h, hh);
   mp::mulf<Fp>(v, X, hh);
   mp::copy<Fp>(Z, h);
-  mp::sqrf<Fp>(r2, r);
   mp::copy<Fp>(y1, Y);
-  mp::sub<Fp>(X, r2, hhh); mp::sub<Fp>(X, X, v); mp::sub<Fp>(X, X, v); mp::freduce_lazy<Fp>(X);
-  mp::sub<Fp>(t, v, X);
+  x3_from<Fp>(X, r, hhh, v);
+  sub_x<Fp>(t, v, X);
   y3_from<Fp>(Y, r, t, y1, hhh);
 }
 

@@ -35,13 +35,13 @@ constexpr int ec_order_bits(int cls) { return cls == jgk::CLS_P256 ? 256 : cls =
 // generator's table is built once per engine and shared by every key, so it
 // gets the wider window (gen = true); per-key tables stay narrower so a JWKS of
 // hundreds of keys still fits:
-//   P-256: G W=24 (11 windows, 7.4 GB), keys W=20 (13 windows, 545 MB each):
-//          23 additions per token (25 with W=20/20, ~32 with 16/16)
+//   P-256: G W=26 (10 windows, 26.8 GB), keys W=20 (13 windows, 545 MB each):
+//          22 additions per token (23 with G W=24, 25 with W=20/20, ~32 with 16/16)
 //   P-384: G W=20 (20 windows, 1.3 GB), keys W=16 (25 windows, 105 MB): 44 (65 at 12/12)
 //   P-521: G W=20 (27 windows, 2.3 GB), keys W=16 (33 windows, 173 MB): 59 (87 at 12/12)
 // The top window of each scalar (u < n) never carries out of the last digit.
 constexpr int ec_comb_w(int cls, bool gen) {
-  return cls == jgk::CLS_P256 ? (gen ? 24 : 20) : (gen ? 20 : 16);
+  return cls == jgk::CLS_P256 ? (gen ? 26 : 20) : (gen ? 20 : 16);
 }
 constexpr int ec_entries(int cls, bool gen) { return 1 << (ec_comb_w(cls, gen) - 1); }
 constexpr int ec_windows(int cls, bool gen) {

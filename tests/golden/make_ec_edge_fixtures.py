@@ -16,7 +16,7 @@ and the HIP kernels, which the tests then hold to these verdicts.
    * ACCEPTING exceptional tokens: key Q = G (private key 1), a fixed nonce k,
      and messages searched until the lowest signed comb digits of u1 (generator
      window) and u2 (key window) have equal magnitude (ecdsa.hpp ec_comb_w:
-     P-256 24/20 bits, P-384 and P-521 20/16 bits).
+     P-256 26/20 bits, P-384 and P-521 20/16 bits).
 2. The x(R) >= n acceptance branch (k_ec_point: X == (r + n) Z^2): a point R0
    with x(R0) = r + n for a small r, key Q = r^-1 (R0 - e G), signature
    (r, s = 1) -- then u1 G + u2 Q = e G + r Q = R0 and Go accepts.  Plus the
@@ -50,7 +50,7 @@ GEN = {
               int("011839296a789a3bc0045c8a5fb42c7d1bd998f54449579b446817afbd17273e"
                   "662c97ee72995ef42640c550b9013fad0761353c7086a272c24088be94769fd16650", 16)),
 }
-COMB_W = {"P-256": (24, 20), "P-384": (20, 16), "P-521": (20, 16)}   # (generator, key) -- ecdsa.hpp
+COMB_W = {"P-256": (26, 20), "P-384": (20, 16), "P-521": (20, 16)}   # (generator, key) -- ecdsa.hpp
 ALG_OF = {"P-256": "ES256", "P-384": "ES384", "P-521": "ES512"}
 SIZE = {"ES256": 32, "ES384": 48, "ES512": 66}
 HASH = {"ES256": hashlib.sha256, "ES384": hashlib.sha384, "ES512": hashlib.sha512}
