@@ -705,6 +705,7 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
     pa.begin = r.begin;
     pa.end = r.end;
     pa.zrows = cls_rows_sig(c);
+    pa.ec_words = (c >= CLS_P256 && c <= CLS_P521) ? ec_sig_words(c) : 0;
     launch_prep(c, P.hash_mask[c], pa, s);
     mark(marks, (std::string(cls_name(c)) + "_prep").c_str());
     if (c <= CLS_RSA4K) {

@@ -70,24 +70,32 @@ __device__ __forceinline__ bool ec_scalar_inputs(const EcArgs& a, int64_t p, uin
     return false;
   }
   const int kidx = job_key(jb);
-  bool ok = a.status[p] == ST_OK && a.keys[kidx].valid;
   const int alg = job_alg(jb);
-  uint32_t rw[17], sw[17];
+  // R18/R21: the signature size comes from the alg, the curve from the key
+  // (go-jose ecEncrypterVerifier: keySize by alg, no curve check), so r and s
+  // are es_size(alg)-byte integers that must be < n of the key's curve.  Prep
+  // leaves them in rows [0, ..) and [EC_S_ROW, ..), zero above what it wrote
+  // up to this curve's CW words; an alg whose r/s are longer than the curve's
+  // (ES512 on a P-256 key) must have zero words past CB as well.
+  bool ok = a.status[p] == ST_OK && a.keys[kidx].valid;
+  constexpr int CW = ec_sig_words(CV::CLS);
+  uint32_t rw[CW], sw[CW];
 #pragma unroll
-  for (int q = 0; q < 17; ++q) {
+  for (int q = 0; q < CW; ++q) {
     rw[q] = a.sigw[(int64_t)q * np + p];
     sw[q] = a.sigw[(int64_t)(EC_S_ROW + q) * np + p];
   }
-#pragma unroll
-  for (int q = 0; q < 17; ++q) {
-    if (4 * q >= CB) ok = ok && rw[q] == 0 && sw[q] == 0;
-    else if (4 * q + 4 > CB) {
-      const uint32_t hi = ~0u << (8 * (CB - 4 * q));
-      ok = ok && (rw[q] & hi) == 0 && (sw[q] & hi) == 0;
-    }
+  if constexpr (4 * CW > CB) {
+    const uint32_t hi = ~0u << (8 * (CB - 4 * (CW - 1)));
+    ok = ok && (rw[CW - 1] & hi) == 0 && (sw[CW - 1] & hi) == 0;
   }
-  mp::words_to_limbs<L, 17>(r, rw);
-  mp::words_to_limbs<L, 17>(s, sw);
+  if (es_size(alg) > CB) {
+    const int aw = (es_size(alg) + 3) / 4;      // words prep wrote for this alg
+    for (int q = CW; q < aw; ++q)
+      ok = ok && a.sigw[(int64_t)q * np + p] == 0 && a.sigw[(int64_t)(EC_S_ROW + q) * np + p] == 0;
+  }
+  mp::words_to_limbs<L, CW>(r, rw);
+  mp::words_to_limbs<L, CW>(s, sw);
   uint32_t nl[L];
   mp::set_const<Fn>(nl, Fn::M);
   ok = ok && !zero_limbs<L>(r) && !zero_limbs<L>(s) && lt_limbs<L>(r, nl) && lt_limbs<L>(s, nl);
@@ -189,12 +197,7 @@ __global__ void __launch_bounds__(64) k_ec_scalar_batch(EcArgs a, int B) {
     (void)ec_scalar_inputs<CV>(a, p, r, s, e);
     mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
     mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
-#pragma unroll
-    for (int k = 0; k < L; ++k) {
-      a.u1w[(int64_t)k * np + p] = u1[k];
-      a.u2w[(int64_t)k * np + p] = u2[k];
-    }
-    store_digits<CV>(a, p, u1, u2);
+    store_digits<CV>(a, p, u1, u2);       // (the rare exact path recomputes u1, u2 itself)
   }
 }
 
@@ -392,10 +395,11 @@ __global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
     return;
   }
   // x(R) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2)
-  uint32_t rw[17], r[L];
+  constexpr int CW = ec_sig_words(CV::CLS);
+  uint32_t rw[CW], r[L];
 #pragma unroll
-  for (int q = 0; q < 17; ++q) rw[q] = a.sigw[(int64_t)q * np + p];
-  mp::words_to_limbs<L, 17>(r, rw);
+  for (int q = 0; q < CW; ++q) rw[q] = a.sigw[(int64_t)q * np + p];
+  mp::words_to_limbs<L, CW>(r, rw);
   uint32_t zz[L], rm[L], tt[L];
   mp::sqr<Fp>(zz, Z);
   mp::to_mont<Fp>(rm, r);
@@ -508,12 +512,17 @@ __global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
   const uint32_t cnt = *a.exc_count;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
     const int64_t p = a.exc_list[i];
-    const int64_t np = a.npad;
     const int kidx = job_key(a.jobs[p]);
     const uint32_t* aux = a.keyblob + a.keys[kidx].aux_off;
-    uint32_t u1[L], u2[L];
-#pragma unroll
-    for (int j = 0; j < L; ++j) { u1[j] = a.u1w[(int64_t)j * np + p]; u2[j] = a.u2w[(int64_t)j * np + p]; }
+    // u1 = e / s, u2 = r / s (mod n), recomputed with one inversion per token
+    // (the status goes back to OK first: ec_scalar_inputs checks it)
+    a.status[p] = ST_OK;
+    uint32_t r[L], s[L], e[L], sm[L], w[L], u1[L], u2[L];
+    (void)ec_scalar_inputs<CV>(a, p, r, s, e);
+    mp::to_mont<Fn>(sm, s);
+    mp::inv<Fn>(w, sm);                          // s^-1 R
+    mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
+    mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
     JPt<Fp> G, Q, GQ, R;
     uint32_t gx[L], gy[L];
     mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
@@ -549,10 +558,6 @@ __global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
         }
         mp::copy<Fp>(x, d);
       }
-      uint32_t rw[17], r[L];
-#pragma unroll
-      for (int q = 0; q < 17; ++q) rw[q] = a.sigw[(int64_t)q * np + p];
-      mp::words_to_limbs<L, 17>(r, rw);
       uint32_t o = 0;
 #pragma unroll
       for (int j = 0; j < L; ++j) o |= x[j] ^ r[j];

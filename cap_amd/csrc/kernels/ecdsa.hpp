@@ -25,6 +25,8 @@ struct EcArgs {
 
 // table geometry per curve: words per entry (x,y Montgomery limbs, 16-B aligned)
 constexpr int ec_limbs(int cls) { return cls == jgk::CLS_P256 ? 10 : cls == jgk::CLS_P384 ? 15 : 20; }
+// 32-bit words of r (and of s) as prep leaves them: ceil(coordinate bytes / 4)
+constexpr int ec_sig_words(int cls) { return cls == jgk::CLS_P256 ? 8 : cls == jgk::CLS_P384 ? 12 : 17; }
 constexpr int ec_stride(int cls) { return (2 * ec_limbs(cls) + 3) & ~3; }
 constexpr int ec_order_bits(int cls) { return cls == jgk::CLS_P256 ? 256 : cls == jgk::CLS_P384 ? 384 : 521; }
 // Fixed-base comb over signed W-bit digits: u = sum_w d_w 2^(W w), d_w in

@@ -127,8 +127,8 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   if (valid) {
     // zero the rows this token may leave unwritten (scratch is reused across batches)
     for (int r = 0; r < a.zrows; ++r) {
-      // ECDSA reads r from rows [0, 17) and s from [EC_S_ROW, EC_S_ROW + 17) only
-      if (layout == LAY_SPLIT_BE && r >= 17 && r < EC_S_ROW) continue;
+      // ECDSA reads r from rows [0, ec_words) and s from [EC_S_ROW, EC_S_ROW + ec_words) only
+      if (layout == LAY_SPLIT_BE && ((r >= a.ec_words && r < EC_S_ROW) || r >= EC_S_ROW + a.ec_words)) continue;
       bool written = false;
       if (fast) {
         if (layout == LAY_SPLIT_BE) {
@@ -330,8 +330,11 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) { dout[2 * k] = (uint32_t)(h64[k] >> 32); dout[2 * k + 1] = (uint32_t)h64[k]; }
     }
+    // digest words only (SHA-256: 8, SHA-384: 12, SHA-512: 16): every consumer
+    // reads the alg's hash length, never the rows past it
 #pragma unroll
-    for (int k = 0; k < 16; ++k) dig[(int64_t)k * np + p] = dout[k];
+    for (int k = 0; k < 16; ++k)
+      if (k < hb / 32) dig[(int64_t)k * np + p] = dout[k];
   }
   a.status[p] = st;
 }

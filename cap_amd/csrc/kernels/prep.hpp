@@ -16,6 +16,7 @@ struct PrepArgs {
   uint16_t* siglen;           // npad
   int64_t npad, begin, end;
   int32_t zrows;              // signature rows the class's kernel reads
+  int32_t ec_words;           // ECDSA classes: words of r (and of s) the kernels read
 };
 
 // hash_mask: bit 0 = some token of the range uses SHA-256, bit 1 = SHA-384/512
