@@ -102,17 +102,20 @@ std::vector<size_t> chunk_cuts(size_t lo, size_t hi, size_t C) {
   return cut;
 }
 
-int cls_rows_sig(int c) {
+// l4: limbs of the largest RSA-4K+ layout among the loaded keys (148/296/592)
+int cls_rows_sig(int c, int l4) {
   switch (c) {
-    case CLS_RSA2K: case CLS_RSA3K: case CLS_RSA4K: return rsa_sig_rows(c);
+    case CLS_RSA2K: case CLS_RSA3K: return rsa_sig_rows(c);
+    case CLS_RSA4K: return rsa_sig_rows_l(l4);
     case CLS_P256: case CLS_P384: case CLS_P521: return EC_S_ROW + 17;
     case CLS_ED25519: return 16;
     default: return 0;
   }
 }
-int cls_rows_scratch(int c) {
+int cls_rows_scratch(int c, int l4) {
   switch (c) {
-    case CLS_RSA2K: case CLS_RSA3K: case CLS_RSA4K: return 2 * rsa_limbs(c) + SIGW_ROWS;
+    case CLS_RSA2K: case CLS_RSA3K: return 2 * rsa_limbs(c) + rsa_sig_rows(c);   // x R, x, y
+    case CLS_RSA4K: return 2 * l4 + rsa_sig_rows_l(l4);
     case CLS_P256: case CLS_P384: case CLS_P521: return ec_digit_rows(c) + 2 * ec_limbs(c);
     case CLS_ED25519: return 4 * ED_L;
     default: return 0;
@@ -172,6 +175,7 @@ struct HGrow {                    // grow-only pinned host allocation
 
 struct HostKey {
   int kind = 0, cls = CLS_REJECT, valid = 0;
+  int nlimbs = 0;                 // RSA: limbs of the key's modexp layout
 };
 
 // Fixed-base tables of the curve generators / Ed25519 base point depend only
@@ -238,6 +242,7 @@ struct Plan {
   int hash_mask[NCLS] = {};       // per class: bit 0 SHA-256 present, bit 1 SHA-384/512
   int pss_any[NCLS] = {};         // per class: some token uses RSASSA-PSS (PS256/384/512)
   int sig_rows = 1, scratch_rows = 1;
+  int rsa4k_limbs = 148, rsa4k_layouts = 1;   // the context's RSA-4K+ layouts at plan time
   int64_t pss_tokens = 0;         // PSS scratch tokens: the RSA classes' ranges back to back
   int64_t pss_off[NCLS] = {};
 };
@@ -359,6 +364,8 @@ struct jg_ctx {
   std::vector<HostKey> keys;
   std::vector<uint8_t> cls_tab;   // [key * NALG + alg] -> kernel class of the job
   std::vector<int32_t> cls_keys[NCLS];   // keys of each class, in index order
+  int rsa4k_limbs = 148;          // largest RSA-4K+ layout among the valid keys
+  int rsa4k_layouts = 1;          // RSA-4K+ layouts present (bit i: rsa4k_layout_limbs(i))
   bool failed = false;            // the last key load failed half-way: nothing verifies
   std::atomic<size_t> chunk{chunk_jobs()};   // jobs per pipeline chunk
   uint64_t epoch = 0;
@@ -415,9 +422,16 @@ void rebuild_class_tables(jg_ctx* ctx) {
   const size_t nk = ctx->keys.size();
   ctx->cls_tab.assign(nk * NALG, (uint8_t)CLS_REJECT);
   for (auto& v : ctx->cls_keys) v.clear();
+  ctx->rsa4k_limbs = rsa4k_layout_limbs(0);
+  ctx->rsa4k_layouts = 1;
   for (size_t k = 0; k < nk; ++k) {
     const HostKey& hk = ctx->keys[k];
     if (hk.valid && hk.cls != CLS_REJECT) ctx->cls_keys[hk.cls].push_back((int32_t)k);
+    if (hk.valid && hk.cls == CLS_RSA4K) {
+      ctx->rsa4k_limbs = std::max(ctx->rsa4k_limbs, hk.nlimbs);
+      for (int i = 0; i < RSA4K_NLAYOUT; ++i)
+        if (hk.nlimbs == rsa4k_layout_limbs(i)) ctx->rsa4k_layouts |= 1 << i;
+    }
     for (int a = 0; a < NALG; ++a)
       if (hk.valid && alg_family(a) == hk.kind) ctx->cls_tab[k * NALG + a] = (uint8_t)hk.cls;
   }
@@ -543,10 +557,12 @@ void plan_layout(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, Plan& P, Pl
   P.sig_rows = 1;
   P.scratch_rows = 1;
   P.pss_tokens = 0;
+  P.rsa4k_limbs = ctx->rsa4k_limbs;
+  P.rsa4k_layouts = ctx->rsa4k_layouts;
   for (int c = 1; c < NCLS; ++c) {
     if (P.ranges[c].end <= P.ranges[c].begin) continue;
-    P.sig_rows = std::max(P.sig_rows, cls_rows_sig(c));
-    P.scratch_rows = std::max(P.scratch_rows, cls_rows_scratch(c));
+    P.sig_rows = std::max(P.sig_rows, cls_rows_sig(c, P.rsa4k_limbs));
+    P.scratch_rows = std::max(P.scratch_rows, cls_rows_scratch(c, P.rsa4k_limbs));
     if (c <= CLS_RSA4K) {
       P.pss_off[c] = P.pss_tokens;
       P.pss_tokens += P.ranges[c].end - P.ranges[c].begin;
@@ -704,7 +720,7 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
     }
     pa.begin = r.begin;
     pa.end = r.end;
-    pa.zrows = cls_rows_sig(c);
+    pa.zrows = cls_rows_sig(c, P.rsa4k_limbs);
     pa.ec_words = (c >= CLS_P256 && c <= CLS_P521) ? ec_sig_words(c) : 0;
     launch_prep(c, P.hash_mask[c], pa, s);
     mark(marks, (std::string(cls_name(c)) + "_prep").c_str());
@@ -712,13 +728,14 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
       RsaArgs ra{};
       ra.jobs = pa.jobs; ra.keys = pa.keys; ra.keyblob = pa.keyblob;
       ra.sigw = pa.sigw; ra.dig = pa.dig;
-      const int Lm = rsa_limbs(c);
+      const int Lm = c == CLS_RSA4K ? P.rsa4k_limbs : rsa_limbs(c);
       ra.xmw = rows;
       ra.xlr = rows + (size_t)Lm * np;
       ra.yw = rows + (size_t)2 * Lm * np;
       ra.status = pa.status; ra.siglen = pa.siglen; ra.verdict_pad = (uint8_t*)B->vpad.p;
       ra.pss_scratch = (uint8_t*)B->pss.p + P.pss_off[c] * 2048;
       ra.has_pss = P.pss_any[c];
+      ra.layouts = c == CLS_RSA4K ? P.rsa4k_layouts : 1;
       ra.npad = np; ra.begin = r.begin; ra.end = r.end;
       launch_rsa(c, ra, s, marker(marks, c));
     } else if (c <= CLS_P521) {
@@ -1027,14 +1044,16 @@ void build_keys(const jg_key* keys, int nkeys, StagedKeys& S, std::vector<HostKe
       // crypto/rsa (Go >= 1.24) public-key checks: odd N of >= 1024 bits
       // (rsa1024min), odd E with 2 <= E <= 2^31-1   [SURVEY R12]
       bool ok = nl > 0 && bits >= 1024 && (n[nl - 1] & 1) && k.e >= 2 && k.e <= 0x7fffffffULL && (k.e & 1);
-      int cls = bits <= rsa_limbs(CLS_RSA2K) * 28 - 2 ? CLS_RSA2K : bits <= 112 * 28 - 2 ? CLS_RSA3K : bits <= 148 * 28 - 2 ? CLS_RSA4K : -1;
-      if (cls < 0) {
+      // layouts: RSA-2K (<= 2070 bits), RSA-3K (<= 3134), RSA-4K+ (148 / 296 /
+      // 592 limbs: <= 4142 / 8286 / 16574 bits, rsa.hpp); Go has no upper bound
+      const int cls = bits <= rsa_limbs(CLS_RSA2K) * 28 - 2 ? CLS_RSA2K : bits <= 112 * 28 - 2 ? CLS_RSA3K : CLS_RSA4K;
+      int L = cls == CLS_RSA4K ? rsa4k_limbs_for_bits(bits) : rsa_limbs(cls);
+      if (L == 0) {
         ok = false;
         *warn = "RSA key " + std::to_string(i) + " has " + std::to_string(bits) +
-                " bits; the GPU path supports up to 4142-bit moduli (key marked unusable)";
-        cls = CLS_RSA4K;
+                " bits; the GPU path supports up to 16574-bit moduli (key marked unusable)";
+        L = rsa4k_layout_limbs(0);
       }
-      const int L = rsa_limbs(cls);
       K.cls = cls;
       K.valid = ok;
       K.kbytes = (bits + 7) / 8;
@@ -1048,6 +1067,7 @@ void build_keys(const jg_key* keys, int nkeys, StagedKeys& S, std::vector<HostKe
       if (ok) S.rsa_idx.push_back(i);
       hk.cls = cls;
       hk.valid = ok;
+      hk.nlimbs = L;
     } else if (k.kind == JG_KEY_EC) {
       const int cls = k.curve == JG_P256 ? CLS_P256 : k.curve == JG_P384 ? CLS_P384 : k.curve == JG_P521 ? CLS_P521 : -1;
       if (cls < 0) { hk.valid = 0; continue; }

@@ -11,7 +11,7 @@ enum Cls : int {
   CLS_REJECT = 0,   // alg/key-type mismatch, unsupported alg, invalid key
   CLS_RSA2K = 1,    // RSA, modulus <= 2070 bits  (74 x 28-bit limbs; rsa.hpp rsa_limbs)
   CLS_RSA3K = 2,    // RSA, modulus <= 3134 bits  (112 limbs)
-  CLS_RSA4K = 3,    // RSA, modulus <= 4142 bits  (148 limbs)
+  CLS_RSA4K = 3,    // RSA, modulus >= 3135 bits: 148, 296 or 592 limbs by key (rsa.hpp)
   CLS_P256 = 4,
   CLS_P384 = 5,
   CLS_P521 = 6,
@@ -25,7 +25,7 @@ constexpr int WAVE = 64;
 enum : uint8_t { ST_OK = 0, ST_REJECT = 1, ST_EXCEPTIONAL = 2 };
 
 // scratch rows (each row holds one 32-bit word per padded token, SoA)
-constexpr int SIGW_ROWS = 132;      // decoded signature, up to 528 bytes (RSA-4142: 518)
+constexpr int SIGW_ROWS = 520;      // decoded signature rows, at most (RSA-16574: 2072 bytes)
 constexpr int EC_S_ROW = 32;        // ECDSA: s starts at row 32 (r at row 0)
 constexpr int DIG_ROWS = 16;        // digest, big-endian 32-bit words
 

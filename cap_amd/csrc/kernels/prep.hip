@@ -125,8 +125,14 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   const bool fast = valid && D != 0 && (D & 3u) == 0 && (layout != LAY_SPLIT_BE || (ks & 3u) == 0);
   const uint32_t DW = D >> 2;                          // decoded words
   if (valid) {
-    // zero the rows this token may leave unwritten (scratch is reused across batches)
-    for (int r = 0; r < a.zrows; ++r) {
+    // zero the rows this token may leave unwritten (scratch is reused across
+    // batches); an RSA key reads the rows of its own layout (rsa_sig_rows_l)
+    int zr = a.zrows;
+    if (layout == LAY_BE) {
+      const int nl = (int)a.keys[__builtin_amdgcn_readfirstlane(job_key(jb))].nlimbs;
+      zr = min(zr, (28 * nl - 1) / 32 + 2);
+    }
+    for (int r = 0; r < zr; ++r) {
       // ECDSA reads r from rows [0, ec_words) and s from [EC_S_ROW, EC_S_ROW + ec_words) only
       if (layout == LAY_SPLIT_BE && ((r >= a.ec_words && r < EC_S_ROW) || r >= EC_S_ROW + a.ec_words)) continue;
       bool written = false;

@@ -39,26 +39,45 @@ using namespace jgk;
 namespace {
 
 // ---------------------------------------------------------------- cross-lane
-// Token = group of G consecutive lanes (G = 2 or 4, inside one DPP quad);
-// lane g of the group holds limbs [g*H, (g+1)*H) of every multi-limb value.
+// Token = group of G consecutive lanes; lane g of the group holds limbs
+// [g*H, (g+1)*H) of every multi-limb value.  G = 2 or 4: one DPP quad
+// (quad_perm); G = 8 or 16 (the RSA-8K / RSA-16K layouts of the 4K+ class):
+// neighbours by DPP row shifts inside a 16-lane row, group-wide broadcasts by
+// ds_swizzle in bitmask mode (lane' = lane & and_mask | or_mask inside each
+// 32-lane half), one instruction each.
+template <int G>
+__device__ __forceinline__ uint32_t swz(uint32_t x, int or_mask) {
+  static_assert(G == 8 || G == 16, "swizzle broadcasts serve the 8/16-lane groups");
+  constexpr int AND = 0x1f & ~(G - 1);
+  if (or_mask == 0) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, AND);
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, AND | ((G - 1) << 5));
+}
 template <int G>
 __device__ __forceinline__ uint32_t bcast0(uint32_t x) {        // value of group lane 0
-  constexpr int ctrl = G == 2 ? 0xA0 /* quad_perm 0,0,2,2 */ : 0x00 /* 0,0,0,0 */;
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
+  if constexpr (G > 4) {
+    return swz<G>(x, 0);
+  } else {
+    constexpr int ctrl = G == 2 ? 0xA0 /* quad_perm 0,0,2,2 */ : 0x00 /* 0,0,0,0 */;
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
+  }
 }
 template <int G>
 __device__ __forceinline__ uint32_t bcast_last(uint32_t x) {    // value of group lane G-1
-  constexpr int ctrl = G == 2 ? 0xF5 /* quad_perm 1,1,3,3 */ : 0xFF /* 3,3,3,3 */;
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
+  if constexpr (G > 4) {
+    return swz<G>(x, G - 1);
+  } else {
+    constexpr int ctrl = G == 2 ? 0xF5 /* quad_perm 1,1,3,3 */ : 0xFF /* 3,3,3,3 */;
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
+  }
 }
 template <int G>
 __device__ __forceinline__ uint32_t from_next(uint32_t x) {     // value of group lane g+1
-  constexpr int ctrl = G == 2 ? 0xF5 /* 1,1,3,3 */ : 0xF9 /* 1,2,3,3 */;
+  constexpr int ctrl = G == 2 ? 0xF5 /* 1,1,3,3 */ : G == 4 ? 0xF9 /* 1,2,3,3 */ : 0x101 /* row_shl:1 */;
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
 }
 template <int G>
 __device__ __forceinline__ uint32_t from_prev(uint32_t x) {     // value of group lane g-1
-  constexpr int ctrl = G == 2 ? 0xA0 /* quad_perm 0,0,2,2 */ : 0x90 /* 0,0,1,2 */;
+  constexpr int ctrl = G == 2 ? 0xA0 /* quad_perm 0,0,2,2 */ : G == 4 ? 0x90 /* 0,0,1,2 */ : 0x111 /* row_shr:1 */;
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, true);
 }
 
@@ -182,8 +201,10 @@ __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const 
 #pragma unroll
     for (int u = 0; u < U; ++u) cios_step<H, G>(P + u, a[u], v, n, np, lane0, mlast);
     if constexpr (2 * L > 250) {
-      // keep every 64-bit column < 2^64 (2L products of < 2^56): normalise half-way
-      if (ib == NB / 2) {
+      // keep every 64-bit column < 2^64: a row adds two products of < 2^56 to
+      // each column, so normalise within the lane every 80 rows (RSA-4K: once,
+      // half-way; the 8K / 16K layouts every 10 blocks)
+      if ((ib + 1) % 10 == 0 && ib + 1 < NB) {
 #pragma unroll
         for (int j = U; j < U + H - 1; ++j) { P[j + 1] += P[j] >> W28; P[j] &= M28; }
       }
@@ -245,7 +266,10 @@ __device__ __forceinline__ void mont_sqr(uint32_t* v, const uint32_t* la, const 
       limb_shift<H, G>(T, lane0, mlast);
     }
     if constexpr (2 * L > 250) {
-      if (r == G / 2 - 1) {   // keep every 64-bit column < 2^64: normalise half-way
+      // keep every 64-bit column < 2^64: a squaring row adds at most one doubled
+      // product (< 2^57) and one reduction product (< 2^56) to a column, so
+      // normalise every two lane blocks (74 rows at H = 37: < 222 * 2^56)
+      if (r % 2 == 1 && r < G - 1) {
 #pragma unroll
         for (int j = H; j < 2 * H - 1; ++j) { P[j + 1] += P[j] >> W28; P[j] &= M28; }
       }
@@ -306,6 +330,7 @@ __global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
   const int64_t np = a.npad;
   const int kidx = __builtin_amdgcn_readfirstlane(job_key(a.jobs[pbase]));
   const DevKey K = a.keys[kidx];
+  if (K.nlimbs != (uint32_t)L) return;      // a wave of another layout of the class (wave-uniform)
   const uint32_t* __restrict__ N = a.keyblob + K.n_off;
   const uint32_t* __restrict__ RR = a.keyblob + K.rr_off;
   const uint32_t np28 = K.np;
@@ -673,7 +698,11 @@ void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const Marker& mk) {
   switch (cls) {
     case CLS_RSA2K: hipLaunchKernelGGL((k_rsa_modexp<RSA2K_H, RSA2K_G, 8>), dim3((unsigned)(waves * RSA2K_G)), b, 0, s, a); break;
     case CLS_RSA3K: hipLaunchKernelGGL((k_rsa_modexp<28, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a); break;
-    case CLS_RSA4K: hipLaunchKernelGGL((k_rsa_modexp<37, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a); break;
+    case CLS_RSA4K:
+      if (a.layouts & 1) hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a);
+      if (a.layouts & 2) hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 8, 8>), dim3((unsigned)(waves * 8)), b, 0, s, a);
+      if (a.layouts & 4) hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 16, 8>), dim3((unsigned)(waves * 16)), b, 0, s, a);
+      break;
     default: return;
   }
   mk("modexp");

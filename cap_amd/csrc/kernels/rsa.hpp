@@ -20,6 +20,7 @@ struct RsaArgs {
   uint8_t* verdict_pad;
   uint8_t* pss_scratch;       // 2 KiB per token of the class range
   int32_t has_pss;            // the range holds PS* tokens (else the PKCS#1-only pad kernel)
+  int32_t layouts;            // RSA-4K+ class: bit i = keys of rsa4k_layout_limbs(i) limbs are loaded
   int64_t npad, begin, end;
 };
 
@@ -29,16 +30,27 @@ struct RsaArgs {
 #endif
 constexpr int RSA2K_G = JG_RSA2K_G;
 constexpr int RSA2K_H = RSA2K_G == 2 ? 37 : 19;
+// limbs of the class's (smallest) layout: 74 / 112 / 148
 constexpr int rsa_limbs(int cls) {
   return cls == jgk::CLS_RSA2K ? RSA2K_G * RSA2K_H : cls == jgk::CLS_RSA3K ? 112 : 148;
 }
-// rows of the signature scratch each RSA class reads: the modexp's limb loads
-// touch words up to (28 L - 1) / 32 + 1 (load_limbs_from_words), so those
-// rows must be zeroed by prep
-constexpr int rsa_sig_rows(int cls) {
-  return (28 * rsa_limbs(cls) - 1) / 32 + 2;
+// The RSA-4K+ class (moduli of 3135 bits and up) has three layouts of H = 37
+// limbs per lane, picked per key by its size: G = 4, 8 or 16 lanes per token
+// (148, 296, 592 limbs: up to 4142, 8286 and 16574 bits).  Each layout's
+// kernel runs over the class range and serves the waves of its own keys.
+constexpr int RSA4K_H = 37;
+constexpr int RSA4K_NLAYOUT = 3;
+constexpr int rsa4k_layout_limbs(int i) { return RSA4K_H * (4 << i); }
+constexpr int rsa4k_limbs_for_bits(int bits) {
+  return bits <= 148 * 28 - 2 ? 148 : bits <= 296 * 28 - 2 ? 296 : bits <= 592 * 28 - 2 ? 592 : 0;
 }
-static_assert(rsa_sig_rows(jgk::CLS_RSA4K) <= jgk::SIGW_ROWS, "RSA-4K signature rows exceed the scratch");
+// rows of the signature scratch an L-limb modexp reads: its limb loads touch
+// words up to (28 L - 1) / 32 + 1 (load_limbs_from_words), so those rows must
+// be zeroed by prep; the result y takes as many rows
+constexpr int rsa_sig_rows_l(int L) { return (28 * L - 1) / 32 + 2; }
+constexpr int rsa_sig_rows(int cls) { return rsa_sig_rows_l(rsa_limbs(cls)); }
+static_assert(rsa_sig_rows_l(rsa4k_layout_limbs(RSA4K_NLAYOUT - 1)) <= jgk::SIGW_ROWS,
+              "RSA-16K signature rows exceed the scratch");
 
 void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const jgk::Marker& mk);
 void launch_rsa_keyprep(jgk::DevKey* keys, uint32_t* blob, int nkeys, hipStream_t s);

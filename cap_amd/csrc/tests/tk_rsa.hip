@@ -30,12 +30,13 @@ T* dev_upload(const std::vector<T>& h) {
 extern "C" int tk_rsa_modexp(int cls, const uint32_t* n_le, int n_words, uint64_t e, const uint32_t* s_le, int ntok,
                              uint32_t* y_le, uint8_t* ok) {
   if (cls < CLS_RSA2K || cls > CLS_RSA4K || ntok <= 0 || n_words <= 0 || n_words > SIGW_ROWS) return -1;
-  const int L = rsa_limbs(cls);
   const int64_t np = (ntok + WAVE - 1) / WAVE * WAVE;
   int bits = 0;
   for (int q = n_words - 1; q >= 0 && !bits; --q)
     if (n_le[q]) bits = 32 * q + 32 - __builtin_clz(n_le[q]);
-  if (bits == 0 || bits > 28 * L - 2 || !(n_le[0] & 1)) return -1;
+  // the RSA-4K+ class picks its layout (148 / 296 / 592 limbs) by the key size
+  const int L = cls == CLS_RSA4K ? rsa4k_limbs_for_bits(bits) : rsa_limbs(cls);
+  if (bits == 0 || L == 0 || bits > 28 * L - 2 || !(n_le[0] & 1)) return -1;
 
   // key blob: n as 28-bit limbs, then R^2 (filled by k_rsa_keyprep)
   std::vector<uint32_t> blob(2 * (size_t)L, 0);
@@ -83,7 +84,11 @@ extern "C" int tk_rsa_modexp(int cls, const uint32_t* n_le, int n_words, uint64_
     switch (cls) {   // the launch shapes of launch_rsa, without the padding check
       case CLS_RSA2K: hipLaunchKernelGGL((k_rsa_modexp<RSA2K_H, RSA2K_G, 8>), dim3(waves * RSA2K_G), dim3(WAVE), 0, 0, a); break;
       case CLS_RSA3K: hipLaunchKernelGGL((k_rsa_modexp<28, 4, 8>), dim3(waves * 4), dim3(WAVE), 0, 0, a); break;
-      default: hipLaunchKernelGGL((k_rsa_modexp<37, 4, 8>), dim3(waves * 4), dim3(WAVE), 0, 0, a); break;
+      default:
+        if (L == rsa4k_layout_limbs(0)) hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 4, 8>), dim3(waves * 4), dim3(WAVE), 0, 0, a);
+        else if (L == rsa4k_layout_limbs(1)) hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 8, 8>), dim3(waves * 8), dim3(WAVE), 0, 0, a);
+        else hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 16, 8>), dim3(waves * 16), dim3(WAVE), 0, 0, a);
+        break;
     }
     if (hipDeviceSynchronize() != hipSuccess) rc = -1;
   }

@@ -178,7 +178,7 @@ long or_b64url_decode(const char* s, size_t n, uint8_t* out, size_t cap) {
 /* ======================================================================= */
 /* bignum: little-endian uint32 limbs                                       */
 /* ======================================================================= */
-#define MAXL 140   /* 4480 bits */
+#define MAXL 600   /* 19200 bits: RSA moduli up to the GPU path's 16574-bit layout */
 
 static void bn_from_be(uint32_t* r, int L, const uint8_t* b, size_t blen) {
   memset(r, 0, sizeof(uint32_t) * L);

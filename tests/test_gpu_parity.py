@@ -179,9 +179,10 @@ def test_key_reload_reuses_tables():
 
 
 def test_rsa_keys_above_4096_bits():
-    """RSA moduli of 4100 and 4142 bits (the largest the 148-limb class holds;
-    signatures of 513-518 bytes): the GPU verdicts equal the oracle's and the
-    fixture's (tests/golden/rsa_big.json, made by make_big_rsa.py)."""
+    """RSA moduli of 4100 to 16384 bits -- every layout of the RSA-4K+ class
+    (148 limbs up to 4142 bits, 296 up to 8286, 592 above; signatures of 513 to
+    2048 bytes, PKCS#1 v1.5 and PSS): the GPU verdicts equal the oracle's and
+    the fixture's (tests/golden/rsa_big.json, made by make_big_rsa.py)."""
     import json
     from oracle import jws
     d = json.load(open(os.path.join(H.ROOT, "tests", "golden", "rsa_big.json")))

@@ -17,9 +17,12 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLS_RSA2K, CLS_RSA3K, CLS_RSA4K = 1, 2, 3
-# modulus bit lengths per class (limits 28 L - 2 bits: 2070 / 3134; 4K up to the 512-byte signature rows)
+# modulus bit lengths per class (limits 28 L - 2 bits: 2070 / 3134; the RSA-4K+
+# class picks 148 / 296 / 592 limbs by key size: up to 4142 / 8286 / 16574 bits)
 SIZES = [(CLS_RSA2K, 2048), (CLS_RSA2K, 2049), (CLS_RSA2K, 2070), (CLS_RSA3K, 3072), (CLS_RSA3K, 2071),
-         (CLS_RSA4K, 4096), (CLS_RSA4K, 3135)]
+         (CLS_RSA4K, 4096), (CLS_RSA4K, 3135), (CLS_RSA4K, 4142)]
+BIG_SIZES = [(CLS_RSA4K, 4143), (CLS_RSA4K, 8192), (CLS_RSA4K, 8286), (CLS_RSA4K, 8287), (CLS_RSA4K, 16384),
+             (CLS_RSA4K, 16574)]
 
 
 @pytest.fixture(scope="module")
@@ -65,7 +68,20 @@ def test_modexp_exact(tk, cls, bits, e):
     assert not bad, (len(bad), bad[:8])
 
 
-@pytest.mark.parametrize("cls,bits", [(CLS_RSA2K, 2048), (CLS_RSA4K, 4096)])
+@pytest.mark.parametrize("cls,bits", BIG_SIZES)
+@pytest.mark.parametrize("e", [65537, 3, 2**31 - 1])
+def test_modexp_exact_big_layouts(tk, cls, bits, e):
+    """The 296- and 592-limb layouts (8 and 16 lanes per token: DPP row shifts
+    and ds_swizzle broadcasts, column normalisation every 80 / 74 rows)."""
+    rng = random.Random(bits * 1000003 + e)
+    n = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+    sigs = edge_sigs(n, rng, 70)
+    ys, ok = modexp(tk, cls, n, e, sigs)
+    bad = [i for i, (s, y) in enumerate(zip(sigs, ys)) if not ok[i] or y != pow(s, e, n)]
+    assert not bad, (len(bad), bad[:8])
+
+
+@pytest.mark.parametrize("cls,bits", [(CLS_RSA2K, 2048), (CLS_RSA4K, 4096), (CLS_RSA4K, 8192), (CLS_RSA4K, 16384)])
 def test_modexp_rejects_sig_not_below_modulus(tk, cls, bits):
     rng = random.Random(bits)
     n = rng.getrandbits(bits) | (1 << (bits - 1)) | 1

@@ -91,9 +91,9 @@ def test_static_keyset_semantics(golden):
 
 
 def test_oracle_rsa_keys_above_4096_bits():
-    """RSA-4100 / RSA-4142 keys (tests/golden/rsa_big.json): Go's crypto/rsa
-    has no 4096-bit ceiling, so valid RS256/RS512 tokens accept and
-    signature-flipped ones reject."""
+    """RSA keys of 4100 to 16384 bits (tests/golden/rsa_big.json): Go's
+    crypto/rsa has no 4096-bit ceiling, so valid RS256 / RS512 / PS512 tokens
+    accept and signature-flipped ones reject."""
     import json
     import os
     from oracle import jws
