@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 KEYDIR = os.path.join(ROOT, "tests", "golden", "keys")
 BENCHKEYS = os.path.join(ROOT, "tools", "benchkeys")
 TOKGEN = os.path.join(ROOT, "tools", "tokgen", "tokgen")
-TRAFFIC = os.path.join(ROOT, "profiles", "r01_s7_pmc_traffic.json")
+TRAFFIC = os.path.join(ROOT, "profiles", "r02_s4_pmc_traffic.json")
 COLL_DEVICE = "cuda"            # device of the timing all-reduce (RCCL); "cpu" under gloo
 
 # measured v_mad_u64_u32 issue rate, chip-wide: the integer multiply-add
@@ -585,7 +585,8 @@ def run_configs(ctx, args, threads, rank, world, dist):
 
 def load_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc pass
-    (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), or None."""
+    (FETCH_SIZE x2 per the gfx950 correction, calibrated for the streaming and
+    80-byte gather patterns in that file, + WRITE_SIZE), or None."""
     try:
         d = json.load(open(TRAFFIC))
         return d["kernels"][kernel]["hbm_bytes_per_launch"]
@@ -667,8 +668,11 @@ def main():
                      "frac": achieved / MAD_PEAK_T, "traffic": load_traffic("p256_point"),
                      "note": "integer multiply-add roofline (SURVEY §8d): algorithmic 32x32->64 MADs "
                              f"per token {p256_point_mads_per_token():.0f} x tokens / HIP-event kernel time; "
-                             "peak = measured v_mad_u64_u32 rate; traffic = HBM bytes per launch from the "
-                             f"rocprofv3 --pmc passes in {os.path.relpath(TRAFFIC, ROOT)}"},
+                             "peak = measured v_mad_u64_u32 rate; traffic = HBM bytes per launch, "
+                             "2 x FETCH_SIZE + WRITE_SIZE of the rocprofv3 --pmc passes in "
+                             f"{os.path.relpath(TRAFFIC, ROOT)} (the x2 calibrated for this kernel's random "
+                             "80-byte comb-entry gathers by tools/ubench/gather_cal: 192 B of 128-B lines per "
+                             "entry, 23 entries per token)"},
         "roofline_other": roofline_line(kms, ntok, {"p256_prep": ("hbm", prep_bytes_per_token(342, 49))}),
         "kernel_ms": kms,
         "cpu": cpu,

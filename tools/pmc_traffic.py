@@ -3,11 +3,18 @@
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  Per /opt/skills/guides/MI355X_MICROARCH.md
 (HBM section) FETCH_SIZE reports half the bytes of wide coalesced streaming
-reads on gfx950, so it is doubled here; WRITE_SIZE is taken as is.  The gathers
-of these kernels are not wide streaming reads, so the doubled figure is an
-upper estimate (the undoubled one is kept beside it).
+reads on gfx950; other access patterns are uncalibrated there, so the third
+input calibrates the point kernel's own pattern: tools/ubench/gather_cal
+(random 80-byte comb-table entries, 16-B aligned, 5 x dwordx4 per entry, a
+7.97 GB table) and a 16-B/lane stream, each with a known requested byte count,
+under rocprofv3 --pmc FETCH_SIZE.  Measured on MI355X: stream FETCH = 0.500 x
+requested (the guide's x2), gather FETCH = 1.20 x requested = 96 B per 80-B
+entry = half of the 1.5 128-B lines an entry touches on average -- so the x2
+correction also gives line traffic for the gathers.  Only the launches of the
+largest grid (the resident 1,048,576-token batch) are used; the bench's
+pipelined chunks launch the same kernels on smaller grids.
 
-usage: python tools/pmc_traffic.py fetch.csv write.csv out.json
+usage: python tools/pmc_traffic.py fetch.csv write.csv cal.csv cal.json out.json
 """
 import collections
 import csv
@@ -27,29 +34,52 @@ ALIASES = {  # bench.py mark name -> kernel symbol prefix
 def load(fn):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(fn)):
-        agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+        agg[(r["Kernel_Name"], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
     return agg
 
 
-def main(fetch_csv, write_csv, out):
+def biggest(agg, sym):
+    ks = [k for k in agg if k[0].startswith(sym)]
+    if not ks:
+        return None, None
+    k = max(ks, key=lambda k: k[1])
+    v = agg[k]
+    return k[1], (sum(v) / len(v) * 1024, len(v))
+
+
+def calibration(cal_csv, cal_json):
+    req = json.load(open(cal_json))
+    agg = load(cal_csv)
+    out = {}
+    for (name, _), v in agg.items():
+        for tag, key in (("gather", "gather_requested_bytes"), ("stream", "stream_requested_bytes")):
+            if name.startswith("k_" + tag):
+                out[tag] = {"fetch_bytes": sum(v) * 1024, "requested_bytes": req[key],
+                            "fetch_per_requested_byte": sum(v) * 1024 / req[key]}
+    out["gather"]["fetch_bytes_per_80B_entry"] = out["gather"]["fetch_per_requested_byte"] * 80
+    return out
+
+
+def main(fetch_csv, write_csv, cal_csv, cal_json, out):
     f, w = load(fetch_csv), load(write_csv)
     res = {}
     for alias, sym in ALIASES.items():
-        fk = [v for k, v in f.items() if k.startswith(sym)]
-        wk = [v for k, v in w.items() if k.startswith(sym)]
-        if not fk or not wk:
+        grid, fv = biggest(f, sym)
+        _, wv = biggest(w, sym)
+        if not fv or not wv:
             continue
-        fetch = sum(fk[0]) / len(fk[0]) * 1024
-        write = sum(wk[0]) / len(wk[0]) * 1024
-        res[alias] = {"symbol": sym, "launches": len(fk[0]), "fetch_bytes_raw": fetch, "write_bytes": write,
+        fetch, write = fv[0], wv[0]
+        res[alias] = {"symbol": sym, "grid": grid, "launches": fv[1], "fetch_bytes_raw": fetch, "write_bytes": write,
                       "hbm_bytes_per_launch": 2 * fetch + write, "hbm_bytes_per_launch_undoubled": fetch + write}
     json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes over "
-                         "`bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-configs` (tools/gpu_profile.sh)",
-               "correction": "FETCH_SIZE x2 (gfx950 streaming-read calibration, MI355X_MICROARCH.md HBM section)",
+                         "`bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-configs` (tools/gpu_profile_r02.sh)",
+               "correction": "FETCH_SIZE x2: the guide's streaming-read calibration, confirmed for this repo's "
+                             "streaming and 80-byte gather patterns by `calibration` below",
+               "calibration": calibration(cal_csv, cal_json),
                "kernels": res}, open(out, "w"), indent=1)
     for k, v in res.items():
-        print(f"{k:16s} fetch {v['fetch_bytes_raw'] / 1e6:9.1f} MB  write {v['write_bytes'] / 1e6:9.1f} MB")
+        print(f"{k:16s} grid {v['grid']:8d} fetch {v['fetch_bytes_raw'] / 1e6:9.1f} MB  write {v['write_bytes'] / 1e6:9.1f} MB")
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:6])
