@@ -506,7 +506,11 @@ def roofline_line(kernel_ms, per_gpu, kernels):
 
 
 def config_line(ctx, name, workload, pool, algs, keyidx, expected_good, per_gpu, steps, warmup, dist, world,
-                kernels=None):
+                kernels=None, class_of_key=None):
+    """One BASELINE config measured like the headline.  `kernels`: roofline
+    work per token of the class kernels to report; a kernel sees only its
+    class's tokens -- by alg family, or by `class_of_key[key index]` (kernel
+    class name per key) where keys of one family fall into several classes."""
     arena, toks = pack(pool, algs, keyidx, per_gpu)
     el, acc, kms, v = measure(ctx, arena, toks, steps, warmup, dist)
     reps = (per_gpu + len(pool) - 1) // len(pool)
@@ -524,7 +528,11 @@ def config_line(ctx, name, workload, pool, algs, keyidx, expected_good, per_gpu,
             share[key] = cls
         counts = {}
         aid = np.asarray(algs)
+        kcls = np.asarray([class_of_key[k] for k in keyidx]) if class_of_key else None
         for key, cls in share.items():
+            if kcls is not None:
+                counts[key] = float((kcls == cls).mean())
+                continue
             fam = {"p256": (7,), "p384": (8,), "p521": (9,), "ed25519": (10,), "rsa2048": (1, 2, 3, 4, 5, 6),
                    "rsa3072": (1, 2, 3, 4, 5, 6), "rsa4096": (1, 2, 3, 4, 5, 6)}[cls]
             frac = float(np.isin(aid, fam).mean()) if cls not in ("rsa2048", "rsa3072", "rsa4096") else None
@@ -576,10 +584,33 @@ def run_configs(ctx, args, threads, rank, world, dist):
     algs = [algs[i] for i in order]
     keyidx = [keyidx[i] for i in order]
     pool, algs, keyidx, good = tamper(pool, algs, keyidx, meta, 0.05)
-    out["mixed_10alg_32kid"] = config_line(
+    # kernel class of each kid's key (ecdsa/rsa/ed25519 classes of the runtime)
+    def key_class(jwk):
+        if jwk["kty"] == "RSA":
+            import base64
+            bits = int.from_bytes(base64.urlsafe_b64decode(jwk["n"] + "=" * (-len(jwk["n"]) % 4)), "big").bit_length()
+            return "rsa2048" if bits <= 2070 else "rsa3072" if bits <= 3134 else "rsa4096"
+        if jwk["kty"] == "EC":
+            return {"P-256": "p256", "P-384": "p384", "P-521": "p521"}[jwk["crv"]]
+        return "ed25519"
+    kcls = [key_class(m[4]) for m in meta]
+    present = set(kcls)
+    work = {"rsa2048_modexp": rsa_modexp_mads_per_token(74, 2), "rsa3072_modexp": rsa_modexp_mads_per_token(112, 4),
+            "rsa4096_modexp": rsa_modexp_mads_per_token(148, 4), "p256_point": p256_point_mads_per_token(),
+            "p384_point": p384_point_mads_per_token(), "ed25519_point": ed25519_point_mads_per_token()}
+    line = config_line(
         ctx, "mixed_10alg_32kid", "all 10 algs, 32 kids, 5% tampered, 10M stream on 8 GPUs in 262144-token chunks "
         "(configs[4]); one chunk per step per GPU", pool, algs, keyidx, good, 262144, max(1, args.steps // 2), 1,
-        dist, world)
+        dist, world, kernels={k: v for k, v in work.items() if k.split("_")[0] in present}, class_of_key=kcls)
+    # the same workload as a real stream: this GPU's 1/8 share of the 10M
+    # tokens (1,310,720) through jg_verify_batch from pinned host memory (H2D,
+    # plan, kernels, verdicts back), chunks overlapping
+    share = 10_000_000 // 8
+    arena, toks = pack(pool, algs, keyidx, share)
+    st = measure_pcie(ctx, arena, toks, iters=2, chunks=(65536, 262144))
+    st["workload"] = f"{share} tokens per GPU (10M / 8) streamed with H2D"
+    line["stream"] = st
+    out["mixed_10alg_32kid"] = line
     return out
 
 

@@ -179,15 +179,17 @@ struct HostKey {
 };
 
 // Fixed-base tables of the curve generators / Ed25519 base point depend only
-// on (device, curve), so every jg_ctx of the process shares one copy per device
-// (the P-256 one is 7.4 GB and takes 0.3 s to build).  Freed with the last
-// context that holds it.
+// on (device, curve): every jg_ctx of the process shares one copy per device,
+// built on first use and kept for the life of the process (they are constants
+// of the curves: ~31 GB per device with all four, the P-256 one 26.8 GB and
+// ~1.1 s to build -- a process that opens and closes contexts must not pay
+// that again).  Deliberately never freed: the cache outlives static
+// destruction, and the driver reclaims device memory at process exit.
 struct SharedTable {
   uint32_t* p = nullptr;
-  ~SharedTable() { if (p) (void)hipFree(p); }
 };
 std::mutex g_tab_mu;
-std::map<std::pair<int, int>, std::weak_ptr<SharedTable>> g_tabs;   // (device id, class) -> table
+auto& g_tabs = *new std::map<std::pair<int, int>, std::shared_ptr<SharedTable>>();   // (device id, class) -> table
 
 // One in-order stream plus per-class fan-out streams: a mixed batch's classes
 // are each too small to fill 256 CUs alone, so untimed runs put every class's
@@ -1127,12 +1129,17 @@ template <class Build>
 std::shared_ptr<SharedTable> shared_table(Device* d, int cls, size_t bytes, Build&& build) {
   std::lock_guard<std::mutex> g(g_tab_mu);
   const auto key = std::make_pair(d->id, cls);
-  if (auto t = g_tabs[key].lock()) return t;
+  if (auto t = g_tabs[key]) return t;
   auto t = std::make_shared<SharedTable>();
   HIPCHK(hipMalloc(&t->p, bytes));
-  build(t->p);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(d->lane0.stream));
+  try {
+    build(t->p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(d->lane0.stream));
+  } catch (...) {
+    (void)hipFree(t->p);          // a failed build is not cached
+    throw;
+  }
   g_tabs[key] = t;
   return t;
 }
