@@ -50,7 +50,7 @@ ALG_IDS = {"RS256": 1, "RS384": 2, "RS512": 3, "PS256": 4, "PS384": 5, "PS512": 
 
 
 # ---------------------------------------------------------------- algorithmic work
-def p256_point_mads_per_token():
+def p256_point_mads_per_token(wq=24):
     """Algorithmic 32x32->64 multiply-accumulates the P-256 comb kernel
     (k_ec_point) issues per token: 28-bit limbs, L = 10; a product is L^2 (mul)
     or L(L+1)/2 (sqr) partial products, a Montgomery reduction L * 4 (p + 1 has
@@ -60,11 +60,13 @@ def p256_point_mads_per_token():
     value fold).  The carry MADs of the unmasked reduction rows (hi32 * 16,
     mp.hpp mont_reduce) and the column adds of x3_from are carries / additions,
     not partial products, and are not counted.
-    Signed comb digits (ecdsa.hpp ec_comb_w): 10 windows of 26 bits for u1
-    (generator table) and 13 of 20 bits for u2 (key table), each non-zero w.p.
-    1 - 2^-W, the first addition an assignment and the second onto Z == 1
-    (madd_z1: 4 mul + 2 sqr under 5 reductions); final check 1 sqr + 2 mul."""
-    return ec_point_mads_per_token(10, 4, 0, 26, 20, 256, 10 * 4, merged=True)
+    Signed comb digits (ecdsa.hpp ec_comb_w / ec_key_w): 10 windows of 26
+    bits for u1 (generator table) and ceil(257 / wq) for u2 (key table: W = 24
+    for the bench's 4 kids under the default 32 GiB table budget, 11 windows),
+    each non-zero w.p. 1 - 2^-W, the first addition an assignment and the
+    second onto Z == 1 (madd_z1: 4 mul + 2 sqr under 5 reductions); final check
+    1 sqr + 2 mul."""
+    return ec_point_mads_per_token(10, 4, 0, 26, wq, 256, 10 * 4, merged=True)
 
 
 def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged):

@@ -21,7 +21,7 @@ CURVE_IDS = {"P-256": 1, "P-384": 2, "P-521": 3}
 EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_last_error",
            "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_enqueue", "jg_batch_sync",
            "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
-           "jg_submit", "jg_wait", "jg_set_chunk"]
+           "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_table_budget"]
 
 
 class JgKey(ctypes.Structure):
@@ -74,6 +74,7 @@ def lib():
         L.jg_submit.argtypes = [vp, vp, sz, ctypes.POINTER(JgTok), sz, vp, ctypes.POINTER(vp)]
         L.jg_wait.argtypes = [vp, vp]
         L.jg_set_chunk.argtypes = [vp, sz]
+        L.jg_set_table_budget.argtypes = [vp, ctypes.c_uint64]
         L.jg_hash_batch.argtypes = [vp, vp, sz, vp, sz, vp]
         L.jg_version.restype = ctypes.c_char_p
         _lib = L
@@ -180,6 +181,11 @@ class Context:
     def set_chunk(self, jobs):
         if lib().jg_set_chunk(self.h, jobs) != 0:
             raise JgError("jg_set_chunk: chunk must be >= 64 jobs")
+
+    def set_table_budget(self, nbytes):
+        """jg_set_table_budget: HBM for P-256 key comb tables (applies at the next load_keys)."""
+        if lib().jg_set_table_budget(self.h, int(nbytes)) != 0:
+            raise JgError("jg_set_table_budget failed")
 
     def submit(self, arena: Arena):
         """jg_submit; returns a Pending whose wait() gives the verdict bytes."""

@@ -88,6 +88,19 @@ size_t chunk_jobs() {
   return n;
 }
 
+// HBM a context may spend on P-256 key comb tables (ecdsa.hpp ec_key_w): 32 GiB
+// by default (up to 4 keys at W = 24, 17 at W = 22), or CAPJWT_TABLE_BUDGET_GB
+uint64_t default_table_budget() {
+  static const uint64_t b = [] {
+    if (const char* e = std::getenv("CAPJWT_TABLE_BUDGET_GB")) {
+      const double v = std::atof(e);
+      if (v >= 0) return (uint64_t)(v * (double)(1ull << 30));
+    }
+    return (uint64_t)32 << 30;
+  }();
+  return b;
+}
+
 // Chunk boundaries of jobs [lo, hi) for a pipeline of C-job chunks: the first
 // chunks ramp up from 4096 jobs (the copy engine starts after a short host
 // plan) and the tail ends in a quarter-size chunk (little kernel time left
@@ -305,6 +318,7 @@ struct Item {                     // one device's share of a submission
 
 struct Device {
   int id = 0;
+  int p256_wq = 20;               // comb width of the loaded P-256 key tables
   Lane lane0;                     // resident batches, key loads, hashing
   uint32_t* gtab[NCLS] = {};
   uint32_t* btab = nullptr;
@@ -370,6 +384,7 @@ struct jg_ctx {
   int rsa4k_layouts = 1;          // RSA-4K+ layouts present (bit i: rsa4k_layout_limbs(i))
   bool failed = false;            // the last key load failed half-way: nothing verifies
   std::atomic<size_t> chunk{chunk_jobs()};   // jobs per pipeline chunk
+  std::atomic<uint64_t> table_budget{default_table_budget()};   // HBM for P-256 key comb tables
   uint64_t epoch = 0;
   std::shared_mutex key_mu;       // key table: exclusive in jg_keys_load, shared by submitters
   std::mutex err_mu;
@@ -752,6 +767,7 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
       ea.exc_list = (int32_t*)B->exc.p + r.begin;
       ea.exc_count = (uint32_t*)B->exc_cnt.p + c;
       ea.npad = np; ea.begin = r.begin; ea.end = r.end;
+      ea.wq = c == CLS_P256 ? d->p256_wq : ec_comb_w(c, false);
       launch_ec(c, ea, s, marker(marks, c));
     } else {
       if (!d->btab) throw std::runtime_error("Ed25519 base table missing");
@@ -1003,6 +1019,7 @@ void wait_idle(Device* d) {
 
 // ---------------------------------------------------------------- keys
 struct StagedKeys {
+  int p256_wq = 20;                // comb width of this load's P-256 key tables (ecdsa.hpp ec_key_w)
   std::vector<DevKey> dk;
   std::vector<uint32_t> blob;      // host-initialised part of the device key blob
   uint64_t tab_words = 0;          // device-only tail: comb tables (built on the GPU)
@@ -1028,10 +1045,16 @@ uint64_t blob_alloc(std::vector<uint32_t>& blob, size_t words) {
 // Host part of a key load.  Touches no context state (the caller commits `hk`
 // only after every device has loaded the new table); `warn` collects
 // informational messages for jg_last_error.
-void build_keys(const jg_key* keys, int nkeys, StagedKeys& S, std::vector<HostKey>& hks, std::string* warn) {
+void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys& S, std::vector<HostKey>& hks,
+                std::string* warn) {
   hks.assign((size_t)nkeys, HostKey{});
   S.dk.assign((size_t)nkeys, DevKey{});
   S.tab_id.assign((size_t)nkeys, std::string());
+  // P-256 key tables: the widest comb whose tables for every P-256 key of the
+  // load fit the context's table budget (fewer additions per token)
+  int n256 = 0;
+  for (int i = 0; i < nkeys; ++i) n256 += keys[i].kind == JG_KEY_EC && keys[i].curve == JG_P256;
+  S.p256_wq = ec_key_w(CLS_P256, n256, table_budget);
   for (int i = 0; i < nkeys; ++i) {
     const jg_key& k = keys[i];
     HostKey& hk = hks[i];
@@ -1078,7 +1101,8 @@ void build_keys(const jg_key* keys, int nkeys, StagedKeys& S, std::vector<HostKe
       K.cls = cls;
       K.kbytes = cb;
       K.aux_off = blob_alloc(S.blob, 2 * L);
-      K.tab_off = tab_alloc(S, i, (uint64_t)ec_table_words(cls, false));
+      const int wq = cls == CLS_P256 ? S.p256_wq : ec_comb_w(cls, false);
+      K.tab_off = tab_alloc(S, i, (uint64_t)ec_table_words_w(cls, wq));
       const size_t cl = k.coord_len > 0 ? (size_t)k.coord_len : 0;
       // crypto/ecdsa pointFromAffine: coordinates must fit the curve's bit size
       bool ok = k.x && k.y && cl > 0 && bitlen_be(k.x, cl) <= (cls == CLS_P521 ? 521 : cb * 8) &&
@@ -1115,7 +1139,8 @@ void build_keys(const jg_key* keys, int nkeys, StagedKeys& S, std::vector<HostKe
     if ((int)S.ec_idx[c].size() > ec_max_keys(c))
       throw std::runtime_error(std::string(cls_name(c)) + ": at most " + std::to_string(ec_max_keys(c)) +
                                " keys per table (comb tables are " +
-                               std::to_string(ec_table_words(c, false) * 4 >> 20) + " MiB each)");
+                               std::to_string(ec_table_words_w(c, c == CLS_P256 ? S.p256_wq : ec_comb_w(c, false)) *
+                                              4 >> 20) + " MiB each)");
   if ((int)S.ed_idx.size() > ED_MAX_KEYS)
     throw std::runtime_error("Ed25519: at most " + std::to_string(ED_MAX_KEYS) + " keys per table (comb tables are " +
                              std::to_string(ed_table_words(false) * 4 >> 20) + " MiB each)");
@@ -1161,6 +1186,7 @@ void ensure_tables(Device* d, const StagedKeys& S) {
 
 void load_keys_device(Device* d, const StagedKeys& S) {
   HIPCHK(hipSetDevice(d->id));
+  d->p256_wq = S.p256_wq;
   hipStream_t s = d->lane0.stream;
   d->lane0.sync();
   if (d->copy) (void)hipStreamSynchronize(d->copy);
@@ -1196,7 +1222,8 @@ void load_keys_device(Device* d, const StagedKeys& S) {
       }
     };
     std::vector<int32_t> build_ec[NCLS], build_ed;
-    for (int c = CLS_P256; c <= CLS_P521; ++c) split(S.ec_idx[c], (uint64_t)ec_table_words(c, false), build_ec[c]);
+    for (int c = CLS_P256; c <= CLS_P521; ++c)
+      split(S.ec_idx[c], (uint64_t)ec_table_words_w(c, c == CLS_P256 ? S.p256_wq : ec_comb_w(c, false)), build_ec[c]);
     split(S.ed_idx, (uint64_t)ed_table_words(false), build_ed);
     // one index array: rsa | p256 | p384 | p521 | ed | builds p256 | p384 | p521 | ed
     std::vector<int32_t> idx;
@@ -1212,7 +1239,7 @@ void load_keys_device(Device* d, const StagedKeys& S) {
     ensure_tables(d, S);
     if (!S.dk.empty()) launch_rsa_keyprep(d->dkeys, d->dblob, (int)S.dk.size(), s);
     for (int c = CLS_P256; c <= CLS_P521; ++c)
-      launch_ec_keyprep(c, d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(),
+      launch_ec_keyprep(c, c == CLS_P256 ? S.p256_wq : ec_comb_w(c, false), d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(),
                         d->didx + at[5 + c - CLS_P256], (int)build_ec[c].size(), s);
     launch_ed_keyprep(d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), d->didx + at[8],
                       (int)build_ed.size(), s);
@@ -1376,7 +1403,7 @@ int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys) {
     StagedKeys S;
     std::vector<HostKey> hk;
     std::string warn;
-    build_keys(keys, nkeys, S, hk, &warn);                  // throws before any device state changes
+    build_keys(keys, nkeys, ctx->table_budget.load(), S, hk, &warn);   // throws before any device state changes
     try {
       for (auto& d : ctx->devs) load_keys_device(d.get(), S);
       // device-side validity (on-curve, Ed25519 decoding) back into the host view
@@ -1449,6 +1476,12 @@ int jg_wait(jg_ctx* ctx, jg_ticket* t) {
 int jg_set_chunk(jg_ctx* ctx, size_t jobs) {
   if (!ctx || jobs < 64) return -1;
   ctx->chunk.store(jobs);
+  return 0;
+}
+
+int jg_set_table_budget(jg_ctx* ctx, uint64_t bytes) {
+  if (!ctx) return -1;
+  ctx->table_budget.store(bytes);
   return 0;
 }
 

@@ -26,9 +26,13 @@ using namespace jgk;
 
 namespace {
 
-struct CurveP256 { using Fp = P256P; using Fn = P256N; using C = P256C; static constexpr int CLS = CLS_P256; };
-struct CurveP384 { using Fp = P384P; using Fn = P384N; using C = P384C; static constexpr int CLS = CLS_P384; };
-struct CurveP521 { using Fp = P521P; using Fn = P521N; using C = P521C; static constexpr int CLS = CLS_P521; };
+// WQ: comb width of the key tables (ecdsa.hpp ec_key_w: P-256 keys 20 / 22 / 24
+// by the context's table budget; one kernel instantiation per width)
+template <int WQ_>
+struct CurveP256W { using Fp = P256P; using Fn = P256N; using C = P256C; static constexpr int CLS = CLS_P256, WQ = WQ_; };
+using CurveP256 = CurveP256W<20>;
+struct CurveP384 { using Fp = P384P; using Fn = P384N; using C = P384C; static constexpr int CLS = CLS_P384, WQ = 16; };
+struct CurveP521 { using Fp = P521P; using Fn = P521N; using C = P521C; static constexpr int CLS = CLS_P521, WQ = 16; };
 
 __device__ __forceinline__ int es_size(int alg) { return alg == 7 ? 32 : alg == 8 ? 48 : 66; }
 __device__ __forceinline__ int es_hash_bytes(int alg) { return alg == 7 ? 32 : alg == 8 ? 48 : 64; }
@@ -139,7 +143,7 @@ __device__ __forceinline__ void store_digit_rows(const EcArgs& a, int64_t p, con
 template <class CV>
 __device__ __forceinline__ void store_digits(const EcArgs& a, int64_t p, const uint32_t* u1, const uint32_t* u2) {
   constexpr int WG = ec_comb_w(CV::CLS, true), NG = ec_windows(CV::CLS, true);
-  constexpr int WQ = ec_comb_w(CV::CLS, false), NQ = ec_windows(CV::CLS, false);
+  constexpr int WQ = CV::WQ, NQ = ec_windows_w(CV::CLS, CV::WQ);
   store_digit_rows<CV, WG, NG>(a, p, u1, 0);
   store_digit_rows<CV, WQ, NQ>(a, p, u2, NG);
 }
@@ -339,7 +343,7 @@ template <class CV, bool GEN, bool Z1ONE = false>
 __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z, bool& empty,
                                            const uint32_t* __restrict__ tab, int w, int d) {
   using Fp = typename CV::Fp;
-  constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS), NE = ec_entries(CV::CLS, GEN);
+  constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS), NE = GEN ? ec_entries(CV::CLS, true) : 1 << (CV::WQ - 1);
   if (d == 0) return;
   const int ad = d < 0 ? -d : d;
   const uint32_t* ent = tab + ((int64_t)w * NE + (ad - 1)) * STRIDE;
@@ -364,7 +368,7 @@ __global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
   using Fp = typename CV::Fp;
   using Fn = typename CV::Fn;
   constexpr int L = Fp::L;
-  constexpr int NG = ec_windows(CV::CLS, true), NQ = ec_windows(CV::CLS, false);
+  constexpr int NG = ec_windows(CV::CLS, true), NQ = ec_windows_w(CV::CLS, CV::WQ);
   constexpr int NWIN = NG > NQ ? NG : NQ;
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
@@ -644,8 +648,8 @@ __device__ void table_entry(uint32_t* out, const uint32_t* base, int d) {
 // bases (entry 1), then thread per (key, entry >= 2) from its window's base.
 template <class CV>
 __global__ void k_ec_table_base_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
-  constexpr int W = ec_comb_w(CV::CLS, false), NWIN = ec_windows(CV::CLS, false);
-  constexpr int NE = ec_entries(CV::CLS, false), STRIDE = ec_stride(CV::CLS);
+  constexpr int W = CV::WQ, NWIN = ec_windows_w(CV::CLS, CV::WQ);
+  constexpr int NE = 1 << (CV::WQ - 1), STRIDE = ec_stride(CV::CLS);
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (k >= n || w >= NWIN) return;
@@ -657,8 +661,8 @@ __global__ void k_ec_table_base_keys(const DevKey* keys, uint32_t* blob, const i
 
 template <class CV>
 __global__ void k_ec_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
-  constexpr int W = ec_comb_w(CV::CLS, false), NWIN = ec_windows(CV::CLS, false);
-  constexpr int NE = ec_entries(CV::CLS, false), STRIDE = ec_stride(CV::CLS);
+  constexpr int W = CV::WQ, NWIN = ec_windows_w(CV::CLS, CV::WQ);
+  constexpr int NE = 1 << (CV::WQ - 1), STRIDE = ec_stride(CV::CLS);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (k >= n || e >= NWIN * NE || e % NE == 0) return;
@@ -709,7 +713,7 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
 template <class CV>
 void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx, int tn,
                    hipStream_t s) {
-  constexpr int NWIN = ec_windows(CV::CLS, false), NE = ec_entries(CV::CLS, false);
+  constexpr int NWIN = ec_windows_w(CV::CLS, CV::WQ), NE = 1 << (CV::WQ - 1);
   dim3 b(64);
   if (n > 0) hipLaunchKernelGGL(k_ec_keyprep<CV>, dim3((n + 63) / 64), b, 0, s, keys, blob, idx, n);
   if (tn <= 0) return;
@@ -729,18 +733,26 @@ void gtable_chain(uint32_t* tab, hipStream_t s) {
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const Marker& mk) {
   if (a.end <= a.begin) return;
   switch (cls) {
-    case CLS_P256: launch_chain<CurveP256>(a, s, mk); break;
+    case CLS_P256:
+      if (a.wq == 24) launch_chain<CurveP256W<24>>(a, s, mk);
+      else if (a.wq == 22) launch_chain<CurveP256W<22>>(a, s, mk);
+      else launch_chain<CurveP256W<20>>(a, s, mk);
+      break;
     case CLS_P384: launch_chain<CurveP384>(a, s, mk); break;
     case CLS_P521: launch_chain<CurveP521>(a, s, mk); break;
     default: break;
   }
 }
 
-void launch_ec_keyprep(int cls, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx,
+void launch_ec_keyprep(int cls, int wq, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx,
                        int tn, hipStream_t s) {
   if (n <= 0) return;
   switch (cls) {
-    case CLS_P256: keyprep_chain<CurveP256>(keys, blob, idx, n, tidx, tn, s); break;
+    case CLS_P256:
+      if (wq == 24) keyprep_chain<CurveP256W<24>>(keys, blob, idx, n, tidx, tn, s);
+      else if (wq == 22) keyprep_chain<CurveP256W<22>>(keys, blob, idx, n, tidx, tn, s);
+      else keyprep_chain<CurveP256W<20>>(keys, blob, idx, n, tidx, tn, s);
+      break;
     case CLS_P384: keyprep_chain<CurveP384>(keys, blob, idx, n, tidx, tn, s); break;
     case CLS_P521: keyprep_chain<CurveP521>(keys, blob, idx, n, tidx, tn, s); break;
     default: break;

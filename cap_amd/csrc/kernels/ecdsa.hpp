@@ -21,6 +21,7 @@ struct EcArgs {
   int32_t* exc_list;          // padded indices needing the exact path
   uint32_t* exc_count;
   int64_t npad, begin, end;
+  int32_t wq;                 // comb width of the keys' tables (P-256: 20 / 22 / 24, else 16)
 };
 
 // table geometry per curve: words per entry (x,y Montgomery limbs, 16-B aligned)
@@ -42,20 +43,35 @@ constexpr int ec_order_bits(int cls) { return cls == jgk::CLS_P256 ? 256 : cls =
 //   P-384: G W=20 (20 windows, 1.3 GB), keys W=16 (25 windows, 105 MB): 44 (65 at 12/12)
 //   P-521: G W=20 (27 windows, 2.3 GB), keys W=16 (33 windows, 173 MB): 59 (87 at 12/12)
 // The top window of each scalar (u < n) never carries out of the last digit.
+// ec_comb_w(cls, false) is the narrowest key window; P-256 keys get a wider
+// one when few keys share the context's table budget (ec_key_w below).
 constexpr int ec_comb_w(int cls, bool gen) {
   return cls == jgk::CLS_P256 ? (gen ? 26 : 20) : (gen ? 20 : 16);
 }
+constexpr int ec_windows_w(int cls, int w) { return (ec_order_bits(cls) + 1 + w - 1) / w; }
 constexpr int ec_entries(int cls, bool gen) { return 1 << (ec_comb_w(cls, gen) - 1); }
-constexpr int ec_windows(int cls, bool gen) {
-  return (ec_order_bits(cls) + 1 + ec_comb_w(cls, gen) - 1) / ec_comb_w(cls, gen);
-}
+constexpr int ec_windows(int cls, bool gen) { return ec_windows_w(cls, ec_comb_w(cls, gen)); }
 // digit rows of the scalar -> point hand-off: one int32 row per window, the
-// u1 (generator) digits first, then the u2 (key) digits
+// u1 (generator) digits first, then the u2 (key) digits (rows for the
+// narrowest key window, which has the most windows)
 constexpr int ec_digit_rows(int cls) { return ec_windows(cls, true) + ec_windows(cls, false); }
 // comb-table budget: at most this many keys of a class per jg_keys_load
 constexpr int ec_max_keys(int cls) { return 256; }
-constexpr int64_t ec_table_words(int cls, bool gen) {
-  return (int64_t)ec_windows(cls, gen) * ec_entries(cls, gen) * ec_stride(cls);
+constexpr int64_t ec_table_words_w(int cls, int w) {
+  return (int64_t)ec_windows_w(cls, w) * (1 << (w - 1)) * ec_stride(cls);
+}
+constexpr int64_t ec_table_words(int cls, bool gen) { return ec_table_words_w(cls, ec_comb_w(cls, gen)); }
+// Key-table width tiers of P-256 (HBM for fewer additions, as the generator's
+// W = 26 does): the widest W whose tables for all `nkeys` keys fit `budget`
+// bytes -- W = 24: 11 windows, 7.4 GB per key (21 additions per token);
+// W = 22: 12 windows, 2.0 GB (21 + 1); W = 20: 13 windows, 545 MB (22), always
+// allowed.  Other curves keep W = 16.
+constexpr int EC_P256_WQ[3] = {24, 22, 20};
+inline int ec_key_w(int cls, int nkeys, uint64_t budget) {
+  if (cls != jgk::CLS_P256) return ec_comb_w(cls, false);
+  for (int w : EC_P256_WQ)
+    if ((uint64_t)nkeys * (uint64_t)ec_table_words_w(cls, w) * 4u <= budget) return w;
+  return ec_comb_w(cls, false);
 }
 
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);
@@ -63,7 +79,7 @@ void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);
 // Montgomery affine coordinates back to aux_off and build its comb table.
 // tidx[0..tn): the subset of idx whose tables are (re)built; the others' tables
 // are copied from a previous load by the runtime.
-void launch_ec_keyprep(int cls, jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx,
-                       int tn, hipStream_t s);
+void launch_ec_keyprep(int cls, int wq, jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n,
+                       const int32_t* tidx, int tn, hipStream_t s);
 // generator table for a curve into `tab` (ec_table_words(cls) words)
 void launch_ec_gtable(int cls, uint32_t* tab, hipStream_t s);

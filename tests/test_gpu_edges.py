@@ -62,6 +62,9 @@ def test_exact_path_is_exercised_per_curve():
     assert {crv_of[t["key"]] for t in exc} == {"P-256", "P-384", "P-521"}
     assert any(t["verdict"] == 1 for t in exc)
     ctx = _lib.Context()
+    # the fixtures' accepting exceptional tokens were searched for the 26/20
+    # comb (make_ec_edge_fixtures.py COMB_W): P-256 key tables at W = 20
+    ctx.set_table_budget(0)
     ctx.load_keys([H.abi_key(k) for k in d["keys"]])
     arena, slots = H.jobs_from_tokens(exc, kid_index)
     b = ctx.stage(arena)

@@ -198,3 +198,33 @@ def test_rsa_keys_above_4096_bits():
         want = int(jws.verify_sig(jws.parse_jws(t["token"]), okeys[t["key"]]))
         assert want == t["want"], t["name"]
         assert out[s] == want, t["name"]
+
+
+@pytest.mark.parametrize("tier", ["w24", "w22", "w20"])
+def test_p256_key_table_widths(tier):
+    """The P-256 key comb width follows the table budget (jg_set_table_budget,
+    ecdsa.hpp ec_key_w): W = 24 / 22 / 20 give the same verdicts as the oracle
+    on every golden token against every key, and on a random ES256 batch."""
+    from cap_amd import _lib
+    from oracle import jws
+    keys, toks = H.golden()
+    n256 = sum(1 for k in keys if k.get("kty") == "EC" and k.get("crv") == "P-256")
+    assert n256 >= 2
+    per_key = {"w24": 11 * (1 << 23) * 80, "w22": 12 * (1 << 21) * 80, "w20": 0}[tier]
+    ctx = _lib.Context()
+    ctx.set_table_budget(n256 * per_key)
+    ctx.load_keys([H.abi_key(k) for k in keys])
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    okeys = {k["kid"]: jws.Key.from_fixture(k) for k in keys}
+    sel = [t for t in toks if t["alg"] in ("ES256", "ES384", "ES512")]
+    cross = [dict(t, key=k["kid"]) for t in sel for k in keys if k.get("kty") == "EC"]
+    arena, slots = H.jobs_from_tokens(cross, kid_index)
+    out = ctx.verify(arena)
+    ctx.close()
+    bad = []
+    for t, s in zip(cross, slots):
+        p = jws.parse_jws(t["token"])
+        want = int(jws.verify_sig(p, okeys[t["key"]])) if p is not None else 0
+        if (0 if s is None else out[s]) != want:
+            bad.append((t["name"], t["key"]))
+    assert not bad, bad[:10]

@@ -22,9 +22,9 @@ import json
 import sys
 
 ALIASES = {  # bench.py mark name -> kernel symbol prefix
-    "p256_point": "void (anonymous namespace)::k_ec_point<(anonymous namespace)::CurveP256>",
+    "p256_point": "void (anonymous namespace)::k_ec_point<(anonymous namespace)::CurveP256W<",
     "p256_prep": "void (anonymous namespace)::k_prep<4, ",
-    "p256_scalar": "void (anonymous namespace)::k_ec_scalar_batch<(anonymous namespace)::CurveP256>",
+    "p256_scalar": "void (anonymous namespace)::k_ec_scalar_batch<(anonymous namespace)::CurveP256W<",
     "rsa2048_modexp": "void (anonymous namespace)::k_rsa_modexp<37, 2, 8>",
     "rsa2048_prep": "void (anonymous namespace)::k_prep<1, ",
     "rsa2048_pad": "(anonymous namespace)::k_rsa_pad",
