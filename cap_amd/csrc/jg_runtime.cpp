@@ -704,11 +704,22 @@ Marker marker(jg_batch* b, int cls) {
 // Launch the verify kernels of a staged plan on lane L.  With `marks` (a
 // timed resident run) the classes run in sequence on L.stream with a HIP event
 // after each kernel; otherwise classes with work run on their own streams.
-void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks) {
+// fanout: run the classes of a mixed plan on the lane's per-class streams
+// (resident batches); pipeline chunks keep them in order on the lane's own
+// stream unless CAPJWT_FANOUT=1 (measurement A/B)
+bool pipeline_fanout() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_FANOUT");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks, bool fanout = true) {
   const bool timed = marks && marks->timing;
   int nact = 0;
   for (int c = 1; c < NCLS; ++c) nact += P.ranges[c].end > P.ranges[c].begin;
-  const bool conc = !timed && nact > 1;
+  const bool conc = !timed && fanout && nact > 1;
   const int64_t np = P.npad;
   const hipStream_t s0 = L->stream;
   mark(marks, "begin");
@@ -926,7 +937,7 @@ void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok
     fa.perm = (int32_t*)S.bufs.perm.p;
     launch_plan_fill(fa, s);
   }
-  run_plan(d, &LN, &S.bufs, P, nullptr);
+  run_plan(d, &LN, &S.bufs, P, nullptr, pipeline_fanout());
   if (tr) HIPCHK(hipEventRecord(S.tr_c, s));
   S.h_verdict.get(std::max<size_t>(n, 1));
   launch_copy(S.bufs.verdict.p, S.h_verdict.dp, n, s);
