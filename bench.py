@@ -282,6 +282,10 @@ def measure_pcie(ctx, arena, toks, iters=5, chunks=(32768, 65536, 131072)):
     for ch in chunks:
         ctx.set_chunk(ch)
         best = float("inf")
+        # one untimed pass first: the pipeline slots size their buffers once
+        # per process (a long-running stream never pays that again)
+        if L.jg_verify_batch(ctx.h, pa.ptr, len(arena), tp, len(toks), out) != 0:
+            raise RuntimeError(ctx.error())
         for _ in range(iters):
             t0 = time.perf_counter()
             if L.jg_verify_batch(ctx.h, pa.ptr, len(arena), tp, len(toks), out) != 0:
@@ -298,7 +302,7 @@ def measure_pcie(ctx, arena, toks, iters=5, chunks=(32768, 65536, 131072)):
             "arena_bytes": len(arena), "h2d_bytes_per_token": bytes_per_tok,
             "raw_h2d_GBps": bw / 1e9, "h2d_bound": bw / bytes_per_tok,
             "note": "jg_verify_batch from pinned host memory (chunked H2D overlapping kernels + plan + D2H), "
-                    f"best of {iters}; h2d_bound = raw pinned H2D bandwidth / bytes per token; not the headline"}
+                    f"best of {iters} after one warm-up pass; h2d_bound = raw pinned H2D bandwidth / bytes per token; not the headline"}
 
 
 def measure_e2e(pool, kids_jwk, total, threads):

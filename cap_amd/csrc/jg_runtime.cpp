@@ -149,6 +149,15 @@ double cls_cost(int c) {
   }
 }
 
+// Grow-only buffers reallocate with 50 % headroom (2 MiB granules): a pipeline
+// slot whose chunks vary in size and class mix (scratch rows per class) grows
+// a few times, not at every larger chunk -- a reallocation costs a device
+// synchronisation (hipFree) or a page-locking pass (hipHostMalloc).
+inline size_t grow_size(size_t n, size_t cap) {
+  const size_t want = std::max(n, cap + cap / 2);
+  return (want + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+}
+
 struct Grow {                     // grow-only device allocation
   void* p = nullptr;
   size_t cap = 0;
@@ -157,9 +166,10 @@ struct Grow {                     // grow-only device allocation
     if (n > cap) {
       if (p) (void)hipFree(p);
       p = nullptr;
+      const size_t c = grow_size(n, cap);
       cap = 0;
-      HIPCHK(hipMalloc(&p, n));
-      cap = n;
+      HIPCHK(hipMalloc(&p, c));
+      cap = c;
     }
     return p;
   }
@@ -175,8 +185,8 @@ struct HGrow {                    // grow-only pinned host allocation
     if (n > cap) {
       if (p) (void)hipHostFree(p);
       p = dp = nullptr;
+      const size_t want = grow_size(n, cap);
       cap = 0;
-      const size_t want = std::max(n, cap + cap / 2);
       HIPCHK(hipHostMalloc(&p, want, hipHostMallocPortable | hipHostMallocMapped));
       HIPCHK(hipHostGetDevicePointer(&dp, p, 0));
       cap = want;
@@ -297,6 +307,8 @@ struct Slot {
   hipEvent_t tr_a = nullptr, tr_b = nullptr, tr_c = nullptr;   // CAPJWT_PIPE_TRACE: H2D start / end, kernels end
   double host_ms[4] = {};                                       // wait, plan, enqueue, of which H2D calls
   int chunk_no = 0;
+  size_t reserved = 0;             // chunk capacity (jobs) the buffers were sized for
+  uint64_t reserved_epoch = ~0ull; // key table they were sized against
   bool inflight = false;
   std::shared_ptr<Ticket> ticket;
   uint8_t* out = nullptr;
@@ -838,8 +850,48 @@ void finish_slot(Slot& S) {
 
 
 // Plan and enqueue one chunk toks[0..n) of an item on slot S.
+// Size a slot's buffers once for the pipeline's chunk capacity C and the
+// key table's classes (their largest scratch rows), so chunks of varying size
+// and class mix never reallocate in the stream (a hipFree synchronises the
+// device, a hipHostMalloc page-locks): ~1 GB of device scratch per slot at
+// C = 64 k for a context with RSA-4K keys, far less for ES256 alone.
+void reserve_slot(const jg_ctx* ctx, Slot& S, size_t C, size_t nbuckets, double bytes_per_job) {
+  const PlanBlock L(nbuckets, C);
+  S.h_meta.get(L.bytes);
+  S.h_verdict.get(C);
+  int sig_rows = 1, scratch_rows = 1;
+  bool rsa = false;
+  for (int c = 1; c < NCLS; ++c) {
+    if (ctx->cls_keys[c].empty()) continue;
+    sig_rows = std::max(sig_rows, cls_rows_sig(c, ctx->rsa4k_limbs));
+    scratch_rows = std::max(scratch_rows, cls_rows_scratch(c, ctx->rsa4k_limbs));
+    rsa = rsa || c <= CLS_RSA4K;
+  }
+  const size_t npad = C + (size_t)WAVE * nbuckets;
+  Bufs* B = &S.bufs;
+  B->arena.get((size_t)(bytes_per_job * 1.25 * (double)C) + ARENA_SLACK);
+  B->jobs.get(sizeof(JobDev) * npad);
+  B->perm.get(sizeof(int32_t) * npad);
+  B->sigw.get(sizeof(uint32_t) * sig_rows * npad);
+  B->dig.get(sizeof(uint32_t) * DIG_ROWS * npad);
+  B->status.get(npad);
+  B->siglen.get(sizeof(uint16_t) * npad);
+  B->vpad.get(npad);
+  B->verdict.get(C);
+  B->rows.get(sizeof(uint32_t) * (size_t)scratch_rows * npad);
+  if (rsa) B->pss.get(C * 2048);
+  B->exc.get(sizeof(int32_t) * npad);
+  S.reserved = C;
+  S.reserved_epoch = ctx->epoch;
+}
+
 void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok* toks, size_t n, uint8_t* out) {
   const auto t_start = std::chrono::steady_clock::now();
+  if (S.reserved != it.chunk || S.reserved_epoch != ctx->epoch) {
+    double bpj = 0;
+    for (size_t i = 0; i < std::min<size_t>(n, 256); ++i) bpj += (double)(tok_end(toks[i]) - toks[i].off);
+    reserve_slot(ctx, S, std::max(it.chunk, n), ctx->keys.size() + 1, n ? bpj / (double)std::min<size_t>(n, 256) : 512.0);
+  }
   // One pass over the caller's jobs: the arena span they use, the bucket
   // counts of the plan, and their copy into the pinned plan block.  The span
   // is DMAed straight from a pinned caller arena when it is compact, else
