@@ -89,12 +89,13 @@ def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged)
     return (adds - 1) * madd + madd_z1 + gsqr + 2 * gmul
 
 
-def p384_point_mads_per_token():
-    """P-384 (ecdsa.hpp: L = 15 28-bit limbs, G W = 20 / key W = 20/16): the hot
-    loop's mulf / sqrf use the special-form reduction, 4 signed MADs per row
-    (mp.hpp mont_reduce_p384); value folds through freduce (5 non-zero
-    constants of 2^384 mod p); final check with m+1's 12 non-zero limbs."""
-    return ec_point_mads_per_token(15, 4, 5, 20, 16, 384, 15 * 12, merged=False)
+def p384_point_mads_per_token(wq=20):
+    """P-384 (ecdsa.hpp: L = 15 28-bit limbs, G W = 20, key W = 20 / 18 / 16 by
+    the table budget -- 20 for config 3's single key): the hot loop's mulf /
+    sqrf use the special-form reduction, 4 signed MADs per row (mp.hpp
+    mont_reduce_p384); value folds through freduce (5 non-zero constants of
+    2^384 mod p); final check with m+1's 12 non-zero limbs."""
+    return ec_point_mads_per_token(15, 4, 5, 20, wq, 384, 15 * 12, merged=False)
 
 
 def ed25519_point_mads_per_token():

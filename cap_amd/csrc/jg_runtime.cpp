@@ -330,7 +330,7 @@ struct Item {                     // one device's share of a submission
 
 struct Device {
   int id = 0;
-  int p256_wq = 20;               // comb width of the loaded P-256 key tables
+  int ec_wq[NCLS] = {};           // comb width of the loaded EC key tables per curve
   Lane lane0;                     // resident batches, key loads, hashing
   uint32_t* gtab[NCLS] = {};
   uint32_t* btab = nullptr;
@@ -790,7 +790,7 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks, bool 
       ea.exc_list = (int32_t*)B->exc.p + r.begin;
       ea.exc_count = (uint32_t*)B->exc_cnt.p + c;
       ea.npad = np; ea.begin = r.begin; ea.end = r.end;
-      ea.wq = c == CLS_P256 ? d->p256_wq : ec_comb_w(c, false);
+      ea.wq = d->ec_wq[c];
       launch_ec(c, ea, s, marker(marks, c));
     } else {
       if (!d->btab) throw std::runtime_error("Ed25519 base table missing");
@@ -1082,7 +1082,7 @@ void wait_idle(Device* d) {
 
 // ---------------------------------------------------------------- keys
 struct StagedKeys {
-  int p256_wq = 20;                // comb width of this load's P-256 key tables (ecdsa.hpp ec_key_w)
+  int ec_wq[NCLS] = {};             // comb width of this load's EC key tables per curve (ecdsa.hpp ec_key_w)
   std::vector<DevKey> dk;
   std::vector<uint32_t> blob;      // host-initialised part of the device key blob
   uint64_t tab_words = 0;          // device-only tail: comb tables (built on the GPU)
@@ -1113,11 +1113,14 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
   hks.assign((size_t)nkeys, HostKey{});
   S.dk.assign((size_t)nkeys, DevKey{});
   S.tab_id.assign((size_t)nkeys, std::string());
-  // P-256 key tables: the widest comb whose tables for every P-256 key of the
-  // load fit the context's table budget (fewer additions per token)
-  int n256 = 0;
-  for (int i = 0; i < nkeys; ++i) n256 += keys[i].kind == JG_KEY_EC && keys[i].curve == JG_P256;
-  S.p256_wq = ec_key_w(CLS_P256, n256, table_budget);
+  // EC key tables: per curve, the widest comb whose tables for every key of
+  // that curve in the load fit the context's table budget (fewer additions)
+  int nec[4] = {};
+  for (int i = 0; i < nkeys; ++i)
+    if (keys[i].kind == JG_KEY_EC && keys[i].curve >= JG_P256 && keys[i].curve <= JG_P521) ++nec[keys[i].curve];
+  S.ec_wq[CLS_P256] = ec_key_w(CLS_P256, nec[JG_P256], table_budget);
+  S.ec_wq[CLS_P384] = ec_key_w(CLS_P384, nec[JG_P384], table_budget);
+  S.ec_wq[CLS_P521] = ec_key_w(CLS_P521, nec[JG_P521], table_budget);
   for (int i = 0; i < nkeys; ++i) {
     const jg_key& k = keys[i];
     HostKey& hk = hks[i];
@@ -1164,8 +1167,7 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
       K.cls = cls;
       K.kbytes = cb;
       K.aux_off = blob_alloc(S.blob, 2 * L);
-      const int wq = cls == CLS_P256 ? S.p256_wq : ec_comb_w(cls, false);
-      K.tab_off = tab_alloc(S, i, (uint64_t)ec_table_words_w(cls, wq));
+      K.tab_off = tab_alloc(S, i, (uint64_t)ec_table_words_w(cls, S.ec_wq[cls]));
       const size_t cl = k.coord_len > 0 ? (size_t)k.coord_len : 0;
       // crypto/ecdsa pointFromAffine: coordinates must fit the curve's bit size
       bool ok = k.x && k.y && cl > 0 && bitlen_be(k.x, cl) <= (cls == CLS_P521 ? 521 : cb * 8) &&
@@ -1202,8 +1204,7 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
     if ((int)S.ec_idx[c].size() > ec_max_keys(c))
       throw std::runtime_error(std::string(cls_name(c)) + ": at most " + std::to_string(ec_max_keys(c)) +
                                " keys per table (comb tables are " +
-                               std::to_string(ec_table_words_w(c, c == CLS_P256 ? S.p256_wq : ec_comb_w(c, false)) *
-                                              4 >> 20) + " MiB each)");
+                               std::to_string(ec_table_words_w(c, S.ec_wq[c]) * 4 >> 20) + " MiB each)");
   if ((int)S.ed_idx.size() > ED_MAX_KEYS)
     throw std::runtime_error("Ed25519: at most " + std::to_string(ED_MAX_KEYS) + " keys per table (comb tables are " +
                              std::to_string(ed_table_words(false) * 4 >> 20) + " MiB each)");
@@ -1249,7 +1250,7 @@ void ensure_tables(Device* d, const StagedKeys& S) {
 
 void load_keys_device(Device* d, const StagedKeys& S) {
   HIPCHK(hipSetDevice(d->id));
-  d->p256_wq = S.p256_wq;
+  for (int c = 0; c < NCLS; ++c) d->ec_wq[c] = S.ec_wq[c];
   hipStream_t s = d->lane0.stream;
   d->lane0.sync();
   if (d->copy) (void)hipStreamSynchronize(d->copy);
@@ -1286,7 +1287,7 @@ void load_keys_device(Device* d, const StagedKeys& S) {
     };
     std::vector<int32_t> build_ec[NCLS], build_ed;
     for (int c = CLS_P256; c <= CLS_P521; ++c)
-      split(S.ec_idx[c], (uint64_t)ec_table_words_w(c, c == CLS_P256 ? S.p256_wq : ec_comb_w(c, false)), build_ec[c]);
+      split(S.ec_idx[c], (uint64_t)ec_table_words_w(c, S.ec_wq[c]), build_ec[c]);
     split(S.ed_idx, (uint64_t)ed_table_words(false), build_ed);
     // one index array: rsa | p256 | p384 | p521 | ed | builds p256 | p384 | p521 | ed
     std::vector<int32_t> idx;
@@ -1302,7 +1303,7 @@ void load_keys_device(Device* d, const StagedKeys& S) {
     ensure_tables(d, S);
     if (!S.dk.empty()) launch_rsa_keyprep(d->dkeys, d->dblob, (int)S.dk.size(), s);
     for (int c = CLS_P256; c <= CLS_P521; ++c)
-      launch_ec_keyprep(c, c == CLS_P256 ? S.p256_wq : ec_comb_w(c, false), d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(),
+      launch_ec_keyprep(c, S.ec_wq[c], d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(),
                         d->didx + at[5 + c - CLS_P256], (int)build_ec[c].size(), s);
     launch_ed_keyprep(d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), d->didx + at[8],
                       (int)build_ed.size(), s);

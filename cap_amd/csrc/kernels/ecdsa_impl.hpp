@@ -1,0 +1,741 @@
+// ecdsa_impl.hpp -- ECDSA P-256 / P-384 / P-521 verification on gfx950: the
+// device code, included by one translation unit per curve (ecdsa_p256.hip,
+// ecdsa_p384.hip, ecdsa_p521.hip: each instantiates its curve's kernels for
+// every key-table width, compiled in parallel) and by the test kernels.
+//
+// Replaces go-jose ecEncrypterVerifier.verifyPayload -> crypto/ecdsa.Verify
+// (rules R18-R22).  Per token:
+//   k_ec_scalar_batch : r, s in [1, n-1] (sizes from the alg, curve from the
+//                 key), e = leftmost bits of H, w = s^-1 (one inversion per B
+//                 tokens), u1 = e w, u2 = r w (mod n), recoded to signed W-bit
+//                 digits (W = ec_comb_w: generator 24 / key 20 for P-256, 20 / 16 above)
+//   k_ec_point  : R = u1 G + u2 Q as a sum of one precomputed affine multiple of
+//                 G and one of Q per window (comb tables in HBM: entries
+//                 d * 2^(W w) * P, d = 1..2^(W-1)), mixed Jacobian+affine
+//                 additions, no doublings; accept iff X == r Z^2 or (r+n) Z^2
+//   k_ec_exact  : tokens whose fast sum hit an exceptional case of the group
+//                 law (Z == 0: a doubling, an inverse pair, or R = infinity) --
+//                 recomputed with complete case handling; rare
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "common.hpp"
+#include "ecdsa.hpp"
+#include "mp.hpp"
+
+using namespace jgk;
+
+namespace {
+
+// WQ: comb width of the key tables (ecdsa.hpp ec_key_w: P-256 keys 20 / 22 / 24,
+// P-384 / P-521 keys 16 / 18 / 20 by the context's table budget; one kernel
+// instantiation per width)
+template <int WQ_>
+struct CurveP256W { using Fp = P256P; using Fn = P256N; using C = P256C; static constexpr int CLS = CLS_P256, WQ = WQ_; };
+using CurveP256 = CurveP256W<20>;
+template <int WQ_>
+struct CurveP384W { using Fp = P384P; using Fn = P384N; using C = P384C; static constexpr int CLS = CLS_P384, WQ = WQ_; };
+using CurveP384 = CurveP384W<16>;
+template <int WQ_>
+struct CurveP521W { using Fp = P521P; using Fn = P521N; using C = P521C; static constexpr int CLS = CLS_P521, WQ = WQ_; };
+using CurveP521 = CurveP521W<16>;
+
+__device__ __forceinline__ int es_size(int alg) { return alg == 7 ? 32 : alg == 8 ? 48 : 66; }
+__device__ __forceinline__ int es_hash_bytes(int alg) { return alg == 7 ? 32 : alg == 8 ? 48 : 64; }
+
+// plain-integer compare of normalized limbs: a < b
+template <int L>
+__device__ __forceinline__ bool lt_limbs(const uint32_t* a, const uint32_t* b) {
+  int lt = 0, gt = 0;
+#pragma unroll
+  for (int j = L - 1; j >= 0; --j) {
+    const int und = !(lt | gt);
+    lt |= und & (a[j] < b[j]);
+    gt |= und & (a[j] > b[j]);
+  }
+  return lt;
+}
+template <int L>
+__device__ __forceinline__ bool zero_limbs(const uint32_t* a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < L; ++j) o |= a[j];
+  return o == 0;
+}
+
+// ------------------------------------------------------------------ scalar
+// Per-token checks and inputs of the scalar stage.  Returns ok; r, s, e as
+// plain 28-bit limbs (s replaced by 1 when the token is rejected, so the batch
+// product stays invertible).
+template <class CV>
+__device__ __forceinline__ bool ec_scalar_inputs(const EcArgs& a, int64_t p, uint32_t* r, uint32_t* s, uint32_t* e) {
+  using Fn = typename CV::Fn;
+  constexpr int L = Fn::L;
+  constexpr int CB = CV::C::BYTES;
+  const int64_t np = a.npad;
+  const JobDev jb = a.jobs[p];
+  if (!job_live(jb)) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) { r[j] = 0; e[j] = 0; s[j] = j == 0 ? 1u : 0u; }
+    return false;
+  }
+  const int kidx = job_key(jb);
+  const int alg = job_alg(jb);
+  // R18/R21: the signature size comes from the alg, the curve from the key
+  // (go-jose ecEncrypterVerifier: keySize by alg, no curve check), so r and s
+  // are es_size(alg)-byte integers that must be < n of the key's curve.  Prep
+  // leaves them in rows [0, ..) and [EC_S_ROW, ..), zero above what it wrote
+  // up to this curve's CW words; an alg whose r/s are longer than the curve's
+  // (ES512 on a P-256 key) must have zero words past CB as well.
+  bool ok = a.status[p] == ST_OK && a.keys[kidx].valid;
+  constexpr int CW = ec_sig_words(CV::CLS);
+  uint32_t rw[CW], sw[CW];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    rw[q] = a.sigw[(int64_t)q * np + p];
+    sw[q] = a.sigw[(int64_t)(EC_S_ROW + q) * np + p];
+  }
+  if constexpr (4 * CW > CB) {
+    const uint32_t hi = ~0u << (8 * (CB - 4 * (CW - 1)));
+    ok = ok && (rw[CW - 1] & hi) == 0 && (sw[CW - 1] & hi) == 0;
+  }
+  if (es_size(alg) > CB) {
+    const int aw = (es_size(alg) + 3) / 4;      // words prep wrote for this alg
+    for (int q = CW; q < aw; ++q)
+      ok = ok && a.sigw[(int64_t)q * np + p] == 0 && a.sigw[(int64_t)(EC_S_ROW + q) * np + p] == 0;
+  }
+  mp::words_to_limbs<L, CW>(r, rw);
+  mp::words_to_limbs<L, CW>(s, sw);
+  uint32_t nl[L];
+  mp::set_const<Fn>(nl, Fn::M);
+  ok = ok && !zero_limbs<L>(r) && !zero_limbs<L>(s) && lt_limbs<L>(r, nl) && lt_limbs<L>(s, nl);
+  {
+    const int hl = es_hash_bytes(alg) < CB ? es_hash_bytes(alg) : CB;   // multiple of 4
+    uint32_t ew[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int src = hl / 4 - 1 - q;
+      ew[q] = src >= 0 ? a.dig[(int64_t)(src < 0 ? 0 : src) * np + p] : 0u;
+    }
+    mp::words_to_limbs<L, 16>(e, ew);
+    mp::csub<Fn>(e);
+  }
+  if (!ok) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) s[j] = j == 0 ? 1u : 0u;
+  }
+  return ok;
+}
+
+// Signed W-bit recoding: u = sum_w d_w 2^(W w), d_w in [-2^(W-1), 2^(W-1)),
+// one int32 row per window starting at digit row `row0`.
+template <class CV, int W, int NWIN>
+__device__ __forceinline__ void store_digit_rows(const EcArgs& a, int64_t p, const uint32_t* u, int row0) {
+  constexpr int L = CV::Fn::L;
+  constexpr uint32_t DM = (1u << W) - 1u;
+  int c = 0;
+#pragma unroll
+  for (int w = 0; w < NWIN; ++w) {
+    const int bit = W * w, q = bit / MP_W, sh = bit % MP_W;
+    uint32_t b = q < L ? (u[q] >> sh) : 0u;
+    if (sh > MP_W - W && q + 1 < L) b |= u[q + 1] << (MP_W - sh);
+    int v = (int)(b & DM) + c;
+    c = v >= (1 << (W - 1));
+    v -= c << W;
+    a.digs[(int64_t)(row0 + w) * a.npad + p] = (uint32_t)v;
+  }
+}
+
+template <class CV>
+__device__ __forceinline__ void store_digits(const EcArgs& a, int64_t p, const uint32_t* u1, const uint32_t* u2) {
+  constexpr int WG = ec_comb_w(CV::CLS, true), NG = ec_windows(CV::CLS, true);
+  constexpr int WQ = CV::WQ, NQ = ec_windows_w(CV::CLS, CV::WQ);
+  store_digit_rows<CV, WG, NG>(a, p, u1, 0);
+  store_digit_rows<CV, WQ, NQ>(a, p, u2, NG);
+}
+
+// Batched scalar stage (Montgomery's trick): thread i owns the B tokens
+// p_j = begin + i + j*S and pays ONE (safegcd) inversion for all of them:
+//   pass 1: c_j = s_0 ... s_j (Montgomery), c_j and s_j parked in the u1/u2 rows
+//   inv = c_{B-1}^-1
+//   pass 2 (j descending): w_j = inv * c_{j-1}, inv *= s_j;
+//           u1 = e w_j, u2 = r w_j (mod n), signed W-bit digits
+template <class CV>
+__global__ void __launch_bounds__(64) k_ec_scalar_batch(EcArgs a, int B) {
+  using Fn = typename CV::Fn;
+  constexpr int L = Fn::L;
+  const int64_t np = a.npad;
+  const int64_t n = a.end - a.begin;
+  const int64_t S = (n + B - 1) / B;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S) return;
+  uint32_t acc[L];
+  mp::set_const<Fn>(acc, Fn::ONE);
+  int nb = 0;
+  for (int j = 0; j < B; ++j) {
+    const int64_t p = a.begin + i + (int64_t)j * S;
+    if (p >= a.end) break;
+    uint32_t r[L], s[L], e[L], sm[L];
+    const bool ok = ec_scalar_inputs<CV>(a, p, r, s, e);
+    if (!ok && job_live(a.jobs[p])) a.status[p] = ST_REJECT;
+    mp::to_mont<Fn>(sm, s);
+    mp::mul<Fn>(acc, acc, sm);
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+      a.u1w[(int64_t)k * np + p] = acc[k];
+      a.u2w[(int64_t)k * np + p] = sm[k];
+    }
+    ++nb;
+  }
+  uint32_t inv[L];
+  mp::inv<Fn>(inv, acc);
+  for (int j = nb - 1; j >= 0; --j) {
+    const int64_t p = a.begin + i + (int64_t)j * S;
+    uint32_t cprev[L], sm[L], w[L];
+    if (j > 0) {
+      const int64_t pp = p - S;
+#pragma unroll
+      for (int k = 0; k < L; ++k) cprev[k] = a.u1w[(int64_t)k * np + pp];
+    } else {
+      mp::set_const<Fn>(cprev, Fn::ONE);
+    }
+#pragma unroll
+    for (int k = 0; k < L; ++k) sm[k] = a.u2w[(int64_t)k * np + p];
+    mp::mul<Fn>(w, inv, cprev);                  // s_j^-1 R
+    mp::mul<Fn>(inv, inv, sm);
+    uint32_t r[L], s[L], e[L], u1[L], u2[L];
+    (void)ec_scalar_inputs<CV>(a, p, r, s, e);
+    mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
+    mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
+    store_digits<CV>(a, p, u1, u2);       // (the rare exact path recomputes u1, u2 itself)
+  }
+}
+
+// ------------------------------------------------------------------ point ops
+// Y3 = r t - Y1 hhh.  Fields with the column headroom (sum_ok) take both
+// products under ONE Montgomery reduction: (r t + (KSUB - Y1) hhh) / R, with
+// r, t < 3*2^28 limbs and KSUB - Y1 < 2^29, hhh < 2^28 (values < 6m, 6m, 4m,
+// 2m: the sum is < 44 m^2, far below R m), so Y3 comes out normalized with no
+// subtraction and no value fold.  P-384 keeps two special-form products.
+template <class Fp>
+constexpr bool sum_ok() {
+  if constexpr (std::is_same<Fp, P384P>::value) {
+    return false;
+  } else {
+    uint32_t kmax = 0;
+    for (int j = 0; j < Fp::L; ++j) kmax = Fp::KSUB[j] > kmax ? Fp::KSUB[j] : kmax;
+    double red = 0;
+    if constexpr (Fp::NP1)
+      for (int j = 1; j < Fp::L; ++j) red += (double)Fp::M1[j] / 16777216.0;
+    else
+      red = 16.0 * Fp::L;
+    return 9.0 * Fp::L + Fp::L * (double)kmax / 268435456.0 + red + 1.0 < 256.0;
+  }
+}
+
+template <class Fp>
+__device__ __forceinline__ void y3_from(uint32_t* Y, const uint32_t* r, const uint32_t* t, const uint32_t* y1,
+                                        const uint32_t* hhh) {
+  constexpr int L = Fp::L;
+  if constexpr (sum_ok<Fp>()) {
+    uint32_t ny1[L];
+    mp::neg<Fp>(ny1, y1);
+    uint64_t T[2 * L];
+    mp::prod<Fp>(T, r, t);
+    mp::prod_acc<Fp>(T, ny1, hhh);
+    mp::mont_reduce<Fp>(Y, T);
+  } else {
+    uint32_t u[L];
+    mp::mulf<Fp>(Y, r, t);
+    mp::mulf<Fp>(u, y1, hhh);
+    mp::sub<Fp>(Y, Y, u); mp::freduce_lazy<Fp>(Y);
+  }
+}
+
+// X3 = r^2 - hhh - 2v.  Fields with a column constant KX3 (P-256,
+// tools/gen_field_consts.py XCOL) subtract inside r^2's high columns:
+// (r^2 + (KX3 - hhh - 2v) R) / R, where KX3 = 8m has every limb >= 3(2^28-1),
+// so KX3 - hhh - 2v >= 0 limb by limb.  X3 then comes out of the reduction
+// with 28-bit limbs and value < 8m + r^2/R + (1 + 2^-24) m < 10m: no value
+// fold.  Subtractions with X as the subtrahend use KSUBX (16m, covers < 10m).
+template <class Fp, class = void>
+struct has_kx3 : std::false_type {};
+template <class Fp>
+struct has_kx3<Fp, std::void_t<decltype(Fp::KX3)>> : std::true_type {};
+
+template <class Fp>
+__device__ __forceinline__ void x3_from(uint32_t* X, const uint32_t* r, const uint32_t* hhh, const uint32_t* v) {
+  constexpr int L = Fp::L;
+  if constexpr (has_kx3<Fp>::value) {
+    uint64_t T[2 * L];
+    mp::sqprod<Fp>(T, r);
+    const uint32_t c1 = (uint32_t)mp::opaque_sgpr(1);
+#pragma unroll
+    for (int j = 0; j < L; ++j) T[L + j] += (uint64_t)(Fp::KX3[j] - (hhh[j] + 2 * v[j])) * c1;
+    mp::mont_reduce<Fp>(X, T);
+  } else {
+    uint32_t r2[L];
+    mp::sqrf<Fp>(r2, r);
+    mp::sub<Fp>(X, r2, hhh); mp::sub<Fp>(X, X, v); mp::sub<Fp>(X, X, v); mp::freduce_lazy<Fp>(X);
+  }
+}
+
+// a - X for an X produced by x3_from (value < 10m on KX3 fields)
+template <class Fp>
+__device__ __forceinline__ void sub_x(uint32_t* r, const uint32_t* a, const uint32_t* x) {
+  if constexpr (has_kx3<Fp>::value) {
+#pragma unroll
+    for (int j = 0; j < Fp::L; ++j) r[j] = a[j] + Fp::KSUBX[j] - x[j];
+  } else {
+    mp::sub<Fp>(r, a, x);
+  }
+}
+
+// Mixed addition P1 (Jacobian; X < 10m on KX3 fields, else < 2m; Y, Z < 2m,
+// 28-bit limbs) += P2 (affine x2, y2).
+// 8M + 3S, lazy; X3, Y3 value-reduced so they can be subtrahends.
+// Products go through mulf / sqrf (P-384: special-form reduction, which needs
+// one operand with 28-bit limbs per product -- h and r are normalised for it).
+// Z1Z1 is semi-normalized where the field allows (mp::sqr_semi): both its
+// consumers multiply it by an operand with 28-bit limbs (x2, Z).
+// An exceptional pair (P1 == +-P2) yields H == 0 and so Z3 == 0, which is
+// absorbing in later additions and is detected at the end.
+template <class Fp>
+__device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, const uint32_t* x2, const uint32_t* y2) {
+  constexpr int L = Fp::L;
+  uint32_t z1z1[L], u2[L], t[L], s2[L], h[L], r[L], hh[L], hhh[L], v[L];
+  mp::sqr_semi<Fp>(z1z1, Z);
+  mp::mulf<Fp>(u2, x2, z1z1);
+  mp::mulf<Fp>(t, Z, z1z1);
+  mp::mulf<Fp>(s2, y2, t);
+  sub_x<Fp>(h, u2, X);
+  mp::sub<Fp>(r, s2, Y);
+  mp::norm_for_mulf<Fp>(h);                  // P-384: h, r are squared (mulf precondition)
+  mp::norm_for_mulf<Fp>(r);
+  mp::sqrf<Fp>(hh, h);
+  mp::mulf<Fp>(hhh, h, hh);
+  mp::mulf<Fp>(v, X, hh);
+  mp::mulf<Fp>(Z, Z, h);
+  uint32_t y1[L];
+  mp::copy<Fp>(y1, Y);
+  x3_from<Fp>(X, r, hhh, v);
+  // Y3 = r (v - X3) - Y1 hhh
+  sub_x<Fp>(t, v, X);
+  y3_from<Fp>(Y, r, t, y1, hhh);
+}
+
+// madd with Z1 == 1 (P1 affine: the accumulator after its first assignment):
+// u2 = x2, s2 = y2, Z3 = h -- 4M + 2S instead of 8M + 3S.
+template <class Fp>
+__device__ __forceinline__ void madd_z1(uint32_t* X, uint32_t* Y, uint32_t* Z, const uint32_t* x2, const uint32_t* y2) {
+  constexpr int L = Fp::L;
+  uint32_t h[L], r[L], hh[L], hhh[L], v[L], t[L], y1[L];
+  mp::sub<Fp>(h, x2, X);
+  mp::sub<Fp>(r, y2, Y);
+  mp::norm<Fp>(h);                           // Z3 = h: 28-bit limbs (mulf operand), value < 6m
+  mp::norm<Fp>(r);                           // y2 may be negated (limbs < 2^29): keep r^2's columns in range
+  mp::sqrf<Fp>(hh, h);
+  mp::mulf<Fp>(hhh, h, hh);
+  mp::mulf<Fp>(v, X, hh);
+  mp::copy<Fp>(Z, h);
+  mp::copy<Fp>(y1, Y);
+  x3_from<Fp>(X, r, hhh, v);
+  sub_x<Fp>(t, v, X);
+  y3_from<Fp>(Y, r, t, y1, hhh);
+}
+
+// Z1ONE: the accumulator, if not empty, holds exactly one table entry (Z == 1)
+template <class CV, bool GEN, bool Z1ONE = false>
+__device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z, bool& empty,
+                                           const uint32_t* __restrict__ tab, int w, int d) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS), NE = GEN ? ec_entries(CV::CLS, true) : 1 << (CV::WQ - 1);
+  if (d == 0) return;
+  const int ad = d < 0 ? -d : d;
+  const uint32_t* ent = tab + ((int64_t)w * NE + (ad - 1)) * STRIDE;
+  uint32_t x2[L], y2[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) { x2[j] = ent[j]; y2[j] = ent[L + j]; }
+  if (d < 0) mp::neg<Fp>(y2, y2);
+  if (empty) {
+    mp::copy<Fp>(X, x2);
+    mp::copy<Fp>(Y, y2); mp::freduce<Fp>(Y);
+    mp::set_const<Fp>(Z, Fp::ONE);
+    empty = false;
+  } else if constexpr (Z1ONE) {
+    madd_z1<Fp>(X, Y, Z, x2, y2);
+  } else {
+    madd<Fp>(X, Y, Z, x2, y2);
+  }
+}
+
+template <class CV>
+__global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
+  using Fp = typename CV::Fp;
+  using Fn = typename CV::Fn;
+  constexpr int L = Fp::L;
+  constexpr int NG = ec_windows(CV::CLS, true), NQ = ec_windows_w(CV::CLS, CV::WQ);
+  constexpr int NWIN = NG > NQ ? NG : NQ;
+  const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
+  const int64_t np = a.npad;
+  const JobDev jb = a.jobs[p];
+  if (!job_live(jb)) return;
+  if (a.status[p] != ST_OK) { a.verdict_pad[p] = 0; return; }
+  const int kidx = __builtin_amdgcn_readfirstlane(job_key(jb));
+  const uint32_t* __restrict__ qtab = a.keyblob + a.keys[kidx].tab_off;
+  const uint32_t* __restrict__ gtab = a.gtab;
+
+  uint32_t X[L], Y[L], Z[L];
+  bool empty = true;
+  // window 0 peeled: its G entry is an assignment, so its Q entry adds onto Z == 1
+  add_window<CV, true>(X, Y, Z, empty, gtab, 0, (int)a.digs[p]);
+  add_window<CV, false, true>(X, Y, Z, empty, qtab, 0, (int)a.digs[(int64_t)NG * np + p]);
+  for (int w = 1; w < NWIN; ++w) {
+    if (w < NG) add_window<CV, true>(X, Y, Z, empty, gtab, w, (int)a.digs[(int64_t)w * np + p]);
+    if (w < NQ) add_window<CV, false>(X, Y, Z, empty, qtab, w, (int)a.digs[(int64_t)(NG + w) * np + p]);
+  }
+  if (empty) { a.verdict_pad[p] = 0; return; }           // R = infinity (unreachable: u2 != 0)
+  uint32_t zc[L];
+  mp::copy<Fp>(zc, Z);
+  mp::canon<Fp>(zc);
+  if (mp::is_zero_canon<Fp>(zc)) {                        // exceptional case: exact recompute
+    const uint32_t idx = atomicAdd(a.exc_count, 1u);
+    a.exc_list[idx] = (int32_t)p;
+    a.status[p] = ST_EXCEPTIONAL;
+    return;
+  }
+  // x(R) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2)
+  constexpr int CW = ec_sig_words(CV::CLS);
+  uint32_t rw[CW], r[L];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) rw[q] = a.sigw[(int64_t)q * np + p];
+  mp::words_to_limbs<L, CW>(r, rw);
+  uint32_t zz[L], rm[L], tt[L];
+  mp::sqr<Fp>(zz, Z);
+  mp::to_mont<Fp>(rm, r);
+  mp::mul<Fp>(tt, rm, zz);
+  bool ok = mp::eq_mod<Fp>(X, tt);
+  if (!ok) {
+    uint32_t rn[L], pl[L];
+    mp::add<Fp>(rn, r, Fn::M);
+    mp::norm<Fp>(rn);
+    mp::set_const<Fp>(pl, Fp::M);
+    if (lt_limbs<L>(rn, pl)) {
+      mp::to_mont<Fp>(rm, rn);
+      mp::mul<Fp>(tt, rm, zz);
+      ok = mp::eq_mod<Fp>(X, tt);
+    }
+  }
+  a.verdict_pad[p] = ok;
+}
+
+// ------------------------------------------------------------------ exact path
+// Jacobian points with an explicit infinity flag; every coordinate kept
+// normalized (< 2p) so any of them can be a subtrahend.
+template <class Fp>
+struct JPt { uint32_t X[Fp::L], Y[Fp::L], Z[Fp::L]; bool inf; };
+
+template <class Fp>
+__device__ bool is_zero_mod(const uint32_t* a) {
+  uint32_t c[Fp::L];
+  mp::copy<Fp>(c, a);
+  mp::canon<Fp>(c);
+  return mp::is_zero_canon<Fp>(c);
+}
+
+template <class Fp>
+__device__ void times2(uint32_t* r, const uint32_t* a) {     // r = 2a, normalized
+  mp::add<Fp>(r, a, a);
+  mp::freduce<Fp>(r);
+}
+
+template <class CV>
+__device__ void jdbl(JPt<typename CV::Fp>& R, const JPt<typename CV::Fp>& P) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  if (P.inf || is_zero_mod<Fp>(P.Y)) { R.inf = true; return; }
+  uint32_t delta[L], gamma[L], beta[L], t1[L], t2[L], alpha[L], b2[L], b4[L], b8[L], x3[L], y3[L], z3[L];
+  mp::sqr<Fp>(delta, P.Z);
+  mp::sqr<Fp>(gamma, P.Y);
+  mp::mul<Fp>(beta, P.X, gamma);
+  mp::sub<Fp>(t1, P.X, delta);
+  mp::add<Fp>(t2, P.X, delta);
+  mp::mul<Fp>(alpha, t1, t2);
+  uint32_t three[L];
+  mp::set_const<Fp>(three, CV::C::THREE_M);
+  mp::mul<Fp>(alpha, alpha, three);                 // 3 (X - delta)(X + delta)
+  times2<Fp>(b2, beta); times2<Fp>(b4, b2); times2<Fp>(b8, b4);
+  mp::sqr<Fp>(x3, alpha);
+  mp::sub<Fp>(x3, x3, b8); mp::freduce<Fp>(x3);     // X3 = alpha^2 - 8 beta
+  mp::mul<Fp>(z3, P.Y, P.Z);
+  times2<Fp>(z3, z3);                               // Z3 = 2 Y Z
+  mp::sub<Fp>(t1, b4, x3);
+  mp::mul<Fp>(y3, alpha, t1);
+  mp::sqr<Fp>(t2, gamma);
+  times2<Fp>(t2, t2); times2<Fp>(t2, t2); times2<Fp>(t2, t2);
+  mp::sub<Fp>(y3, y3, t2); mp::freduce<Fp>(y3);     // Y3 = alpha (4 beta - X3) - 8 gamma^2
+  mp::copy<Fp>(R.X, x3); mp::copy<Fp>(R.Y, y3); mp::copy<Fp>(R.Z, z3);
+  R.inf = false;
+}
+
+template <class CV>
+__device__ void jadd(JPt<typename CV::Fp>& R, const JPt<typename CV::Fp>& P, const JPt<typename CV::Fp>& Q) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  if (P.inf) { R = Q; return; }
+  if (Q.inf) { R = P; return; }
+  uint32_t z1z1[L], z2z2[L], u1[L], u2[L], s1[L], s2[L], t[L], h[L], rr[L];
+  mp::sqr<Fp>(z1z1, P.Z); mp::sqr<Fp>(z2z2, Q.Z);
+  mp::mul<Fp>(u1, P.X, z2z2); mp::mul<Fp>(u2, Q.X, z1z1);
+  mp::mul<Fp>(t, Q.Z, z2z2); mp::mul<Fp>(s1, P.Y, t);
+  mp::mul<Fp>(t, P.Z, z1z1); mp::mul<Fp>(s2, Q.Y, t);
+  mp::sub<Fp>(h, u2, u1); mp::freduce<Fp>(h);
+  mp::sub<Fp>(rr, s2, s1); mp::freduce<Fp>(rr);
+  if (is_zero_mod<Fp>(h)) {
+    if (is_zero_mod<Fp>(rr)) { jdbl<CV>(R, P); return; }
+    R.inf = true;
+    return;
+  }
+  uint32_t hh[L], hhh[L], v[L], x3[L], y3[L], z3[L];
+  mp::sqr<Fp>(hh, h); mp::mul<Fp>(hhh, h, hh); mp::mul<Fp>(v, u1, hh);
+  mp::add<Fp>(t, hhh, v); mp::add<Fp>(t, t, v); mp::freduce<Fp>(t);
+  mp::sqr<Fp>(x3, rr); mp::sub<Fp>(x3, x3, t); mp::freduce<Fp>(x3);
+  mp::sub<Fp>(t, v, x3); mp::mul<Fp>(y3, rr, t);
+  mp::mul<Fp>(t, s1, hhh); mp::sub<Fp>(y3, y3, t); mp::freduce<Fp>(y3);
+  mp::mul<Fp>(t, P.Z, Q.Z); mp::mul<Fp>(z3, t, h);
+  mp::copy<Fp>(R.X, x3); mp::copy<Fp>(R.Y, y3); mp::copy<Fp>(R.Z, z3);
+  R.inf = false;
+}
+
+template <class CV>
+__device__ void affine_point(JPt<typename CV::Fp>& P, const uint32_t* xm, const uint32_t* ym) {
+  using Fp = typename CV::Fp;
+  mp::copy<Fp>(P.X, xm); mp::copy<Fp>(P.Y, ym); mp::set_const<Fp>(P.Z, Fp::ONE);
+  P.inf = false;
+}
+
+template <class CV>
+__global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
+  using Fp = typename CV::Fp;
+  using Fn = typename CV::Fn;
+  constexpr int L = Fp::L;
+  const uint32_t cnt = *a.exc_count;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    const int64_t p = a.exc_list[i];
+    const int kidx = job_key(a.jobs[p]);
+    const uint32_t* aux = a.keyblob + a.keys[kidx].aux_off;
+    // u1 = e / s, u2 = r / s (mod n), recomputed with one inversion per token
+    // (the status goes back to OK first: ec_scalar_inputs checks it)
+    a.status[p] = ST_OK;
+    uint32_t r[L], s[L], e[L], sm[L], w[L], u1[L], u2[L];
+    (void)ec_scalar_inputs<CV>(a, p, r, s, e);
+    mp::to_mont<Fn>(sm, s);
+    mp::inv<Fn>(w, sm);                          // s^-1 R
+    mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
+    mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
+    JPt<Fp> G, Q, GQ, R;
+    uint32_t gx[L], gy[L];
+    mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
+    affine_point<CV>(G, gx, gy);
+    affine_point<CV>(Q, aux, aux + L);
+    jadd<CV>(GQ, G, Q);
+    R.inf = true;
+    for (int b = Fn::BITS - 1; b >= 0; --b) {
+      jdbl<CV>(R, R);
+      const int q = b / MP_W, sh = b % MP_W;
+      const bool b1 = (u1[q] >> sh) & 1u, b2 = (u2[q] >> sh) & 1u;
+      if (b1 && b2) jadd<CV>(R, R, GQ);
+      else if (b1) jadd<CV>(R, R, G);
+      else if (b2) jadd<CV>(R, R, Q);
+    }
+    bool ok = false;
+    if (!R.inf) {
+      uint32_t zi[L], zi2[L], xa[L], x[L];
+      mp::inv<Fp>(zi, R.Z);
+      mp::sqr<Fp>(zi2, zi);
+      mp::mul<Fp>(xa, R.X, zi2);
+      mp::from_mont<Fp>(x, xa);                  // canonical x < p
+      // x mod n (x < p < 2n)
+      uint32_t nl[L], d[L];
+      mp::set_const<Fp>(nl, Fn::M);
+      if (!lt_limbs<L>(x, nl)) {
+        int32_t br = 0;
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const int32_t tt = (int32_t)x[j] - (int32_t)nl[j] + br;
+          d[j] = (uint32_t)tt & MP_MASK;
+          br = tt >> MP_W;
+        }
+        mp::copy<Fp>(x, d);
+      }
+      uint32_t o = 0;
+#pragma unroll
+      for (int j = 0; j < L; ++j) o |= x[j] ^ r[j];
+      ok = o == 0;
+    }
+    a.verdict_pad[p] = ok;
+    a.status[p] = ST_OK;
+  }
+}
+
+// ------------------------------------------------------------------ staging
+// thread per key: validate (coordinates < p, on the curve) and convert to Montgomery
+template <class CV>
+__global__ void k_ec_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DevKey& K = keys[idx[i]];
+  uint32_t* aux = blob + K.aux_off;
+  uint32_t x[L], y[L], pl[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) { x[j] = aux[j]; y[j] = aux[L + j]; }
+  mp::set_const<Fp>(pl, Fp::M);
+  bool ok = K.valid && lt_limbs<L>(x, pl) && lt_limbs<L>(y, pl);
+  uint32_t xm[L], ym[L], lhs[L], rhs[L], t[L], three[L], b[L];
+  mp::to_mont<Fp>(xm, x);
+  mp::to_mont<Fp>(ym, y);
+  mp::sqr<Fp>(lhs, ym);
+  mp::sqr<Fp>(t, xm); mp::mul<Fp>(rhs, t, xm);
+  mp::set_const<Fp>(three, CV::C::THREE_M);
+  mp::mul<Fp>(t, xm, three);
+  mp::sub<Fp>(rhs, rhs, t);
+  mp::set_const<Fp>(b, CV::C::B_M);
+  mp::add<Fp>(rhs, rhs, b);
+  ok = ok && mp::eq_mod<Fp>(rhs, lhs);
+  mp::canon<Fp>(xm); mp::canon<Fp>(ym);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { aux[j] = xm[j]; aux[L + j] = ym[j]; }
+  K.valid = ok ? 1 : 0;
+}
+
+template <class CV>
+__device__ void store_affine(uint32_t* out, const JPt<typename CV::Fp>& P) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  uint32_t zi[L], zi2[L], zi3[L], x[L], y[L];
+  mp::inv<Fp>(zi, P.Z);
+  mp::sqr<Fp>(zi2, zi);
+  mp::mul<Fp>(zi3, zi2, zi);
+  mp::mul<Fp>(x, P.X, zi2);
+  mp::mul<Fp>(y, P.Y, zi3);
+  mp::canon<Fp>(x); mp::canon<Fp>(y);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { out[j] = x[j]; out[L + j] = y[j]; }
+}
+
+// window base 2^(W w) * B (= entry d = 1 of window w), affine Montgomery form
+template <class CV, int W>
+__device__ void window_base(uint32_t* out, const uint32_t* bx, const uint32_t* by, int w) {
+  using Fp = typename CV::Fp;
+  JPt<Fp> P;
+  affine_point<CV>(P, bx, by);
+  for (int i = 0; i < W * w; ++i) jdbl<CV>(P, P);
+  store_affine<CV>(out, P);
+}
+
+// entry d * base (d < 2^W), affine Montgomery form
+template <class CV, int W>
+__device__ void table_entry(uint32_t* out, const uint32_t* base, int d) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  JPt<Fp> P, acc;
+  affine_point<CV>(P, base, base + L);
+  acc.inf = true;
+  for (int bit = W - 1; bit >= 0; --bit) {
+    jdbl<CV>(acc, acc);
+    if ((d >> bit) & 1) jadd<CV>(acc, acc, P);
+  }
+  store_affine<CV>(out, acc);
+}
+
+// Tables are built in two launches: thread per (key, window) for the window
+// bases (entry 1), then thread per (key, entry >= 2) from its window's base.
+template <class CV>
+__global__ void k_ec_table_base_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  constexpr int W = CV::WQ, NWIN = ec_windows_w(CV::CLS, CV::WQ);
+  constexpr int NE = 1 << (CV::WQ - 1), STRIDE = ec_stride(CV::CLS);
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (k >= n || w >= NWIN) return;
+  const DevKey& K = keys[idx[k]];
+  if (!K.valid) return;
+  const uint32_t* aux = blob + K.aux_off;
+  window_base<CV, W>(blob + K.tab_off + (int64_t)w * NE * STRIDE, aux, aux + CV::Fp::L, w);
+}
+
+template <class CV>
+__global__ void k_ec_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+  constexpr int W = CV::WQ, NWIN = ec_windows_w(CV::CLS, CV::WQ);
+  constexpr int NE = 1 << (CV::WQ - 1), STRIDE = ec_stride(CV::CLS);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (k >= n || e >= NWIN * NE || e % NE == 0) return;
+  const DevKey& K = keys[idx[k]];
+  if (!K.valid) return;
+  uint32_t* tab = blob + K.tab_off;
+  table_entry<CV, W>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
+}
+
+template <class CV>
+__global__ void k_ec_table_base_g(uint32_t* tab) {
+  constexpr int W = ec_comb_w(CV::CLS, true), NWIN = ec_windows(CV::CLS, true);
+  constexpr int NE = ec_entries(CV::CLS, true), STRIDE = ec_stride(CV::CLS);
+  using Fp = typename CV::Fp;
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= NWIN) return;
+  uint32_t gx[Fp::L], gy[Fp::L];
+  mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
+  window_base<CV, W>(tab + (int64_t)w * NE * STRIDE, gx, gy, w);
+}
+
+template <class CV>
+__global__ void k_ec_table_g(uint32_t* tab) {
+  constexpr int W = ec_comb_w(CV::CLS, true), NWIN = ec_windows(CV::CLS, true);
+  constexpr int NE = ec_entries(CV::CLS, true), STRIDE = ec_stride(CV::CLS);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= NWIN * NE || e % NE == 0) return;
+  table_entry<CV, W>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
+}
+
+template <class CV>
+void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
+  const int64_t waves = (a.end - a.begin) / WAVE;
+  dim3 g((unsigned)waves), b(WAVE);
+  (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
+  // tokens per thread for the batched inversion: keep >= ~8 waves per CU
+  const int64_t n = a.end - a.begin;
+  int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * 8 * WAVE)));
+  const int64_t S = (n + B - 1) / B;
+  hipLaunchKernelGGL(k_ec_scalar_batch<CV>, dim3((unsigned)((S + WAVE - 1) / WAVE)), b, 0, s, a, B);
+  mk("scalar");
+  hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
+  mk("point");
+  hipLaunchKernelGGL(k_ec_exact<CV>, dim3(64), b, 0, s, a);
+  mk("exact");
+}
+
+template <class CV>
+void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx, int tn,
+                   hipStream_t s) {
+  constexpr int NWIN = ec_windows_w(CV::CLS, CV::WQ), NE = 1 << (CV::WQ - 1);
+  dim3 b(64);
+  if (n > 0) hipLaunchKernelGGL(k_ec_keyprep<CV>, dim3((n + 63) / 64), b, 0, s, keys, blob, idx, n);
+  if (tn <= 0) return;
+  hipLaunchKernelGGL(k_ec_table_base_keys<CV>, dim3((NWIN + 63) / 64, tn), b, 0, s, keys, blob, tidx, tn);
+  hipLaunchKernelGGL(k_ec_table_keys<CV>, dim3((NWIN * NE + 63) / 64, tn), b, 0, s, keys, blob, tidx, tn);
+}
+
+template <class CV>
+void gtable_chain(uint32_t* tab, hipStream_t s) {
+  constexpr int NWIN = ec_windows(CV::CLS, true), NE = ec_entries(CV::CLS, true);
+  hipLaunchKernelGGL(k_ec_table_base_g<CV>, dim3((NWIN + 63) / 64), dim3(64), 0, s, tab);
+  hipLaunchKernelGGL(k_ec_table_g<CV>, dim3((NWIN * NE + 63) / 64), dim3(64), 0, s, tab);
+}
+
+}  // namespace
+

@@ -7,7 +7,7 @@
 #include <cstdint>
 
 #include "../kernels/mp.hpp"
-#include "../kernels/ecdsa.hip"   // EC device functions (anonymous namespace) for point-level tests
+#include "../kernels/ecdsa_impl.hpp"   // EC device functions (anonymous namespace) for point-level tests
 
 #include <type_traits>
 
