@@ -98,14 +98,16 @@ def p384_point_mads_per_token(wq=20):
     return ec_point_mads_per_token(15, 4, 5, 20, wq, 384, 15 * 12, merged=False)
 
 
-def ed25519_point_mads_per_token():
-    """k_ed_point: 13 + 16 comb windows (B W = 20, key W = 16), each a Niels
-    addition of 7 field products (ed25519.hip add_niels); p = 2^255 - 19 is
-    reduced with 2 MADs per row (mp.hpp mont_reduce_25519): a product is
-    L^2 + 2L = 120 MADs.  Plus k = H mod L (one reduction + one product mod L)."""
+def ed25519_point_mads_per_token(wa=20):
+    """k_ed_point: 13 comb windows of the base point (W = 20) + ceil(254 / wa)
+    of the key (ed25519.hpp ed_key_w: W = 20 / 18 / 16 by the table budget, 20
+    for config 3's single key), each a Niels addition of 7 field products
+    (ed25519.hip add_niels); p = 2^255 - 19 is reduced with 2 MADs per row
+    (mp.hpp mont_reduce_25519): a product is L^2 + 2L = 120 MADs.  Plus
+    k = H mod L (one reduction + one product mod L)."""
     L = 10
     mul = L * L + 2 * L
-    adds = 13 * (1 - 2.0 ** -20) + 16 * (1 - 2.0 ** -16)
+    adds = 13 * (1 - 2.0 ** -20) + -(-254 // wa) * (1 - 2.0 ** -wa)
     return adds * 7 * mul + 220
 
 

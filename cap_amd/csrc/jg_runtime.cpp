@@ -331,6 +331,7 @@ struct Item {                     // one device's share of a submission
 struct Device {
   int id = 0;
   int ec_wq[NCLS] = {};           // comb width of the loaded EC key tables per curve
+  int ed_wa = 16;                 // comb width of the loaded Ed25519 key tables
   Lane lane0;                     // resident batches, key loads, hashing
   uint32_t* gtab[NCLS] = {};
   uint32_t* btab = nullptr;
@@ -801,6 +802,7 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks, bool 
       ea.xyz = rows;
       ea.btab = d->btab;
       ea.npad = np; ea.begin = r.begin; ea.end = r.end;
+      ea.wa = d->ed_wa;
       launch_ed(ea, s, marker(marks, c));
     }
     if (conc) {
@@ -1083,6 +1085,7 @@ void wait_idle(Device* d) {
 // ---------------------------------------------------------------- keys
 struct StagedKeys {
   int ec_wq[NCLS] = {};             // comb width of this load's EC key tables per curve (ecdsa.hpp ec_key_w)
+  int ed_wa = 16;                  // comb width of this load's Ed25519 key tables (ed25519.hpp ed_key_w)
   std::vector<DevKey> dk;
   std::vector<uint32_t> blob;      // host-initialised part of the device key blob
   uint64_t tab_words = 0;          // device-only tail: comb tables (built on the GPU)
@@ -1121,6 +1124,9 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
   S.ec_wq[CLS_P256] = ec_key_w(CLS_P256, nec[JG_P256], table_budget);
   S.ec_wq[CLS_P384] = ec_key_w(CLS_P384, nec[JG_P384], table_budget);
   S.ec_wq[CLS_P521] = ec_key_w(CLS_P521, nec[JG_P521], table_budget);
+  int ned = 0;
+  for (int i = 0; i < nkeys; ++i) ned += keys[i].kind == JG_KEY_ED25519;
+  S.ed_wa = ed_key_w(ned, table_budget);
   for (int i = 0; i < nkeys; ++i) {
     const jg_key& k = keys[i];
     HostKey& hk = hks[i];
@@ -1185,7 +1191,7 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
       K.cls = CLS_ED25519;
       K.kbytes = 32;
       K.aux_off = blob_alloc(S.blob, 8 + 2 * ED_L);
-      K.tab_off = tab_alloc(S, i, (uint64_t)ed_table_words(false));
+      K.tab_off = tab_alloc(S, i, (uint64_t)ed_table_words_w(S.ed_wa));
       // crypto/ed25519.Verify panics on len(pub) != 32; go-jose never hands it one
       const bool ok = k.x && k.coord_len == 32;
       if (ok) {
@@ -1207,7 +1213,7 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
                                std::to_string(ec_table_words_w(c, S.ec_wq[c]) * 4 >> 20) + " MiB each)");
   if ((int)S.ed_idx.size() > ED_MAX_KEYS)
     throw std::runtime_error("Ed25519: at most " + std::to_string(ED_MAX_KEYS) + " keys per table (comb tables are " +
-                             std::to_string(ed_table_words(false) * 4 >> 20) + " MiB each)");
+                             std::to_string(ed_table_words_w(S.ed_wa) * 4 >> 20) + " MiB each)");
   blob_alloc(S.blob, 0);                                      // align the host part
   for (int k : S.tab_keys) S.dk[k].tab_off += S.blob.size();
 }
@@ -1251,6 +1257,7 @@ void ensure_tables(Device* d, const StagedKeys& S) {
 void load_keys_device(Device* d, const StagedKeys& S) {
   HIPCHK(hipSetDevice(d->id));
   for (int c = 0; c < NCLS; ++c) d->ec_wq[c] = S.ec_wq[c];
+  d->ed_wa = S.ed_wa;
   hipStream_t s = d->lane0.stream;
   d->lane0.sync();
   if (d->copy) (void)hipStreamSynchronize(d->copy);
@@ -1288,7 +1295,7 @@ void load_keys_device(Device* d, const StagedKeys& S) {
     std::vector<int32_t> build_ec[NCLS], build_ed;
     for (int c = CLS_P256; c <= CLS_P521; ++c)
       split(S.ec_idx[c], (uint64_t)ec_table_words_w(c, S.ec_wq[c]), build_ec[c]);
-    split(S.ed_idx, (uint64_t)ed_table_words(false), build_ed);
+    split(S.ed_idx, (uint64_t)ed_table_words_w(S.ed_wa), build_ed);
     // one index array: rsa | p256 | p384 | p521 | ed | builds p256 | p384 | p521 | ed
     std::vector<int32_t> idx;
     std::vector<size_t> at;
@@ -1305,7 +1312,7 @@ void load_keys_device(Device* d, const StagedKeys& S) {
     for (int c = CLS_P256; c <= CLS_P521; ++c)
       launch_ec_keyprep(c, S.ec_wq[c], d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(),
                         d->didx + at[5 + c - CLS_P256], (int)build_ec[c].size(), s);
-    launch_ed_keyprep(d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), d->didx + at[8],
+    launch_ed_keyprep(S.ed_wa, d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), d->didx + at[8],
                       (int)build_ed.size(), s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));

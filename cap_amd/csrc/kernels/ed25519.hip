@@ -63,20 +63,27 @@ __device__ void add_full(EPt& R, const EPt& P, const EPt& Q) {
   mp::mul<Fp>(R.X, E, F); mp::mul<Fp>(R.Y, G, H); mp::mul<Fp>(R.T, E, H); mp::mul<Fp>(R.Z, F, G);
 }
 
-template <bool BASE>
+template <int NE>
 __device__ __forceinline__ void add_window(EPt& P, const uint32_t* __restrict__ tab, int w, int d) {
   if (d == 0) return;
   const int ad = d < 0 ? -d : d;
-  const uint32_t* ent = tab + ((int64_t)w * ed_entries(BASE) + (ad - 1)) * ED_STRIDE;
+  const uint32_t* ent = tab + ((int64_t)w * NE + (ad - 1)) * ED_STRIDE;
   uint32_t ypx[L], ymx[L], t2d[L];
 #pragma unroll
   for (int j = 0; j < L; ++j) { ypx[j] = ent[j]; ymx[j] = ent[L + j]; t2d[j] = ent[2 * L + j]; }
-  if (d < 0) {                                // -(x, y) = (-x, y): swap y+x / y-x, negate 2dxy
-    mp::neg<Fp>(t2d, t2d);
-    add_niels(P, ymx, ypx, t2d);
-  } else {
-    add_niels(P, ypx, ymx, t2d);
+  // -(x, y) = (-x, y): swap y+x / y-x and negate 2dxy -- selected per lane, so
+  // the wave runs ONE addition (a branch on the digit's sign made lanes of
+  // both signs execute both inlined copies of add_niels)
+  const bool neg = d < 0;
+  uint32_t a1[L], a2[L], nt[L];
+  mp::neg<Fp>(nt, t2d);
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    a1[j] = neg ? ymx[j] : ypx[j];
+    a2[j] = neg ? ypx[j] : ymx[j];
+    t2d[j] = neg ? nt[j] : t2d[j];
   }
+  add_niels(P, a1, a2, t2d);
 }
 
 // signed W-bit digits d_w in [-2^(W-1), 2^(W-1)], s = sum d_w 2^(W w)
@@ -95,6 +102,7 @@ __device__ __forceinline__ void recode(int* dg, const uint32_t* s) {
   }
 }
 
+template <int WA>
 __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
@@ -131,10 +139,10 @@ __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
     mp::mul<Fl>(k, kr, rr);                 // H mod L (< 2L)
     mp::csub<Fl>(k);
   }
-  constexpr int NB = ed_windows(true), NA = ed_windows(false), NW = NB > NA ? NB : NA;
+  constexpr int NB = ed_windows(true), NA = ed_windows_w(WA), NW = NB > NA ? NB : NA;
   int d1[NB], d2[NA];
   recode<ed_comb_w(true), NB>(d1, s);
-  recode<ed_comb_w(false), NA>(d2, k);
+  recode<WA, NA>(d2, k);
   EPt P;
 #pragma unroll
   for (int j = 0; j < L; ++j) { P.X[j] = 0; P.T[j] = 0; P.Y[j] = Fp::ONE[j]; P.Z[j] = Fp::ONE[j]; }
@@ -146,8 +154,8 @@ __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
     for (int i = 0; i < NB; ++i) if (i == w) e1 = d1[i];
 #pragma unroll
     for (int i = 0; i < NA; ++i) if (i == w) e2 = d2[i];
-    add_window<true>(P, a.btab, w, e1);
-    add_window<false>(P, atab, w, e2);
+    add_window<ed_entries(true)>(P, a.btab, w, e1);
+    add_window<(1 << (WA - 1))>(P, atab, w, e2);
   }
 #pragma unroll
   for (int j = 0; j < L; ++j) {
@@ -356,8 +364,9 @@ __global__ void k_ed_decode(DevKey* keys, uint32_t* blob, const int32_t* idx, in
   K.valid = (K.valid && ok) ? 1 : 0;
 }
 
+template <int W>
 __global__ void k_ed_table_base_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
-  constexpr int W = ed_comb_w(false), NWIN = ed_windows(false), NE = ed_entries(false);
+  constexpr int NWIN = ed_windows_w(W), NE = 1 << (W - 1);
   const int w = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (k >= n || w >= NWIN) return;
@@ -367,8 +376,9 @@ __global__ void k_ed_table_base_keys(const DevKey* keys, uint32_t* blob, const i
   window_base(blob + K.tab_off + (int64_t)w * NE * ED_STRIDE, aux, aux + L, W * w);
 }
 
+template <int W>
 __global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
-  constexpr int W = ed_comb_w(false), NWIN = ed_windows(false), NE = ed_entries(false);
+  constexpr int NWIN = ed_windows_w(W), NE = 1 << (W - 1);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (k >= n || e >= NWIN * NE || e % NE == 0) return;
@@ -384,7 +394,9 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   if (waves <= 0) return;
   dim3 g((unsigned)waves), b(WAVE);
-  hipLaunchKernelGGL(k_ed_point, g, b, 0, s, a);
+  if (a.wa == 20) hipLaunchKernelGGL(k_ed_point<20>, g, b, 0, s, a);
+  else if (a.wa == 18) hipLaunchKernelGGL(k_ed_point<18>, g, b, 0, s, a);
+  else hipLaunchKernelGGL(k_ed_point<16>, g, b, 0, s, a);
   mk("point");
   // tokens per thread for the batched inversion: keep >= ~8 waves per CU
   const int64_t n = a.end - a.begin;
@@ -394,14 +406,23 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   mk("finish");
 }
 
-void launch_ed_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx, int tn,
+namespace {
+template <int W>
+void ed_tables(DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
+  constexpr int NWIN = ed_windows_w(W), NE = 1 << (W - 1);
+  hipLaunchKernelGGL(k_ed_table_base_keys<W>, dim3((NWIN + 63) / 64, tn), dim3(64), 0, s, keys, blob, tidx, tn);
+  hipLaunchKernelGGL(k_ed_table_keys<W>, dim3((NWIN * NE + 63) / 64, tn), dim3(64), 0, s, keys, blob, tidx, tn);
+}
+}  // namespace
+
+void launch_ed_keyprep(int wa, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx, int tn,
                        hipStream_t s) {
   if (n <= 0) return;
-  constexpr int NWIN = ed_windows(false), NE = ed_entries(false);
   hipLaunchKernelGGL(k_ed_decode, dim3((n + 63) / 64), dim3(64), 0, s, keys, blob, idx, n);
   if (tn <= 0) return;
-  hipLaunchKernelGGL(k_ed_table_base_keys, dim3((NWIN + 63) / 64, tn), dim3(64), 0, s, keys, blob, tidx, tn);
-  hipLaunchKernelGGL(k_ed_table_keys, dim3((NWIN * NE + 63) / 64, tn), dim3(64), 0, s, keys, blob, tidx, tn);
+  if (wa == 20) ed_tables<20>(keys, blob, tidx, tn, s);
+  else if (wa == 18) ed_tables<18>(keys, blob, tidx, tn, s);
+  else ed_tables<16>(keys, blob, tidx, tn, s);
 }
 
 void launch_ed_btable(uint32_t* tab, hipStream_t s) {
