@@ -91,6 +91,34 @@ void parallel_for(size_t n, int threads, F&& fn) {
   for (auto& t : th) t.join();
 }
 
+// A fixed cut of [0, n) into per-thread ranges, so that several passes over a
+// batch (count, prefix, fill) see the same ranges and keep running offsets per
+// range instead of one serial prefix sum over every token.
+struct Chunks {
+  std::vector<size_t> b;        // range c = [b[c], b[c+1])
+  size_t count() const { return b.size() - 1; }
+};
+Chunks make_chunks(size_t n, int threads) {
+  const size_t min_chunk = 512;
+  const size_t nt = std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, threads), (n + min_chunk - 1) / min_chunk));
+  Chunks c;
+  c.b.resize(nt + 1);
+  for (size_t t = 0; t <= nt; ++t) c.b[t] = n * t / nt;
+  return c;
+}
+template <class F>
+void run_chunks(const Chunks& c, F&& fn) {
+  // fn(chunk, begin, end)
+  if (c.count() == 1) {
+    fn((size_t)0, c.b[0], c.b[1]);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(c.count());
+  for (size_t t = 0; t < c.count(); ++t) th.emplace_back([&fn, &c, t] { fn(t, c.b[t], c.b[t + 1]); });
+  for (auto& t : th) t.join();
+}
+
 int64_t wall_now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
       .count();
@@ -188,18 +216,54 @@ struct ParArray {
   size_t size() const { return n; }
 };
 
+// Decoded payloads of one parse range, in a few large blocks (one free per
+// block instead of one per token)
+struct ByteArena {
+  std::vector<std::unique_ptr<char[]>> blocks;
+  char* cur = nullptr;
+  size_t left = 0;
+  char* alloc(size_t n) {
+    if (n > left) {
+      const size_t sz = std::max<size_t>(n, (size_t)1 << 20);
+      blocks.emplace_back(new char[sz]);
+      cur = blocks.back().get();
+      left = sz;
+    }
+    char* r = cur;
+    cur += n;
+    left -= n;
+    return r;
+  }
+  void give_back(size_t n) {     // the unused tail of the last alloc
+    cur -= n;
+    left += n;
+  }
+};
+
+struct GeneralParse {            // storage of a token that took jose.ParseSigned's general path
+  std::string alg, kid, payload;
+};
+
 struct Tok {
-  TokenInfo info;
-  std::string payload;
-  std::string kid;
-  int alg = 0;
+  // ParseSigned outcome (validateSigningAlgorithm's inputs)
+  bool parsed = false;
   bool verifiable = false;     // DetachedVerify gets as far as verifyPayload
+  int alg = 0;
+  uint32_t nsigs = 0;
+  size_t sig0_len = 0;
+  std::string parse_err;
+  std::string_view alg_name, kid, payload;     // into hdr / gen / the batch's ByteArena
+  std::shared_ptr<const HdrInfo> hdr;           // compact path: the shared header decode
+  std::unique_ptr<GeneralParse> gen;
   // arena entry: literal token span, or owned bytes
   const char* lit = nullptr;
   size_t lit_len = 0;
   std::string owned;
   uint32_t si_len = 0, sig_b64_len = 0;
-  uint64_t arena_off = 0;
+  uint32_t ncand = 0;          // candidate keys (jobs) in the current GPU batch
+  uint64_t job0 = 0;           // first job of this token in that batch
+  size_t entry_len() const { return lit ? lit_len : owned.size(); }
+  TokenView view() const { return TokenView{parsed, parse_err, nsigs, sig0_len, alg_name}; }
 };
 
 template <class T>
@@ -224,22 +288,37 @@ void ParArray<T>::release() {
   n = 0;
 }
 
-void parse_one(std::string_view token, HdrCache& cache, Tok* t) {
+void parse_one(std::string_view token, HdrCache& cache, ByteArena& pay, Tok* t) {
   // compact fast path: no whitespace / non-ASCII, exactly three segments
   if (!token.empty() && token[0] != '{' && !has_go_space_or_nonascii(token)) {
     const size_t d1 = token.find('.');
     const size_t d2 = d1 == std::string_view::npos ? d1 : token.find('.', d1 + 1);
     if (d1 == std::string_view::npos || d2 == std::string_view::npos ||
         token.find('.', d2 + 1) != std::string_view::npos) {
-      t->info.parse_err = "square/go-jose: compact JWS format must have three parts";
+      t->parse_err = "square/go-jose: compact JWS format must have three parts";
       return;
     }
     const std::string_view hs = token.substr(0, d1), ps = token.substr(d1 + 1, d2 - d1 - 1),
                            ss = token.substr(d2 + 1);
     const std::shared_ptr<const HdrInfo>& h = cache.get(hs);
     // parseSignedCompact order: protected, payload, signature decodes, then sanitize
-    if (!h->b64_ok) { t->info.parse_err = h->b64_err; return; }
-    if (!b64url_decode(ps, &t->payload, &t->info.parse_err)) return;
+    if (!h->b64_ok) { t->parse_err = h->b64_err; return; }
+    bool pay_canon = false;
+    {
+      const size_t cap = ps.size() / 4 * 3 + 2;
+      char* dst = pay.alloc(cap);
+      const long len = b64url_decode_fast(ps, dst, &pay_canon);
+      if (len >= 0) {
+        pay.give_back(cap - (size_t)len);
+        t->payload = std::string_view(dst, (size_t)len);
+      } else {                 // '=', CR/LF or an illegal byte: Go's skipping and error text
+        pay.give_back(cap);
+        t->gen = std::make_unique<GeneralParse>();
+        if (!b64url_decode(ps, &t->gen->payload, &t->parse_err)) return;
+        t->payload = t->gen->payload;
+        pay_canon = false;
+      }
+    }
     // the signature bytes themselves are only needed when the segment is not
     // canonical (the device decodes canonical base64url itself)
     const bool sig_canon = b64url_canonical(ss);
@@ -248,19 +327,20 @@ void parse_one(std::string_view token, HdrCache& cache, Tok* t) {
     if (sig_canon) {
       siglen = b64_decoded_len(ss.size());
     } else {
-      if (!b64url_decode(ss, &sig, &t->info.parse_err)) return;
+      if (!b64url_decode(ss, &sig, &t->parse_err)) return;
       siglen = sig.size();
     }
-    if (!h->ok) { t->info.parse_err = h->err; return; }
-    t->info.parsed = true;
-    t->info.nsigs = 1;
-    t->info.sig0_len = siglen;
-    t->info.alg = h->sig.alg;
+    if (!h->ok) { t->parse_err = h->err; return; }
+    t->parsed = true;
+    t->nsigs = 1;
+    t->sig0_len = siglen;
+    t->hdr = h;
+    t->alg_name = h->sig.alg;
     t->kid = h->sig.kid;
     t->alg = h->alg;
     t->verifiable = h->verifiable && t->alg != 0;
     if (!t->verifiable) return;
-    if (h->seg_canonical && h->needs_b64 && b64url_canonical(ps) && sig_canon) {
+    if (h->seg_canonical && h->needs_b64 && pay_canon && sig_canon) {
       t->lit = token.data();
       t->lit_len = token.size();
       t->si_len = (uint32_t)d2;
@@ -268,7 +348,7 @@ void parse_one(std::string_view token, HdrCache& cache, Tok* t) {
       return;
     }
     JWS j;
-    j.payload = t->payload;
+    j.payload = std::string(t->payload);
     j.sigs.push_back(h->sig);
     std::string si;
     signing_input(j, &si);
@@ -282,13 +362,17 @@ void parse_one(std::string_view token, HdrCache& cache, Tok* t) {
   }
   // general path: jose.ParseSigned
   JWS j;
-  if (!parse_signed(token, &j, &t->info.parse_err)) return;
-  t->info.parsed = true;
-  t->info.nsigs = j.sigs.size();
-  t->info.sig0_len = j.sigs.empty() ? 0 : j.sigs[0].signature.size();
-  t->info.alg = j.sigs.empty() ? "" : j.sigs[0].alg;
-  t->kid = j.sigs.empty() ? "" : j.sigs[0].kid;      // go-oidc: the first signature's kid
-  t->payload = j.payload;
+  if (!parse_signed(token, &j, &t->parse_err)) return;
+  t->parsed = true;
+  t->nsigs = (uint32_t)j.sigs.size();
+  t->sig0_len = j.sigs.empty() ? 0 : j.sigs[0].signature.size();
+  t->gen = std::make_unique<GeneralParse>();
+  t->gen->alg = j.sigs.empty() ? "" : j.sigs[0].alg;
+  t->gen->kid = j.sigs.empty() ? "" : j.sigs[0].kid;      // go-oidc: the first signature's kid
+  t->gen->payload = j.payload;
+  t->alg_name = t->gen->alg;
+  t->kid = t->gen->kid;
+  t->payload = t->gen->payload;
   std::string si;
   if (!signing_input(j, &si)) return;
   t->alg = alg_id(j.sigs[0].alg);
@@ -303,7 +387,7 @@ void parse_one(std::string_view token, HdrCache& cache, Tok* t) {
 }
 
 // json.Unmarshal(payload, &map[string]interface{})  [R33, R35, R40]
-bool claims_map(const std::string& payload, json::Value* out, std::string* err) {
+bool claims_map(std::string_view payload, json::Value* out, std::string* err) {
   if (!json::parse(payload, out, err)) return false;
   if (out->is_null()) return true;
   if (out->kind != json::Value::Object) {
@@ -358,7 +442,8 @@ int key_family(const PublicKey& k) {
 // pushes the key indices to try for token t.
 struct Verified {
   ParArray<Tok> toks;
-  std::vector<uint8_t> any;      // some candidate key verified
+  std::vector<ByteArena> payloads;   // one per parse range
+  std::vector<uint8_t> any;          // some candidate key verified
 };
 
 template <class Cand>
@@ -367,69 +452,82 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
   const size_t n = subset ? subset->size() : tokens.size();
   auto tok_index = [&](size_t i) { return subset ? (*subset)[i] : i; };
   PhaseTimer pt("verify");
+  const Chunks ch = make_chunks(n, eng.threads());
   if (!subset) {
     V->toks.init(tokens.size(), eng.threads());
-    parallel_for(n, eng.threads(), [&](size_t lo, size_t hi) {
+    V->any.assign(tokens.size(), 0);
+    V->payloads.resize(ch.count());
+    run_chunks(ch, [&](size_t c, size_t lo, size_t hi) {
       HdrCache cache;
-      for (size_t i = lo; i < hi; ++i) parse_one(tokens[i], cache, &V->toks[i]);
+      for (size_t i = lo; i < hi; ++i) parse_one(tokens[i], cache, V->payloads[c], &V->toks[i]);
     });
     pt.lap("parse");
   }
-  V->any.resize(tokens.size(), 0);
-  // pass 1: candidate keys per token (counted), arena entry sizes
-  std::vector<uint64_t> off(n + 1, 0);
-  std::vector<uint32_t> njob(n + 1, 0);
-  parallel_for(n, eng.threads(), [&](size_t lo, size_t hi) {
+  // pass 1: candidate keys per token, arena bytes and jobs per range
+  std::vector<uint64_t> rbytes(ch.count() + 1, 0), rjobs(ch.count() + 1, 0);
+  run_chunks(ch, [&](size_t c, size_t lo, size_t hi) {
     std::vector<uint16_t> ks;
+    uint64_t bytes = 0, jobs = 0;
     for (size_t i = lo; i < hi; ++i) {
-      const Tok& t = V->toks[tok_index(i)];
+      Tok& t = V->toks[tok_index(i)];
       ks.clear();
       if (t.verifiable) cand(t, ks);
-      njob[i + 1] = (uint32_t)ks.size();
-      off[i + 1] = ks.empty() ? 0 : (t.lit ? t.lit_len : t.owned.size());
+      t.ncand = (uint32_t)ks.size();
+      if (t.ncand) bytes += t.entry_len();
+      jobs += t.ncand;
     }
+    rbytes[c + 1] = bytes;
+    rjobs[c + 1] = jobs;
   });
-  for (size_t i = 0; i < n; ++i) {                  // prefix sums (arena layout, job slots)
-    off[i + 1] += off[i];
-    njob[i + 1] += njob[i];
+  for (size_t c = 0; c < ch.count(); ++c) {
+    rbytes[c + 1] += rbytes[c];
+    rjobs[c + 1] += rjobs[c];
   }
-  const size_t total_jobs = njob[n];
+  const size_t total_jobs = rjobs[ch.count()];
   pt.lap("plan");
   if (total_jobs == 0) return;
-  const uint64_t arena_len = off[n];
+  const uint64_t arena_len = rbytes[ch.count()];
   uint8_t* arena = eng.arena_buffer(arena_len);
-  std::vector<jg_tok> jobs(total_jobs);
-  std::vector<uint32_t> job_tok(total_jobs);
-  // pass 2: pack the arena and the jobs
-  parallel_for(n, eng.threads(), [&](size_t lo, size_t hi) {
+  std::unique_ptr<jg_tok[]> jobs(new jg_tok[total_jobs]);      // filled below, not zeroed first
+  std::unique_ptr<uint8_t[]> verdict(new uint8_t[total_jobs]);
+  // pass 2: pack the arena and the jobs, each range from its own offsets
+  run_chunks(ch, [&](size_t c, size_t lo, size_t hi) {
     std::vector<uint16_t> ks;
+    uint64_t off = rbytes[c], jn = rjobs[c];
     for (size_t i = lo; i < hi; ++i) {
-      if (njob[i + 1] == njob[i]) continue;
       Tok& t = V->toks[tok_index(i)];
-      t.arena_off = off[i];
-      if (t.lit) std::memcpy(arena + off[i], t.lit, t.lit_len);
-      else std::memcpy(arena + off[i], t.owned.data(), t.owned.size());
+      if (!t.ncand) continue;
+      const size_t len = t.entry_len();
+      std::memcpy(arena + off, t.lit ? t.lit : t.owned.data(), len);
       ks.clear();
       cand(t, ks);
+      t.job0 = jn;
       for (size_t k = 0; k < ks.size(); ++k) {
-        jg_tok& j = jobs[njob[i] + k];
-        j.off = off[i];
+        jg_tok& j = jobs[jn + k];
+        j.off = off;
         j.sig_in_len = t.si_len;
         j.sig_rel_off = t.si_len + 1;
         j.sig_b64_len = t.sig_b64_len;
         j.key_idx = ks[k];
         j.alg = (uint8_t)t.alg;
         j.flags = 0;
-        job_tok[njob[i] + k] = (uint32_t)tok_index(i);
       }
+      off += len;
+      jn += ks.size();
     }
   });
   pt.lap("pack");
-  std::vector<uint8_t> verdict(total_jobs, 0);
-  eng.verify(arena, arena_len, jobs.data(), total_jobs, verdict.data());
+  eng.verify(arena, arena_len, jobs.get(), total_jobs, verdict.get());
   pt.lap("gpu");
-  for (size_t j = 0; j < total_jobs; ++j)
-    if (verdict[j] == JG_ACCEPT) V->any[job_tok[j]] = 1;
+  run_chunks(ch, [&](size_t, size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      const size_t ti = tok_index(i);
+      const Tok& t = V->toks[ti];
+      for (uint32_t k = 0; k < t.ncand; ++k)
+        if (verdict[t.job0 + k] == JG_ACCEPT) V->any[ti] = 1;
+    }
+  });
+  pt.lap("verdicts");
 }
 
 // ---------------------------------------------------------------- static key set
@@ -439,7 +537,7 @@ class StaticKeySet final : public KeySet {
     eng_.load(keys_);
     for (const auto& k : keys_) fam_.push_back(key_family(k));
   }
-  std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, std::vector<TokenInfo>* info) override {
+  std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
     std::lock_guard<std::mutex> g(mu_);
     Verified V;
     gpu_verify(eng_, tokens, &V, [&](const Tok& t, std::vector<uint16_t>& out) {
@@ -455,25 +553,25 @@ class StaticKeySet final : public KeySet {
       for (size_t i = lo; i < hi; ++i) {
         const Tok& t = V.toks[i];
         Result& r = res[i];
-        if (!t.info.parsed) { r.err = t.info.parse_err; continue; }     // jwt.ParseSigned error
-        std::string jerr;
-        // parsedJWT.Claims(key, &allClaims): verify, then unmarshal; a JSON
-        // error moves on to the next key, so it ends as "no known key"
-        if (V.any[i] && claims_map(t.payload, &r.claims, &jerr)) {
-          r.ok = true;
+        if (!t.parsed) {
+          r.err = t.parse_err;                                           // jwt.ParseSigned error
         } else {
-          r.claims = json::Value();
-          r.err = "no known key successfully validated the token signature";
+          std::string jerr;
+          // parsedJWT.Claims(key, &allClaims): verify, then unmarshal; a JSON
+          // error moves on to the next key, so it ends as "no known key"
+          if (V.any[i] && claims_map(t.payload, &r.claims, &jerr)) {
+            r.ok = true;
+          } else {
+            r.claims = json::Value();
+            r.err = "no known key successfully validated the token signature";
+          }
         }
+        if (post) (*post)(r, t.view());
       }
     });
     pt.lap("payload-json");
-    if (info) {
-      info->resize(tokens.size());
-      parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; ++i) (*info)[i] = std::move(V.toks[i].info);
-      });
-    }
+    V.toks.release();
+    pt.lap("free-toks");
     return res;
   }
 
@@ -512,7 +610,7 @@ class JSONWebKeySet final : public KeySet {
   JSONWebKeySet(std::string url, std::string ca, Fetcher f, const std::vector<int>& devices)
       : url_(std::move(url)), ca_(std::move(ca)), fetch_(std::move(f)), eng_(devices) {}
 
-  std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, std::vector<TokenInfo>* info) override {
+  std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
     std::lock_guard<std::mutex> g(mu_);
     Verified V;
     std::string miss_err;
@@ -523,21 +621,19 @@ class JSONWebKeySet final : public KeySet {
       for (size_t i = lo; i < hi; ++i) {
         const Tok& t = V.toks[i];
         Result& r = res[i];
-        if (!t.info.parsed) { r.err = "oidc: malformed jwt: " + t.info.parse_err; continue; }
-        if (!V.any[i]) { r.err = miss_err; continue; }
-        std::string jerr;       // jsonWebKeySet.VerifySignature: json.Unmarshal(payload)
-        if (claims_map(t.payload, &r.claims, &jerr)) r.ok = true;
-        else { r.claims = json::Value(); r.err = jerr; }
+        if (!t.parsed) {
+          r.err = "oidc: malformed jwt: " + t.parse_err;
+        } else if (!V.any[i]) {
+          r.err = miss_err;
+        } else {
+          std::string jerr;       // jsonWebKeySet.VerifySignature: json.Unmarshal(payload)
+          if (claims_map(t.payload, &r.claims, &jerr)) r.ok = true;
+          else { r.claims = json::Value(); r.err = jerr; }
+        }
+        if (post) (*post)(r, t.view());
       }
     });
     pt.lap("payload-json");
-    if (info) {
-      info->resize(tokens.size());
-      parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; ++i) (*info)[i] = std::move(V.toks[i].info);
-      });
-    }
-    pt.lap("info");
     V.toks.release();
     pt.lap("free-toks");
     return res;
@@ -553,9 +649,9 @@ class JSONWebKeySet final : public KeySet {
     parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
         Tok& t = V.toks[i];
-        if (!t.info.parsed) res[i].err = "oidc: malformed jwt: " + t.info.parse_err;
+        if (!t.parsed) res[i].err = "oidc: malformed jwt: " + t.parse_err;
         else if (!V.any[i]) res[i].err = miss_err;
-        else { res[i].ok = true; res[i].payload = std::move(t.payload); }
+        else { res[i].ok = true; res[i].payload = std::string(t.payload); }
       }
     });
     return res;
@@ -581,7 +677,7 @@ class JSONWebKeySet final : public KeySet {
     // expired (now + keysExpiryDelta(30s) after expiry), then retry them
     std::vector<size_t> miss;
     for (size_t i = 0; i < tokens.size(); ++i)
-      if (V->toks[i].info.parsed && !V->any[i]) miss.push_back(i);
+      if (V->toks[i].parsed && !V->any[i]) miss.push_back(i);
     std::string fetch_err;
     bool refreshed = false;
     if (!miss.empty() && (!have_keys_ || wall_now_ns() + 30 * kSecond > expiry_ns_)) {
@@ -836,13 +932,46 @@ std::unique_ptr<Validator> NewValidator(KeySet* ks, std::string* err) {
   return std::make_unique<Validator>(ks);
 }
 
+namespace {
+// The jwt.Claims field a claims-map member lands in under encoding/json's
+// case-insensitive matching (fold_eq).  Every field name is 3 letters: a
+// 3-byte ASCII key is matched by upper-casing it; a key with non-ASCII runes
+// (the 'ſ' and Kelvin-sign foldings) takes fold_eq.
+enum ClaimField { F_NONE, F_ISS, F_SUB, F_JTI, F_AUD, F_EXP, F_NBF, F_IAT };
+ClaimField claim_field(const std::string& key) {
+  static const char* const names[] = {"", "ISS", "SUB", "JTI", "AUD", "EXP", "NBF", "IAT"};
+  const size_t n = key.size();
+  if (n < 3 || n > 9) return F_NONE;         // 3 runes of 1..3 bytes
+  if (n == 3) {
+    char u[3];
+    for (int i = 0; i < 3; ++i) {
+      const unsigned char c = (unsigned char)key[i];
+      if (c >= 0x80) return F_NONE;          // a multi-byte rune cannot fit 3 bytes with 2 more
+      u[i] = (char)(c >= 'a' && c <= 'z' ? c - 32 : c);
+    }
+    for (int f = F_ISS; f <= F_IAT; ++f)
+      if (u[0] == names[f][0] && u[1] == names[f][1] && u[2] == names[f][2]) return (ClaimField)f;
+    return F_NONE;
+  }
+  for (int f = F_ISS; f <= F_IAT; ++f)
+    if (fold_eq(key, names[f])) return (ClaimField)f;
+  return F_NONE;
+}
+}  // namespace
+
 Result validate_claims(const json::Value& all_claims, const TokenInfo& info, const Expected& expected,
+                       int64_t now_unix_ns) {
+  return validate_claims(all_claims, TokenView{info.parsed, info.parse_err, info.nsigs, info.sig0_len, info.alg},
+                         expected, now_unix_ns);
+}
+
+Result validate_claims(const json::Value& all_claims, const TokenView& info, const Expected& expected,
                        int64_t now_unix_ns) {
   Result r;
   // validateSigningAlgorithm (jwt/jwt.go:207-239)  [R36]
   {
     std::string e = SupportedSigningAlgorithm(expected.SigningAlgorithms);
-    if (e.empty() && !info.parsed) e = info.parse_err;
+    if (e.empty() && !info.parsed) e = std::string(info.parse_err);
     if (e.empty() && (info.nsigs == 0 || (info.nsigs == 1 && info.sig0_len == 0))) e = "token must be signed";
     if (e.empty() && info.nsigs > 1) e = "token with multiple signatures not supported";
     if (e.empty()) {
@@ -857,9 +986,10 @@ Result validate_claims(const json::Value& all_claims, const TokenInfo& info, con
     }
   }
   // json.Marshal(allClaims) -> json.Unmarshal(&jwt.Claims{})  [R37]: members in
-  // sorted key order, each assigned to the case-insensitively matching field
-  std::string iss, sub, jti;
-  std::vector<std::string> aud;
+  // sorted key order, each assigned to the case-insensitively matching field.
+  // The fields are views into all_claims (which outlives this call).
+  std::string_view iss, sub, jti;
+  const json::Value* aud = nullptr;            // a String, or an Array of Strings
   bool has_iat = false, has_exp = false, has_nbf = false;
   int64_t iat = 0, exp = 0, nbf = 0;
   if (all_claims.kind == json::Value::Object) {
@@ -876,49 +1006,39 @@ Result validate_claims(const json::Value& all_claims, const TokenInfo& info, con
     for (size_t mk = 0; mk < nm; ++mk) {
       const json::Member* m = ms[mk];
       const json::Value& v = m->second;
-      std::string* sfield = fold_eq(m->first, "ISS") ? &iss : fold_eq(m->first, "SUB") ? &sub
-                            : fold_eq(m->first, "JTI") ? &jti : nullptr;
-      if (sfield) {
+      const ClaimField f = claim_field(m->first);
+      if (f == F_NONE) continue;
+      if (f == F_ISS || f == F_SUB || f == F_JTI) {
         if (v.is_null()) continue;
         if (v.kind != json::Value::String) {
           r.err = "json: cannot unmarshal into Go struct field Claims." + m->first + " of type string";
           return r;
         }
-        *sfield = v.str;
+        (f == F_ISS ? iss : f == F_SUB ? sub : jti) = v.str;
         continue;
       }
-      if (fold_eq(m->first, "AUD")) {
+      if (f == F_AUD) {
         // jwt.Audience.UnmarshalJSON: string or array of strings; null included
-        if (v.kind == json::Value::String) {
-          aud.assign(1, v.str);
-          continue;
-        }
-        bool ok = v.kind == json::Value::Array;
-        std::vector<std::string> a;
-        if (ok)
-          for (const auto& e : v.arr) {
+        bool ok = v.kind == json::Value::String || v.kind == json::Value::Array;
+        if (v.kind == json::Value::Array)
+          for (const auto& e : v.arr)
             if (e.kind != json::Value::String) { ok = false; break; }
-            a.push_back(e.str);
-          }
         if (!ok) {
           r.err = "square/go-jose/jwt: expected string or array value to unmarshal to Audience";
           return r;
         }
-        aud = std::move(a);
+        aud = &v;
         continue;
       }
-      bool* has = fold_eq(m->first, "EXP") ? &has_exp : fold_eq(m->first, "NBF") ? &has_nbf
-                  : fold_eq(m->first, "IAT") ? &has_iat : nullptr;
-      if (has) {
-        int64_t* dst = has == &has_exp ? &exp : has == &has_nbf ? &nbf : &iat;
-        if (v.is_null()) { *has = false; *dst = 0; continue; }       // *NumericDate = nil
-        if (v.kind != json::Value::Number) {
-          r.err = "square/go-jose/jwt: expected number value to unmarshal NumericDate";
-          return r;
-        }
-        *has = true;
-        *dst = go_f64_to_i64(v.num);                                 // NumericDate(f)
+      bool* has = f == F_EXP ? &has_exp : f == F_NBF ? &has_nbf : &has_iat;
+      int64_t* dst = f == F_EXP ? &exp : f == F_NBF ? &nbf : &iat;
+      if (v.is_null()) { *has = false; *dst = 0; continue; }       // *NumericDate = nil
+      if (v.kind != json::Value::Number) {
+        r.err = "square/go-jose/jwt: expected number value to unmarshal NumericDate";
+        return r;
       }
+      *has = true;
+      *dst = go_f64_to_i64(v.num);                                 // NumericDate(f)
     }
   }
   // time defaulting (jwt/jwt.go:117-170)  [R38]
@@ -955,8 +1075,12 @@ Result validate_claims(const json::Value& all_claims, const TokenInfo& info, con
   if (!expected.ID.empty() && expected.ID != jti) { r.err = "invalid ID (jti) claim"; return r; }
   if (!expected.Audiences.empty()) {
     bool found = false;
-    for (const auto& e : expected.Audiences)
-      for (const auto& a : aud) found = found || a == e;
+    for (const auto& e : expected.Audiences) {
+      if (!aud) break;
+      if (aud->kind == json::Value::String) found = found || aud->str == e;
+      else
+        for (const auto& a : aud->arr) found = found || a.str == e;
+    }
     if (!found) {
       r.err = "invalid audience (aud) claim: audience claim does not match any expected audience";
       return r;
@@ -983,31 +1107,20 @@ Result Validator::Validate(std::string_view token, const Expected& expected) {
 }
 
 std::vector<Result> Validator::ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected) {
-  std::vector<TokenInfo> info;
-  std::vector<Result> res = ks_->verify_batch(tokens, &info);
-  PhaseTimer pt("validate");
   const int64_t now = expected.has_now ? expected.now_unix_ns : wall_now_ns();
-  // results are rewritten in place (no second 1M-entry vector to build and
-  // free serially); a claims map that fails validation is destroyed here, by
-  // the host threads
-  parallel_for(tokens.size(), host_threads(), [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) {
-      Result& r = res[i];
-      if (!r.ok) {
-        r.err = "error verifying token signature: " + r.err;
-        continue;
-      }
-      Result v = validate_claims(r.claims, info[i], expected, now);
-      if (v.ok) v.claims = std::move(r.claims);
-      r = std::move(v);
+  // the claim checks run inside the key set's per-token pass, on the host
+  // threads, while each token's claims map is still in cache; a claims map
+  // that fails validation is destroyed there
+  const PostFn post = [&](Result& r, const TokenView& t) {
+    if (!r.ok) {
+      r.err = "error verifying token signature: " + r.err;
+      return;
     }
-  });
-  pt.lap("claims");
-  parallel_for(info.size(), host_threads(), [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) info[i] = TokenInfo();
-  });
-  pt.lap("release");
-  return res;
+    Result v = validate_claims(r.claims, t, expected, now);
+    if (v.ok) v.claims = std::move(r.claims);
+    r = std::move(v);
+  };
+  return ks_->verify_batch(tokens, &post);
 }
 
 // ====================================================================== oidc hash claims

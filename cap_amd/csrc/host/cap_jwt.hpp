@@ -94,6 +94,18 @@ struct TokenInfo {          // what validateSigningAlgorithm needs from ParseSig
   size_t sig0_len = 0;
   std::string alg;
 };
+// The same, as views into a batch's parse records (valid during a PostFn call)
+struct TokenView {
+  bool parsed = false;
+  std::string_view parse_err;
+  size_t nsigs = 0;
+  size_t sig0_len = 0;
+  std::string_view alg;
+};
+// Per-token continuation of a batch verify: called on the host threads, once
+// per token, right after that token's (claims, error) is final -- the
+// Validator's claim checks run there while the claims map is still in cache.
+using PostFn = std::function<void(Result& r, const TokenView& t)>;
 
 class KeySet {
  public:
@@ -101,9 +113,9 @@ class KeySet {
   // jwt/keyset.go:27-32
   Result VerifySignature(std::string_view token);
   std::vector<Result> VerifySignatureBatch(const std::vector<std::string_view>& tokens);
-  // batch verify that also returns what the parse learned (Validator reuses it)
-  virtual std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens,
-                                           std::vector<TokenInfo>* info) = 0;
+  // batch verify; `post` (may be null) continues each token's result with what
+  // the parse learned (Validator::ValidateBatch)
+  virtual std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) = 0;
 };
 
 std::unique_ptr<KeySet> NewStaticKeySet(const std::vector<PublicKey>& keys, std::string* err,
@@ -168,6 +180,8 @@ std::unique_ptr<Validator> NewValidator(KeySet* ks, std::string* err);
 // The claim checks of Validate after the signature (jwt/jwt.go:103-201), on a
 // verified claims map and the token's parse info.  Exposed for tests.
 Result validate_claims(const json::Value& all_claims, const TokenInfo& info, const Expected& expected,
+                       int64_t now_unix_ns);
+Result validate_claims(const json::Value& all_claims, const TokenView& info, const Expected& expected,
                        int64_t now_unix_ns);
 
 bool ParsePublicKeyPEM(std::string_view data, PublicKey* out, std::string* err);

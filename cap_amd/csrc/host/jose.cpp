@@ -95,6 +95,13 @@ bool b64url_decode(std::string_view s, std::string* out, std::string* err) {
   // go-jose base64URLDecode: strings.TrimRight(value, "=")   [R3]
   size_t n = s.size();
   while (n > 0 && s[n - 1] == '=') --n;
+  out->resize(n / 4 * 3 + 2);
+  bool canon;
+  const long len = b64url_decode_fast(s.substr(0, n), out->data(), &canon);
+  if (len >= 0) {
+    out->resize((size_t)len);
+    return true;
+  }
   return raw_decode(tabs().url, s.substr(0, n), out, err);
 }
 
@@ -154,6 +161,42 @@ bool b64url_canonical(std::string_view s) {
   return r == 2 ? (v & 15) == 0 : (v & 3) == 0;          // unused low bits must be zero
 }
 
+long b64url_decode_fast(std::string_view s, char* out, bool* canonical) {
+  // 4 characters -> 3 bytes per step; an invalid symbol has the table's sign
+  // bit, so one OR over the group detects it
+  const int8_t* t = tabs().url;
+  const unsigned char* p = (const unsigned char*)s.data();
+  const size_t n = s.size(), full = n / 4 * 4;
+  unsigned char* o = (unsigned char*)out;
+  for (size_t i = 0; i < full; i += 4) {
+    const int32_t a = t[p[i]], b = t[p[i + 1]], c = t[p[i + 2]], d = t[p[i + 3]];
+    if ((a | b | c | d) < 0) return -1;
+    const uint32_t v = (uint32_t)a << 18 | (uint32_t)b << 12 | (uint32_t)c << 6 | (uint32_t)d;
+    o[0] = (unsigned char)(v >> 16);
+    o[1] = (unsigned char)(v >> 8);
+    o[2] = (unsigned char)v;
+    o += 3;
+  }
+  const size_t r = n - full;
+  bool canon = true;
+  if (r == 1) return -1;
+  if (r == 2) {
+    const int32_t a = t[p[full]], b = t[p[full + 1]];
+    if ((a | b) < 0) return -1;
+    *o++ = (unsigned char)((a << 2) | (b >> 4));
+    canon = (b & 15) == 0;
+  } else if (r == 3) {
+    const int32_t a = t[p[full]], b = t[p[full + 1]], c = t[p[full + 2]];
+    if ((a | b | c) < 0) return -1;
+    const uint32_t v = (uint32_t)a << 12 | (uint32_t)b << 6 | (uint32_t)c;
+    *o++ = (unsigned char)(v >> 10);
+    *o++ = (unsigned char)(v >> 2);
+    canon = (c & 3) == 0;
+  }
+  *canonical = canon;
+  return (long)(o - (unsigned char*)out);
+}
+
 // ====================================================================== whitespace
 namespace {
 bool go_is_space(uint32_t r) {
@@ -168,7 +211,15 @@ bool go_is_space(uint32_t r) {
 }  // namespace
 
 bool has_go_space_or_nonascii(std::string_view s) {
-  for (char ch : s) {
+  // 8 bytes at a time: a byte >= 0x80, or a byte < 0x21 (SWAR "has less than")
+  constexpr uint64_t ones = 0x0101010101010101ULL, highs = 0x8080808080808080ULL;
+  size_t i = 0;
+  for (; i + 8 <= s.size(); i += 8) {
+    uint64_t w;
+    std::memcpy(&w, s.data() + i, 8);
+    if ((w & highs) | ((w - ones * 0x21) & ~w & highs)) return true;
+  }
+  for (char ch : s.substr(i)) {
     const unsigned char c = (unsigned char)ch;
     if (c >= 0x80 || c <= ' ') return true;
   }

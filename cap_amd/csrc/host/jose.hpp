@@ -34,6 +34,12 @@ bool b64std_decode(std::string_view s, std::string* out);
 // unused non-zero bits.  Only then is the literal token text the
 // signing input.
 bool b64url_canonical(std::string_view s);
+// Fast path of b64url_decode for a segment of alphabet characters only (no
+// '=', CR, LF or other byte): decodes into out[0 .. s.size()*3/4] and returns
+// the length, with *canonical = b64url_canonical(s).  Returns -1 if s holds any
+// other byte or ends in a 1-character group; the caller then takes
+// b64url_decode (which reproduces Go's skipping and error text).
+long b64url_decode_fast(std::string_view s, char* out, bool* canonical);
 
 // go-jose stripWhitespace: removes every rune for which unicode.IsSpace holds;
 // invalid UTF-8 bytes become U+FFFD (ranging over a Go string).

@@ -191,14 +191,25 @@ struct Reader {
 
   bool number(Value* v) {
     const unsigned char* s = p;
-    if (*p == '-') ++p;
+    const bool neg = *p == '-';
+    if (neg) ++p;
     if (p >= end) return fail("in numeric literal");
+    uint64_t iv = 0;
     if (*p == '0') {
       ++p;
     } else if (*p >= '1' && *p <= '9') {
-      while (p < end && *p >= '0' && *p <= '9') ++p;
+      while (p < end && *p >= '0' && *p <= '9') iv = iv * 10 + (uint64_t)(*p++ - '0');
     } else {
       return fail("in numeric literal");
+    }
+    const size_t ndig = (size_t)(p - s) - neg;
+    if (ndig <= 15 && (p >= end || (*p != '.' && *p != 'e' && *p != 'E'))) {
+      // an integer below 10^15 is exact in float64: ParseFloat's result without strtod
+      v->kind = Value::Number;
+      v->str.assign((const char*)s, (size_t)(p - s));
+      v->num = neg ? -(double)iv : (double)iv;
+      v->num_range_err = false;
+      return true;
     }
     if (p < end && *p == '.') {
       ++p;
@@ -294,6 +305,7 @@ struct Reader {
         if (it != index.end()) at = it->second;
         else index.emplace(key, v->obj.size());
       }
+      if (at == v->obj.size() && v->obj.empty()) v->obj.reserve(8);   // one allocation for a claims set
       if (at == v->obj.size()) v->obj.emplace_back(std::move(key), std::move(val));
       else v->obj[at].second = std::move(val);
       ws();

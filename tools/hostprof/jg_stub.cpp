@@ -1,0 +1,26 @@
+// jg_stub.cpp -- timing stand-in for libcapjwt.so's C ABI, linked ONLY into
+// tools/hostprof (the host-phase timing harness).  It verifies nothing: every
+// job is reported accepted so the host layer runs its full accept path.  Never
+// linked into the product or any test.
+#include <cstdlib>
+#include <cstring>
+
+#include "../../include/jg.h"
+
+struct jg_ctx {
+  int dummy;
+};
+
+extern "C" {
+jg_ctx* jg_create(const int*, int) { return new jg_ctx{0}; }
+void jg_destroy(jg_ctx* c) { delete c; }
+const char* jg_last_error(jg_ctx*) { return "stub"; }
+int jg_keys_load(jg_ctx*, const jg_key*, int) { return 0; }
+void* jg_host_alloc(size_t n) { return std::malloc(n); }
+void jg_host_free(void* p) { std::free(p); }
+int jg_verify_batch(jg_ctx*, const uint8_t*, size_t, const jg_tok*, size_t n, uint8_t* verdicts) {
+  std::memset(verdicts, JG_ACCEPT, n);
+  return 0;
+}
+int jg_hash_batch(jg_ctx*, const uint8_t*, size_t, const jg_hjob*, size_t, uint8_t*) { return -1; }
+}
