@@ -258,6 +258,7 @@ struct Bufs {
   // index -> caller index, for the device-side verdict scatter (pipeline
   // chunks scatter on the host from their staged perm instead)
   Grow arena, jobs, perm, meta, sigw, dig, status, siglen, vpad, verdict, rows, pss, exc, exc_cnt;
+  Grow mid;                       // per key: shared SHA-256 block 0 and its midstate (k_prep_mid)
 };
 
 // Host side of one staged chunk: the counting-sort layout.
@@ -270,6 +271,7 @@ struct Plan {
   int rsa4k_limbs = 148, rsa4k_layouts = 1;   // the context's RSA-4K+ layouts at plan time
   int64_t pss_tokens = 0;         // PSS scratch tokens: the RSA classes' ranges back to back
   int64_t pss_off[NCLS] = {};
+  int64_t nkeys = 0;              // key table size at plan time (prep midstate slots)
 };
 
 struct PlanScratch {              // reused across chunks
@@ -589,6 +591,7 @@ void plan_layout(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, Plan& P, Pl
   P.pss_tokens = 0;
   P.rsa4k_limbs = ctx->rsa4k_limbs;
   P.rsa4k_layouts = ctx->rsa4k_layouts;
+  P.nkeys = (int64_t)ctx->keys.size();
   for (int c = 1; c < NCLS; ++c) {
     if (P.ranges[c].end <= P.ranges[c].begin) continue;
     P.sig_rows = std::max(P.sig_rows, cls_rows_sig(c, P.rsa4k_limbs));
@@ -720,6 +723,15 @@ Marker marker(jg_batch* b, int cls) {
 // fanout: run the classes of a mixed plan on the lane's per-class streams
 // (resident batches); pipeline chunks keep them in order on the lane's own
 // stream unless CAPJWT_FANOUT=1 (measurement A/B)
+// CAPJWT_MIDSTATE=0 turns the shared block-0 midstate of the prep kernel off (A/B)
+bool prep_midstate() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_MIDSTATE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 bool pipeline_fanout() {
   static const bool on = [] {
     const char* e = std::getenv("CAPJWT_FANOUT");
@@ -747,6 +759,8 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks, bool 
   pa.status = (uint8_t*)B->status.p;
   pa.siglen = (uint16_t*)B->siglen.p;
   pa.npad = np;
+  pa.mid = prep_midstate() ? (uint32_t*)B->mid.get(sizeof(uint32_t) * PREP_MID_WORDS * (size_t)std::max<int64_t>(P.nkeys, 1))
+                           : nullptr;
   uint32_t* rows = (uint32_t*)B->rows.p;
   if (conc) HIPCHK(hipEventRecord(L->ev_start, s0));
   for (int c = 1; c < NCLS; ++c) {
@@ -883,6 +897,7 @@ void reserve_slot(const jg_ctx* ctx, Slot& S, size_t C, size_t nbuckets, double 
   B->rows.get(sizeof(uint32_t) * (size_t)scratch_rows * npad);
   if (rsa) B->pss.get(C * 2048);
   B->exc.get(sizeof(int32_t) * npad);
+  B->mid.get(sizeof(uint32_t) * PREP_MID_WORDS * std::max<size_t>(ctx->keys.size(), 1));
   S.reserved = C;
   S.reserved_epoch = ctx->epoch;
 }

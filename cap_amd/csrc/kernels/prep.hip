@@ -81,6 +81,48 @@ __device__ __forceinline__ void window_words(const uint32_t* u, uint32_t i0, uin
   }
 }
 
+// Shared block 0 (SHA-256 classes).  Tokens of one issuer usually share their
+// first 64 bytes of signing input: the protected header (alg, kid, typ) and the
+// start of the payload.  One thread per key run (the first wave of each run in
+// the key-sorted plan) hashes its first token's block 0 and records the block
+// and the midstate in the key's slot; k_prep then skips block 0 for a wave
+// whose every live lane has exactly that block (16-word compare), starting from
+// the recorded midstate.  Equal blocks give equal compression outputs, so the
+// digest is unchanged.  Runs before k_prep on the same stream; the slots live
+// in the batch's own scratch (no sharing between batches in flight).
+__global__ void __launch_bounds__(64) k_prep_mid(PrepArgs a) {
+  const int64_t w = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (w >= (a.end - a.begin) / WAVE) return;
+  const int64_t p0 = a.begin + w * WAVE;
+  const JobDev jb = a.jobs[p0];
+  if (!job_live(jb)) return;
+  const int key = job_key(jb);
+  if (w > 0) {
+    const JobDev prev = a.jobs[p0 - WAVE];
+    if (job_live(prev) && job_key(prev) == key) return;    // not the run's first wave
+  }
+  uint32_t* slot = a.mid + (size_t)key * PREP_MID_WORDS;
+  const uint32_t len = jb.sig_in_len;
+  if (alg_hash_bits(job_alg(jb)) != 256 || (len + 9 + 63) / 64 < 2) {   // block 0 is the last block
+    slot[24] = 0u;
+    return;
+  }
+  const uint32_t* arena_w = reinterpret_cast<const uint32_t*>(a.arena);
+  const uint64_t mw0 = jb.off >> 2;
+  uint32_t u[17];
+#pragma unroll
+  for (int k = 0; k < 17; ++k) u[k] = arena_w[mw0 + k];    // within the arena's slack
+  uint32_t blk[16], h[8];
+  window_words<16>(u, 0, jb.off & 3u, len, blk);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) slot[k] = blk[k];
+  sha2::sha256_init(h);
+  sha2::sha256_compress(h, blk);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) slot[16 + k] = h[k];
+  slot[24] = 1u;
+}
+
 // HM: hash families present in the launch range (bit 0 SHA-256, bit 1
 // SHA-384/512, from the runtime's dispatch plan).  A single-family variant
 // drops the other SHA's code and registers: the SHA-512 path alone raises the
@@ -305,6 +347,18 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
             w[14] = len >> 29;
             w[15] = len << 3;
           }
+          if (blk == 0 && a.mid) {
+            // the key run's shared block 0 (k_prep_mid): wave-uniform skip
+            const uint32_t* ms = a.mid + (size_t)__builtin_amdgcn_readfirstlane(job_key(jb)) * PREP_MID_WORDS;
+            bool same = nblk >= 2 && ms[24] != 0u;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) same = same && w[k] == ms[k];
+            if (__ballot(!same) == 0ull) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) h32[k] = ms[16 + k];
+              continue;
+            }
+          }
           sha2::sha256_compress(h32, w);
         }
       }
@@ -356,9 +410,12 @@ void launch_hm(int hm, dim3 g, dim3 b, const PrepArgs& a, hipStream_t s) {
   }
 }
 
-void launch_prep(int cls, int hash_mask, const PrepArgs& a, hipStream_t s) {
-  const int64_t waves = (a.end - a.begin) / WAVE;
+void launch_prep(int cls, int hash_mask, const PrepArgs& a0, hipStream_t s) {
+  const int64_t waves = (a0.end - a0.begin) / WAVE;
   if (waves <= 0) return;
+  PrepArgs a = a0;
+  if (cls == CLS_ED25519 || !(hash_mask & 1)) a.mid = nullptr;      // SHA-256 block 0 only
+  if (a.mid) hipLaunchKernelGGL(k_prep_mid, dim3((unsigned)((waves + 63) / 64)), dim3(64), 0, s, a);
   dim3 g((unsigned)waves), b(WAVE);
   switch (cls) {
     case CLS_RSA2K: case CLS_RSA3K: case CLS_RSA4K:
