@@ -119,6 +119,14 @@ void run_chunks(const Chunks& c, F&& fn) {
   for (auto& t : th) t.join();
 }
 
+}  // namespace
+
+void batch_parallel(size_t n, int threads, const std::function<void(size_t, size_t)>& fn) {
+  parallel_for(n, threads, fn);
+}
+
+namespace {
+
 int64_t wall_now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
       .count();
@@ -537,7 +545,7 @@ class StaticKeySet final : public KeySet {
     eng_.load(keys_);
     for (const auto& k : keys_) fam_.push_back(key_family(k));
   }
-  std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
+  Results verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
     std::lock_guard<std::mutex> g(mu_);
     Verified V;
     gpu_verify(eng_, tokens, &V, [&](const Tok& t, std::vector<uint16_t>& out) {
@@ -547,7 +555,7 @@ class StaticKeySet final : public KeySet {
       for (size_t k = 0; k < keys_.size(); ++k)
         if (fam_[k] == fam) out.push_back((uint16_t)k);
     });
-    std::vector<Result> res(tokens.size());
+    Results res(tokens.size(), eng_.threads());
     PhaseTimer pt("static");
     parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
@@ -610,12 +618,12 @@ class JSONWebKeySet final : public KeySet {
   JSONWebKeySet(std::string url, std::string ca, Fetcher f, const std::vector<int>& devices)
       : url_(std::move(url)), ca_(std::move(ca)), fetch_(std::move(f)), eng_(devices) {}
 
-  std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
+  Results verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
     std::lock_guard<std::mutex> g(mu_);
     Verified V;
     std::string miss_err;
     remote_verify(tokens, &V, &miss_err);
-    std::vector<Result> res(tokens.size());
+    Results res(tokens.size(), eng_.threads());
     PhaseTimer pt("jwks");
     parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
@@ -835,10 +843,10 @@ void Engine::verify(const uint8_t* arena, size_t arena_len, const void* jobs, si
 
 // ====================================================================== KeySet
 Result KeySet::VerifySignature(std::string_view token) {
-  return verify_batch({token}, nullptr)[0];
+  return std::move(verify_batch({token}, nullptr)[0]);
 }
 
-std::vector<Result> KeySet::VerifySignatureBatch(const std::vector<std::string_view>& tokens) {
+Results KeySet::VerifySignatureBatch(const std::vector<std::string_view>& tokens) {
   return verify_batch(tokens, nullptr);
 }
 
@@ -1095,18 +1103,13 @@ Result validate_claims(const json::Value& all_claims, const TokenView& info, con
   return r;
 }
 
-void release_results(std::vector<Result>& rs) {
-  parallel_for(rs.size(), host_threads(), [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) rs[i] = Result();
-  });
-  std::vector<Result>().swap(rs);
-}
+void release_results(Results& rs) { rs.release(); }
 
 Result Validator::Validate(std::string_view token, const Expected& expected) {
-  return ValidateBatch({token}, expected)[0];
+  return std::move(ValidateBatch({token}, expected)[0]);
 }
 
-std::vector<Result> Validator::ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected) {
+Results Validator::ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected) {
   const int64_t now = expected.has_now ? expected.now_unix_ns : wall_now_ns();
   // the claim checks run inside the key set's per-token pass, on the host
   // threads, while each token's claims map is still in cache; a claims map

@@ -49,6 +49,63 @@ struct Result {
   std::string err;
 };
 
+// ---------------------------------------------------------------- batch arrays
+// Runs fn(begin, end) over [0, n) on `threads` host threads (contiguous ranges;
+// small n stays on the caller's thread).
+void batch_parallel(size_t n, int threads, const std::function<void(size_t, size_t)>& fn);
+int host_threads();
+
+// The per-token records of a batch, constructed and destroyed by all host
+// threads: a 1M-token batch's results are ~150 MB of records plus their claims
+// maps, and a serial std::vector construction or free of that costs more than
+// the batch's parse.  Move-only; indexable and iterable like a vector.
+template <class T>
+class BatchArray {
+ public:
+  BatchArray() = default;
+  explicit BatchArray(size_t n, int threads = host_threads()) : threads_(threads) {
+    p_ = static_cast<T*>(::operator new(sizeof(T) * (n ? n : 1)));
+    batch_parallel(n, threads_, [this](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) new (p_ + i) T();
+    });
+    n_ = n;
+  }
+  BatchArray(BatchArray&& o) noexcept : p_(o.p_), n_(o.n_), threads_(o.threads_) { o.p_ = nullptr; o.n_ = 0; }
+  BatchArray& operator=(BatchArray&& o) noexcept {
+    if (this != &o) {
+      release();
+      p_ = o.p_; n_ = o.n_; threads_ = o.threads_;
+      o.p_ = nullptr; o.n_ = 0;
+    }
+    return *this;
+  }
+  BatchArray(const BatchArray&) = delete;
+  BatchArray& operator=(const BatchArray&) = delete;
+  ~BatchArray() { release(); }
+  void release() {
+    if (!p_) return;
+    batch_parallel(n_, threads_, [this](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) p_[i].~T();
+    });
+    ::operator delete(p_);
+    p_ = nullptr;
+    n_ = 0;
+  }
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  size_t size() const { return n_; }
+  T* begin() { return p_; }
+  T* end() { return p_ + n_; }
+  const T* begin() const { return p_; }
+  const T* end() const { return p_ + n_; }
+
+ private:
+  T* p_ = nullptr;
+  size_t n_ = 0;
+  int threads_ = 1;
+};
+using Results = BatchArray<Result>;
+
 // ---------------------------------------------------------------- HTTP
 // The JWKS / discovery GET.  The reference uses net/http with a TLS client
 // built from the CA PEM (createCAContext, jwt/keyset.go:204-227); here the
@@ -112,10 +169,10 @@ class KeySet {
   virtual ~KeySet() = default;
   // jwt/keyset.go:27-32
   Result VerifySignature(std::string_view token);
-  std::vector<Result> VerifySignatureBatch(const std::vector<std::string_view>& tokens);
+  Results VerifySignatureBatch(const std::vector<std::string_view>& tokens);
   // batch verify; `post` (may be null) continues each token's result with what
   // the parse learned (Validator::ValidateBatch)
-  virtual std::vector<Result> verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) = 0;
+  virtual Results verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) = 0;
 };
 
 std::unique_ptr<KeySet> NewStaticKeySet(const std::vector<PublicKey>& keys, std::string* err,
@@ -170,7 +227,7 @@ class Validator {
  public:
   explicit Validator(KeySet* ks) : ks_(ks) {}
   Result Validate(std::string_view token, const Expected& expected);
-  std::vector<Result> ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected);
+  Results ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected);
  private:
   KeySet* ks_;
 };
@@ -186,13 +243,11 @@ Result validate_claims(const json::Value& all_claims, const TokenView& info, con
 
 bool ParsePublicKeyPEM(std::string_view data, PublicKey* out, std::string* err);
 
-// Frees a large result vector with all host threads (1M claims maps are ~10M
-// allocations; a serial free costs more than the batch's parse).
-void release_results(std::vector<Result>& rs);
+// Frees a batch's results now (all host threads; the destructor does the same).
+void release_results(Results& rs);
 
 // Host threads used by batch parsing / claims (CAPJWT_HOST_THREADS, default
-// available_cpus()).
-int host_threads();
+// available_cpus()): declared above.
 // CPUs available to this process (affinity mask, cgroup v2 quota)
 int available_cpus();
 
