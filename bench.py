@@ -50,7 +50,10 @@ ALG_IDS = {"RS256": 1, "RS384": 2, "RS512": 3, "PS256": 4, "PS384": 5, "PS512": 
 
 
 # ---------------------------------------------------------------- algorithmic work
-def p256_point_mads_per_token(wq=24):
+P256_WQ = 24          # key comb width of the run (main() sets it from the table budget)
+
+
+def p256_point_mads_per_token(wq=None):
     """Algorithmic 32x32->64 multiply-accumulates the P-256 comb kernel
     (k_ec_point) issues per token: 28-bit limbs, L = 10; a product is L^2 (mul)
     or L(L+1)/2 (sqr) partial products, a Montgomery reduction L * 4 (p + 1 has
@@ -61,12 +64,21 @@ def p256_point_mads_per_token(wq=24):
     mp.hpp mont_reduce) and the column adds of x3_from are carries / additions,
     not partial products, and are not counted.
     Signed comb digits (ecdsa.hpp ec_comb_w / ec_key_w): 10 windows of 26
-    bits for u1 (generator table) and ceil(257 / wq) for u2 (key table: W = 24
-    for the bench's 4 kids under the default 32 GiB table budget, 11 windows),
+    bits for u1 (generator table) and ceil(257 / wq) for u2 (key table: W = 26
+    for the bench's 4 kids under its 110 GiB table budget, 10 windows),
     each non-zero w.p. 1 - 2^-W, the first addition an assignment and the
     second onto Z == 1 (madd_z1: 4 mul + 2 sqr under 5 reductions); final check
     1 sqr + 2 mul."""
-    return ec_point_mads_per_token(10, 4, 0, 26, wq, 256, 10 * 4, merged=True)
+    return ec_point_mads_per_token(10, 4, 0, 26, wq or P256_WQ, 256, 10 * 4, merged=True)
+
+
+def p256_key_w(nkeys, budget):
+    """ecdsa.hpp ec_key_w for P-256: the widest key comb whose tables for
+    `nkeys` keys fit `budget` bytes (W = 26 / 24 / 22 / 20)."""
+    for w in (26, 24, 22, 20):
+        if nkeys * (-(-257 // w)) * (1 << (w - 1)) * 80 <= budget:
+            return w
+    return 20
 
 
 def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged):
@@ -648,6 +660,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--table-budget-gb", type=float, default=110.0,
+                    help="HBM for P-256 key comb tables (jg_set_table_budget): 110 GiB holds the 4 kids at W = 26")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -671,6 +685,10 @@ def main():
     cpu = cpu_info()
     host_threads = cpu["cores_used"]          # every core this process may use (cgroup quota, affinity)
     ctx = _lib.Context([dev])
+    budget = int(args.table_budget_gb * (1 << 30))
+    ctx.set_table_budget(budget)
+    global P256_WQ
+    P256_WQ = p256_key_w(4, budget)
 
     # ---- ES256, P-256 JWKS with 4 kids (configs[1]): 1M unique OpenSSL-signed tokens
     kids = ["p256-a", "p256-b", "p256-c", "p256-d"]
@@ -701,6 +719,7 @@ def main():
                 + (f" replicated to {ntok}" if npool < ntok else "") + " per GPU, no verdict caching",
         "config": {"workload": "ES256 P-256 JWKS with 4 kids, 1M tokens batch-verified per MI355X (BASELINE configs[1])",
                    "tokens_per_gpu": ntok, "unique_tokens": npool, "kids": 4,
+                   "table_budget_GiB": args.table_budget_gb, "p256_key_comb_w": P256_WQ,
                    "parallelism": f"independent shards x{world}"},
         "accepted": acc,
         "roofline": {"bound": "valu", "kernel": "k_ec_point<P256>",

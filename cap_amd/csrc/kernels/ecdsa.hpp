@@ -63,17 +63,19 @@ constexpr int64_t ec_table_words_w(int cls, int w) {
 constexpr int64_t ec_table_words(int cls, bool gen) { return ec_table_words_w(cls, ec_comb_w(cls, gen)); }
 // Key-table width tiers (HBM for fewer additions, as the generators' wide
 // windows do): the widest W whose tables for all `nkeys` keys of the curve fit
-// `budget` bytes.  P-256: W = 24 (11 windows, 7.4 GB per key), 22 (12, 2.0 GB),
-// 20 (13, 545 MB); P-384: 20 (20 windows, 1.34 GB), 18 (22, 369 MB), 16 (25,
-// 105 MB); P-521: 20 (27, 2.26 GB), 18 (29, 608 MB), 16 (33, 173 MB).  The
-// narrowest width is always allowed.  The budget applies to each curve.
-constexpr int EC_P256_WQ[3] = {24, 22, 20};
+// `budget` bytes.  P-256: W = 26 (10 windows, 26.8 GB per key: 20 additions
+// per token with the W = 26 generator), 24 (11 windows, 7.4 GB), 22 (12,
+// 2.0 GB), 20 (13, 545 MB); P-384: 20 (20 windows, 1.34 GB), 18 (22, 369 MB),
+// 16 (25, 105 MB); P-521: 20 (27, 2.26 GB), 18 (29, 608 MB), 16 (33, 173 MB).
+// The narrowest width is always allowed.  The budget applies to each curve.
+constexpr int EC_P256_WQ[4] = {26, 24, 22, 20};
 constexpr int EC_WIDE_WQ[3] = {20, 18, 16};
 inline int ec_key_w(int cls, int nkeys, uint64_t budget) {
   const int* t = cls == jgk::CLS_P256 ? EC_P256_WQ : EC_WIDE_WQ;
-  for (int i = 0; i < 3; ++i)
+  const int nt = cls == jgk::CLS_P256 ? 4 : 3;
+  for (int i = 0; i < nt; ++i)
     if ((uint64_t)nkeys * (uint64_t)ec_table_words_w(cls, t[i]) * 4u <= budget) return t[i];
-  return t[2];
+  return t[nt - 1];
 }
 
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);

@@ -200,17 +200,17 @@ def test_rsa_keys_above_4096_bits():
         assert out[s] == want, t["name"]
 
 
-@pytest.mark.parametrize("tier", ["w24", "w22", "w20"])
+@pytest.mark.parametrize("tier", ["w26", "w24", "w22", "w20"])
 def test_p256_key_table_widths(tier):
     """The P-256 key comb width follows the table budget (jg_set_table_budget,
-    ecdsa.hpp ec_key_w): W = 24 / 22 / 20 give the same verdicts as the oracle
+    ecdsa.hpp ec_key_w): W = 26 / 24 / 22 / 20 give the same verdicts as the oracle
     on every golden token against every key, and on a random ES256 batch."""
     from cap_amd import _lib
     from oracle import jws
     keys, toks = H.golden()
     n256 = sum(1 for k in keys if k.get("kty") == "EC" and k.get("crv") == "P-256")
     assert n256 >= 2
-    per_key = {"w24": 11 * (1 << 23) * 80, "w22": 12 * (1 << 21) * 80, "w20": 0}[tier]
+    per_key = {"w26": 10 * (1 << 25) * 80, "w24": 11 * (1 << 23) * 80, "w22": 12 * (1 << 21) * 80, "w20": 0}[tier]
     ctx = _lib.Context()
     ctx.set_table_budget(n256 * per_key)
     ctx.load_keys([H.abi_key(k) for k in keys])
