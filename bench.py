@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 KEYDIR = os.path.join(ROOT, "tests", "golden", "keys")
 BENCHKEYS = os.path.join(ROOT, "tools", "benchkeys")
 TOKGEN = os.path.join(ROOT, "tools", "tokgen", "tokgen")
-TRAFFIC = os.path.join(ROOT, "profiles", "r02_s4_pmc_traffic.json")
+TRAFFIC = os.path.join(ROOT, "profiles", "r02_s10_pmc_traffic.json")
 COLL_DEVICE = "cuda"            # device of the timing all-reduce (RCCL); "cpu" under gloo
 
 # measured v_mad_u64_u32 issue rate, chip-wide: the integer multiply-add
@@ -628,7 +628,7 @@ def run_configs(ctx, args, threads, rank, world, dist):
     # plan, kernels, verdicts back), chunks overlapping
     share = 10_000_000 // 8
     arena, toks = pack(pool, algs, keyidx, share)
-    st = measure_pcie(ctx, arena, toks, iters=2, chunks=(65536, 262144))
+    st = measure_pcie(ctx, arena, toks, iters=2, chunks=(65536, 262144, 524288))
     st["workload"] = f"{share} tokens per GPU (10M / 8) streamed with H2D"
     line["stream"] = st
     out["mixed_10alg_32kid"] = line

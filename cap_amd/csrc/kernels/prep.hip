@@ -71,6 +71,11 @@ __device__ __forceinline__ void stage(uint32_t* slots, uint64_t* wsh, const uint
 template <int N>
 __device__ __forceinline__ void window_words(const uint32_t* u, uint32_t i0, uint32_t shift, uint32_t len,
                                              uint32_t* out) {
+  if (4u * (i0 + N) <= len) {            // all N words inside the message: no length masks
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = sha2::bswap32(__builtin_amdgcn_alignbyte(u[k + 1], u[k], shift));
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     const uint32_t raw = sha2::bswap32(__builtin_amdgcn_alignbyte(u[k + 1], u[k], shift));
