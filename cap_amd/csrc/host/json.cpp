@@ -281,33 +281,38 @@ struct Reader {
     ws();
     if (p < end && *p == '}') { ++p; return true; }
     std::unordered_map<std::string, size_t> index;   // only for large objects
+    v->obj.reserve(8);                                // one allocation for a claims set
     while (true) {
       ws();
       if (p >= end) return fail("");
       if (*p != '"') return fail("looking for beginning of object key string");
-      std::string key;
-      if (!string(&key)) return false;
+      // the member is parsed in place at the end of the object; a duplicate
+      // name then moves its value onto the earlier member (map assignment:
+      // the last duplicate wins)
+      v->obj.emplace_back();
+      const size_t at_new = v->obj.size() - 1;
+      if (!string(&v->obj[at_new].first)) return false;
       ws();
       if (p >= end) return fail("");
       if (*p != ':') return fail("after object key");
       ++p;
-      Value val;
-      if (!value(&val, depth)) return false;
-      // map assignment: the last duplicate wins
-      size_t at = v->obj.size();
-      if (v->obj.size() < 16) {
-        for (size_t i = 0; i < v->obj.size(); ++i)
+      if (!value(&v->obj[at_new].second, depth)) return false;
+      const std::string& key = v->obj[at_new].first;
+      size_t at = at_new;
+      if (at_new < 16) {
+        for (size_t i = 0; i < at_new; ++i)
           if (v->obj[i].first == key) { at = i; break; }
-        if (at == v->obj.size() && v->obj.size() == 15)
-          for (size_t i = 0; i < v->obj.size(); ++i) index.emplace(v->obj[i].first, i);
+        if (at == at_new && at_new == 15)
+          for (size_t i = 0; i <= at_new; ++i) index.emplace(v->obj[i].first, i);
       } else {
         auto it = index.find(key);
         if (it != index.end()) at = it->second;
-        else index.emplace(key, v->obj.size());
+        else index.emplace(key, at_new);
       }
-      if (at == v->obj.size() && v->obj.empty()) v->obj.reserve(8);   // one allocation for a claims set
-      if (at == v->obj.size()) v->obj.emplace_back(std::move(key), std::move(val));
-      else v->obj[at].second = std::move(val);
+      if (at != at_new) {
+        v->obj[at].second = std::move(v->obj[at_new].second);
+        v->obj.pop_back();
+      }
       ws();
       if (p >= end) return fail("");
       if (*p == ',') { ++p; continue; }

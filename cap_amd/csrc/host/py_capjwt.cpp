@@ -203,6 +203,13 @@ PYBIND11_MODULE(_capjwt_host, m) {
     if (json::has_range_error(v)) return py::make_tuple(py::none(), py::str("number out of range"));
     return py::make_tuple(to_py(v), py::none());
   });
+  m.def("json_marshal", [](py::bytes b) -> py::object {
+    // json.Marshal of the parsed interface{} (sorted keys; a member appears once)
+    json::Value v;
+    std::string err, s = b;
+    if (!json::parse(s, &v, &err)) return py::none();
+    return py::bytes(json::marshal(v));
+  });
   m.def("b64url_decode", [](const std::string& s) -> py::object {
     std::string out, err;
     if (!b64url_decode(s, &out, &err)) return py::none();

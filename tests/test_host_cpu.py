@@ -37,7 +37,21 @@ JSON_DOCS = [
     b'1e400', b'[1e400]', b'1e-400', b'{"a":1}x', b'{"a":1,}', b'[1,]', b'01', b'1.', b'.5', b'+1', b'NaN',
     b'Infinity', b'"a\x01"', b'"\\x"', b'{"a"}', b'', b' ', b'tru', b'nul', b'{"a":1', b'[1 2]', b'"\\u12"',
     b'{"a":"\\/\\b\\f\\n\\r\\t"}', b'123456789012345678901234567890', b'1.7976931348623157e308', b'-1.8e308',
+    # integer literals around the parser's exact fast path (<= 15 digits)
+    b'999999999999999', b'-999999999999999', b'1000000000000000', b'9007199254740993', b'[0,-0,7,1611699344]',
 ]
+
+
+def _big_object(n, dups):
+    # n distinct members k00..k{n-1}, then re-assignments of the members in `dups`
+    mem = [f'"k{i:02d}":{i}' for i in range(n)] + [f'"k{i:02d}":"again{i}"' for i in dups]
+    return ("{" + ",".join(mem) + "}").encode()
+
+
+# objects across the linear-scan / index switch (16 members): a duplicate of
+# each position must replace the earlier member (the last duplicate wins)
+JSON_DOCS += [_big_object(n, d) for n, d in [(15, [14]), (16, [15]), (16, [0, 15]), (17, [15, 16]), (20, [15, 3, 19]),
+                                              (40, [15, 16, 39, 0])]]
 
 
 @pytest.mark.parametrize("doc", JSON_DOCS)
@@ -51,6 +65,17 @@ def test_json_matches_go_semantics(doc):
     assert (err is None) == ok, (doc, err)
     if ok:
         assert v == want
+
+
+@pytest.mark.parametrize("n,dups", [(15, [14]), (16, [15]), (17, [15, 16]), (20, [15, 3, 19]), (40, [15, 16, 39, 0])])
+def test_json_duplicate_members_replace_in_place(n, dups):
+    """map assignment: a re-assigned member keeps one entry holding the last
+    value, on both sides of the parser's 16-member index switch"""
+    out = H.json_marshal(_big_object(n, dups))
+    for i in range(n):
+        assert out.count(f'"k{i:02d}":'.encode()) == 1, (i, out)
+    for i in dups:
+        assert f'"k{i:02d}":"again{i}"'.encode() in out
 
 
 # ---------------------------------------------------------------- base64url / whitespace
