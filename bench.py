@@ -686,6 +686,10 @@ def main():
     host_threads = cpu["cores_used"]          # every core this process may use (cgroup quota, affinity)
     ctx = _lib.Context([dev])
     budget = int(args.table_budget_gb * (1 << 30))
+    if dist and COLL_DEVICE == "cpu":
+        # ranks sharing one GPU (a rehearsal of N > 1 on a smaller box): each
+        # process holds its own tables, so keep them at the 32 GiB default
+        budget = min(budget, 32 << 30)
     ctx.set_table_budget(budget)
     global P256_WQ
     P256_WQ = p256_key_w(4, budget)
@@ -719,7 +723,7 @@ def main():
                 + (f" replicated to {ntok}" if npool < ntok else "") + " per GPU, no verdict caching",
         "config": {"workload": "ES256 P-256 JWKS with 4 kids, 1M tokens batch-verified per MI355X (BASELINE configs[1])",
                    "tokens_per_gpu": ntok, "unique_tokens": npool, "kids": 4,
-                   "table_budget_GiB": args.table_budget_gb, "p256_key_comb_w": P256_WQ,
+                   "table_budget_GiB": budget / (1 << 30), "p256_key_comb_w": P256_WQ,
                    "parallelism": f"independent shards x{world}"},
         "accepted": acc,
         "roofline": {"bound": "valu", "kernel": "k_ec_point<P256>",
