@@ -1,0 +1,38 @@
+"""CPU checks of bench.py's accounting (no GPU): the key comb width it assumes
+for the roofline's MAD count must be the one the library picks for the same
+table budget (kernels/ecdsa.hpp ec_key_w / include/jg.h jg_set_table_budget),
+and the MAD counts must follow the additions per token."""
+import os
+import re
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GiB = 1 << 30
+
+
+def _header_tiers():
+    src = open(os.path.join(ROOT, "cap_amd", "csrc", "kernels", "ecdsa.hpp")).read()
+    m = re.search(r"EC_P256_WQ\[\d+\]\s*=\s*\{([^}]*)\}", src)
+    return [int(x) for x in m.group(1).split(",")]
+
+
+def test_p256_width_tiers_match_the_library():
+    assert _header_tiers() == [26, 24, 22, 20]
+    # the documented cut-offs (jg.h)
+    assert bench.p256_key_w(4, 110 * GiB) == 26
+    assert bench.p256_key_w(5, 110 * GiB) == 24
+    assert bench.p256_key_w(4, 32 * GiB) == 24
+    assert bench.p256_key_w(17, 32 * GiB) == 22
+    assert bench.p256_key_w(18, 32 * GiB) == 20
+    assert bench.p256_key_w(1, 0) == 20
+
+
+def test_point_mads_follow_the_window_count():
+    # one fewer key window (one fewer mixed addition) per step of the tiers
+    m = {w: bench.p256_point_mads_per_token(w) for w in (20, 22, 24, 26)}
+    assert m[20] > m[22] > m[24] > m[26]
+    per_add = m[24] - m[26]
+    assert abs((m[22] - m[24]) - per_add) < 1 and abs((m[20] - m[22]) - per_add) < 1
+    # a mixed addition: 8 mul + 3 sqr (L = 10) under 10 reductions of 4 L MADs
+    assert abs(per_add - (8 * 100 + 3 * 55 + 10 * 40)) < 1
