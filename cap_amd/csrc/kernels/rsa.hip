@@ -82,25 +82,26 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t x) {     // value of grou
 }
 
 // T[k] += a * b[k] for k < n (n compile-time after unrolling) as blocks of up
-// to 8 MADs per inline-asm statement: LLVM pads a hazard s_nop after an asm
-// statement whose results the next instruction touches, so one MAD per asm
-// cost ~1 s_nop per 4 MADs here (profiles/r01_int_rates2.json: 28.8 T MAD/s
-// with one MAD per asm vs 33.6 T with 8 per asm at 2 waves/SIMD).
+// to JG_RSA_MADBLK MADs per inline-asm statement: LLVM pads a hazard s_nop
+// after an asm statement whose results the next instruction touches, so one
+// MAD per asm cost ~1 s_nop per 4 MADs here (profiles/r01_int_rates2.json:
+// 28.8 T MAD/s with one MAD per asm vs 33.6 T with 8 per asm at 2 waves/SIMD).
+// 16-MAD blocks halve the s_nops but measured the same at 2 waves/SIMD and
+// spill more (profiles/r02_s11_rsa_occupancy_ab.json).
+//
+// Occupancy: left alone, the compiler gives k_rsa_modexp 256 VGPRs plus a few
+// AGPRs as spill space (RSA-2048: 262 in all), which allows ONE wave per
+// SIMD.  Capped at 256 (two waves per SIMD) it spills 5 registers to scratch
+// (RSA-4096: 2) and the RSA-2048 modexp runs 13 % faster (7.93 -> 6.91 ms per
+// 1M tokens): the second wave covers the CIOS rows' dependent chains.
+#ifndef JG_RSA_MODEXP_ATTR
+#define JG_RSA_MODEXP_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#endif
+#ifndef JG_RSA_MADBLK
+#define JG_RSA_MADBLK 8
+#endif
 __device__ __forceinline__ void madv_run(uint64_t* T, uint32_t a, const uint32_t* b, int n) {
-  for (int k = 0; k < n; k += 8) {
-    uint64_t* t = T + k;
-    const uint32_t* c = b + k;
-    switch (n - k < 8 ? n - k : 8) {
-      case 1: mb::madv1(t[0], a, c[0]); break;
-      case 2: mb::madv2(t[0], t[1], a, c[0], c[1]); break;
-      case 3: mb::madv3(t[0], t[1], t[2], a, c[0], c[1], c[2]); break;
-      case 4: mb::madv4(t[0], t[1], t[2], t[3], a, c[0], c[1], c[2], c[3]); break;
-      case 5: mb::madv5(t[0], t[1], t[2], t[3], t[4], a, c[0], c[1], c[2], c[3], c[4]); break;
-      case 6: mb::madv6(t[0], t[1], t[2], t[3], t[4], t[5], a, c[0], c[1], c[2], c[3], c[4], c[5]); break;
-      case 7: mb::madv7(t[0], t[1], t[2], t[3], t[4], t[5], t[6], a, c[0], c[1], c[2], c[3], c[4], c[5], c[6]); break;
-      default: mb::madv8(t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7], a, c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]); break;
-    }
-  }
+  for (int k = 0; k < n; k += JG_RSA_MADBLK) mb::madv_n(n - k < JG_RSA_MADBLK ? n - k : JG_RSA_MADBLK, T + k, a, b + k);
 }
 
 // All-ones in the lanes that keep a cross-lane value, zero in the others, as
@@ -316,7 +317,7 @@ __device__ __forceinline__ void store_limb_rows(uint32_t* rows, int64_t np, uint
 }
 
 template <int H, int G, int U>
-__global__ void __launch_bounds__(64) k_rsa_modexp(RsaArgs a) {
+__global__ void __launch_bounds__(64) JG_RSA_MODEXP_ATTR k_rsa_modexp(RsaArgs a) {
   constexpr int L = H * G, TPW = WAVE / G;
   constexpr int NWOUT = (W28 * L + 31) / 32;
   static_assert((W28 * L - 1) / 32 + 2 <= SIGW_ROWS, "limb loads and y words must fit the signature rows");
