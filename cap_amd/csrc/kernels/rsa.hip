@@ -97,6 +97,9 @@ __device__ __forceinline__ uint32_t from_prev(uint32_t x) {     // value of grou
 #ifndef JG_RSA_MODEXP_ATTR
 #define JG_RSA_MODEXP_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #endif
+#ifndef JG_RSA_PAD_ATTR
+#define JG_RSA_PAD_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#endif
 #ifndef JG_RSA_MADBLK
 #define JG_RSA_MADBLK 8
 #endif
@@ -506,7 +509,7 @@ __device__ __forceinline__ void mgf1_block(int hb, const uint32_t* Hw, int hw, u
 }
 
 template <bool PSS>
-__global__ void __launch_bounds__(64) k_rsa_pad(RsaArgs a) {
+__global__ void __launch_bounds__(64) JG_RSA_PAD_ATTR k_rsa_pad(RsaArgs a) {
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
   const JobDev jb = a.jobs[p];
