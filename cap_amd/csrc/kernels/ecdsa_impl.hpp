@@ -164,7 +164,16 @@ __device__ __forceinline__ void store_digits(const EcArgs& a, int64_t p, const u
 //   pass 2 (j descending): w_j = inv * c_{j-1}, inv *= s_j;
 //           u1 = e w_j, u2 = r w_j (mod n), signed W-bit digits
 template <class CV>
-__global__ void __launch_bounds__(64) k_ec_scalar_batch(EcArgs a, int B) {
+// JG_EC_SCALAR_ATTR: per translation unit.  ecdsa_p521.hip caps the kernel at
+// two waves per SIMD: left alone the compiler gives the P-521 instantiation
+// 295 VGPRs (+18 spilled), one wave per SIMD; capped it needs 198 and spills
+// nothing (scalar 0.172 -> 0.162 ms in configs[4]).  The same cap on P-384
+// squeezes 241 -> 139 VGPRs and runs 37 % slower, so the others keep the
+// compiler's choice.
+#ifndef JG_EC_SCALAR_ATTR
+#define JG_EC_SCALAR_ATTR
+#endif
+__global__ void __launch_bounds__(64) JG_EC_SCALAR_ATTR k_ec_scalar_batch(EcArgs a, int B) {
   using Fn = typename CV::Fn;
   constexpr int L = Fn::L;
   const int64_t np = a.npad;

@@ -1,5 +1,6 @@
 // ecdsa_p521.hip -- the P521 instantiations of ecdsa_impl.hpp: the verify
 // chain, key staging and generator table for every key-table width.
+#define JG_EC_SCALAR_ATTR __attribute__((amdgpu_waves_per_eu(2)))
 #include "ecdsa_impl.hpp"
 
 void launch_ec_p521(const EcArgs& a, hipStream_t s, const Marker& mk) {
