@@ -22,6 +22,10 @@ using namespace jgk;
 
 namespace {
 
+#ifndef JG_PREP_ED_ATTR
+#define JG_PREP_ED_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#endif
+
 constexpr int WIN = 32;         // dwords per window step (128 bytes of string)
 constexpr int SLOT = 36;        // LDS words per token slot (33 used; stride 36 keeps lanes' reads on distinct banks)
 
@@ -133,7 +137,7 @@ __global__ void __launch_bounds__(64) k_prep_mid(PrepArgs a) {
 // drops the other SHA's code and registers: the SHA-512 path alone raises the
 // kernel to ~224 VGPRs (2 waves/SIMD).
 template <int CLS, int HM>
-__global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
+__device__ __forceinline__ void prep_body(const PrepArgs& a) {
   __shared__ uint32_t slots[WAVE * SLOT];
   __shared__ uint64_t wsh[WAVE];
   __shared__ int8_t b64tab[256];
@@ -404,6 +408,17 @@ __global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
   a.status[p] = st;
 }
 
+template <int CLS, int HM>
+__global__ void __launch_bounds__(64) k_prep(PrepArgs a) {
+  prep_body<CLS, HM>(a);
+}
+
+// Ed25519's prep (SHA-512 of R || A || M) at three waves per SIMD: the
+// compiler's own choice is 216 VGPRs, two waves
+__global__ void __launch_bounds__(64) JG_PREP_ED_ATTR k_prep_ed(PrepArgs a) {
+  prep_body<CLS_ED25519, 2>(a);
+}
+
 }  // namespace
 
 template <int CLS>
@@ -428,7 +443,7 @@ void launch_prep(int cls, int hash_mask, const PrepArgs& a0, hipStream_t s) {
     case CLS_P256: case CLS_P384: case CLS_P521:
       launch_hm<CLS_P256>(hash_mask, g, b, a, s); break;
     case CLS_ED25519:
-      hipLaunchKernelGGL((k_prep<CLS_ED25519, 2>), g, b, 0, s, a); break;
+      hipLaunchKernelGGL(k_prep_ed, g, b, 0, s, a); break;
     default: break;
   }
 }
