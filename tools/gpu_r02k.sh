@@ -6,6 +6,6 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 bash tools/gpu_r02h.sh || exit 1
 for v in default padw1 rsaw1 default padw1 rsaw1; do
   if [ $v = default ]; then lib=cap_amd/libcapjwt.so; else lib=cap_amd/ab_$v.so; fi
-  CAPJWT_LIB=$lib timeout -k 10 300 python -u tools/ps512_probe.py > gpurun_out/ps512_$v.json 2> gpurun_out/ps512_$v.err || { echo PROBE_FAIL $v; tail -20 gpurun_out/ps512_$v.err; exit 1; }
+  CAPJWT_LIB=$lib timeout -k 10 300 python -u tools/config_probe.py ps512 > gpurun_out/ps512_$v.json 2> gpurun_out/ps512_$v.err || { echo PROBE_FAIL $v; tail -20 gpurun_out/ps512_$v.err; exit 1; }
   echo "$v $(cat gpurun_out/ps512_$v.json)"
 done
