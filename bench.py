@@ -101,13 +101,24 @@ def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged)
     return (adds - 1) * madd + madd_z1 + gsqr + 2 * gmul
 
 
-def p384_point_mads_per_token(wq=20):
-    """P-384 (ecdsa.hpp: L = 15 28-bit limbs, G W = 20, key W = 20 / 18 / 16 by
-    the table budget -- 20 for config 3's single key): the hot loop's mulf /
+def p384_key_w(nkeys, budget):
+    """ecdsa.hpp ec_key_w for P-384 (W = 24 / 20 / 18 / 16)."""
+    for w in (24, 20, 18, 16):
+        if nkeys * (-(-385 // w)) * (1 << (w - 1)) * 128 <= budget:
+            return w
+    return 16
+
+
+P384_BUDGET = 32 << 30    # main() sets the run's table budget
+
+
+def p384_point_mads_per_token(wq=None, nkeys=1):
+    """P-384 (ecdsa.hpp: L = 15 28-bit limbs, G W = 20, key W = 24 / 20 / 18 / 16
+    by the table budget -- 24 for config 3's single key): the hot loop's mulf /
     sqrf use the special-form reduction, 4 signed MADs per row (mp.hpp
     mont_reduce_p384); value folds through freduce (5 non-zero constants of
     2^384 mod p); final check with m+1's 12 non-zero limbs."""
-    return ec_point_mads_per_token(15, 4, 5, 20, wq, 384, 15 * 12, merged=False)
+    return ec_point_mads_per_token(15, 4, 5, 20, wq or p384_key_w(nkeys, P384_BUDGET), 384, 15 * 12, merged=False)
 
 
 def ed25519_point_mads_per_token(wa=20):
@@ -618,7 +629,7 @@ def run_configs(ctx, args, threads, rank, world, dist):
     present = set(kcls)
     work = {"rsa2048_modexp": rsa_modexp_mads_per_token(74, 2), "rsa3072_modexp": rsa_modexp_mads_per_token(112, 4),
             "rsa4096_modexp": rsa_modexp_mads_per_token(148, 4), "p256_point": p256_point_mads_per_token(),
-            "p384_point": p384_point_mads_per_token(), "ed25519_point": ed25519_point_mads_per_token()}
+            "p384_point": p384_point_mads_per_token(nkeys=3), "ed25519_point": ed25519_point_mads_per_token()}
     line = config_line(
         ctx, "mixed_10alg_32kid", "all 10 algs, 32 kids, 5% tampered, 10M stream on 8 GPUs in 262144-token chunks "
         "(configs[4]); one chunk per step per GPU", pool, algs, keyidx, good, 262144, max(1, args.steps // 2), 1,
@@ -691,8 +702,9 @@ def main():
         # process holds its own tables, so keep them at the 32 GiB default
         budget = min(budget, 32 << 30)
     ctx.set_table_budget(budget)
-    global P256_WQ
+    global P256_WQ, P384_BUDGET
     P256_WQ = p256_key_w(4, budget)
+    P384_BUDGET = budget
 
     # ---- ES256, P-256 JWKS with 4 kids (configs[1]): 1M unique OpenSSL-signed tokens
     kids = ["p256-a", "p256-b", "p256-c", "p256-d"]

@@ -65,14 +65,16 @@ constexpr int64_t ec_table_words(int cls, bool gen) { return ec_table_words_w(cl
 // windows do): the widest W whose tables for all `nkeys` keys of the curve fit
 // `budget` bytes.  P-256: W = 26 (10 windows, 26.8 GB per key: 20 additions
 // per token with the W = 26 generator), 24 (11 windows, 7.4 GB), 22 (12,
-// 2.0 GB), 20 (13, 545 MB); P-384: 20 (20 windows, 1.34 GB), 18 (22, 369 MB),
-// 16 (25, 105 MB); P-521: 20 (27, 2.26 GB), 18 (29, 608 MB), 16 (33, 173 MB).
-// The narrowest width is always allowed.  The budget applies to each curve.
+// 2.0 GB), 20 (13, 545 MB); P-384: 24 (17 windows, 18.3 GB), 20 (20 windows,
+// 1.34 GB), 18 (22, 369 MB), 16 (25, 105 MB); P-521: 20 (27, 2.26 GB), 18 (29,
+// 608 MB), 16 (33, 173 MB).  The narrowest width is always allowed.  The
+// budget applies to each curve.
 constexpr int EC_P256_WQ[4] = {26, 24, 22, 20};
-constexpr int EC_WIDE_WQ[3] = {20, 18, 16};
+constexpr int EC_P384_WQ[4] = {24, 20, 18, 16};
+constexpr int EC_P521_WQ[3] = {20, 18, 16};
 inline int ec_key_w(int cls, int nkeys, uint64_t budget) {
-  const int* t = cls == jgk::CLS_P256 ? EC_P256_WQ : EC_WIDE_WQ;
-  const int nt = cls == jgk::CLS_P256 ? 4 : 3;
+  const int* t = cls == jgk::CLS_P256 ? EC_P256_WQ : cls == jgk::CLS_P384 ? EC_P384_WQ : EC_P521_WQ;
+  const int nt = cls == jgk::CLS_P521 ? 3 : 4;
   for (int i = 0; i < nt; ++i)
     if ((uint64_t)nkeys * (uint64_t)ec_table_words_w(cls, t[i]) * 4u <= budget) return t[i];
   return t[nt - 1];

@@ -3,14 +3,16 @@
 #include "ecdsa_impl.hpp"
 
 void launch_ec_p384(const EcArgs& a, hipStream_t s, const Marker& mk) {
-  if (a.wq == 20) launch_chain<CurveP384W<20>>(a, s, mk);
+  if (a.wq == 24) launch_chain<CurveP384W<24>>(a, s, mk);
+  else if (a.wq == 20) launch_chain<CurveP384W<20>>(a, s, mk);
   else if (a.wq == 18) launch_chain<CurveP384W<18>>(a, s, mk);
   else launch_chain<CurveP384W<16>>(a, s, mk);
 }
 
 void launch_ec_keyprep_p384(int wq, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx,
                           int tn, hipStream_t s) {
-  if (wq == 20) keyprep_chain<CurveP384W<20>>(keys, blob, idx, n, tidx, tn, s);
+  if (wq == 24) keyprep_chain<CurveP384W<24>>(keys, blob, idx, n, tidx, tn, s);
+  else if (wq == 20) keyprep_chain<CurveP384W<20>>(keys, blob, idx, n, tidx, tn, s);
   else if (wq == 18) keyprep_chain<CurveP384W<18>>(keys, blob, idx, n, tidx, tn, s);
   else keyprep_chain<CurveP384W<16>>(keys, blob, idx, n, tidx, tn, s);
 }

@@ -28,6 +28,16 @@ def test_p256_width_tiers_match_the_library():
     assert bench.p256_key_w(1, 0) == 20
 
 
+def test_p384_width_tiers_match_the_library():
+    src = open(os.path.join(ROOT, "cap_amd", "csrc", "kernels", "ecdsa.hpp")).read()
+    m = re.search(r"EC_P384_WQ\[\d+\]\s*=\s*\{([^}]*)\}", src)
+    assert [int(x) for x in m.group(1).split(",")] == [24, 20, 18, 16]
+    assert bench.p384_key_w(1, 32 * GiB) == 24          # configs[3]: one P-384 key
+    assert bench.p384_key_w(3, 110 * GiB) == 24         # configs[4]: three, at the bench's budget
+    assert bench.p384_key_w(3, 32 * GiB) == 20
+    assert bench.p384_key_w(1, 0) == 16
+
+
 def test_point_mads_follow_the_window_count():
     # one fewer key window (one fewer mixed addition) per step of the tiers
     m = {w: bench.p256_point_mads_per_token(w) for w in (20, 22, 24, 26)}

@@ -203,7 +203,8 @@ def test_rsa_keys_above_4096_bits():
 @pytest.mark.parametrize("tier", ["w26", "w24", "w22", "w20"])
 def test_p256_key_table_widths(tier):
     """The P-256 key comb width follows the table budget (jg_set_table_budget,
-    ecdsa.hpp ec_key_w): W = 26 / 24 / 22 / 20 give the same verdicts as the oracle
+    ecdsa.hpp ec_key_w): W = 26 / 24 / 22 / 20 give the same verdicts (the w26
+    budget also gives the P-384 keys their W = 24 tier) as the oracle
     on every golden token against every key, and on a random ES256 batch."""
     from cap_amd import _lib
     from oracle import jws
