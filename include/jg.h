@@ -127,8 +127,8 @@ int jg_set_chunk(jg_ctx* ctx, size_t jobs);
  * of its EC keys (default 32 GiB, or CAPJWT_TABLE_BUDGET_GB).  The next
  * jg_keys_load gives each curve's keys the widest comb window whose tables for
  * all of them fit: P-256 W = 26 (26.8 GB per key, 20 point additions per
- * token), 24 (7.4 GB, 21), 22 (2.0 GB) or 20 (545 MB); P-384 / P-521 W = 20,
- * 18 or 16 -- HBM traded for
+ * token), 24 (7.4 GB, 21), 22 (2.0 GB) or 20 (545 MB); P-384 W = 24 (18.3 GB),
+ * 20, 18 or 16; P-521 W = 20, 18 or 16 -- HBM traded for
  * fewer additions, as the shared generator tables do.  The narrowest width is
  * always allowed.  Returns 0 or -1. */
 int jg_set_table_budget(jg_ctx* ctx, uint64_t bytes);
