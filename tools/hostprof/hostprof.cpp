@@ -1,7 +1,7 @@
 // hostprof -- CPU-only timing harness for the host half of Validator.ValidateBatch
 // (parse, kid routing, arena packing, payload JSON, claims, frees), the part
 // bench.py's `e2e` line found to be the ceiling.  It links the host sources with
-// jg_stub.cpp, a STAND-IN for libcapjwt.so that marks every job accepted: the
+// jg_timing_stub.cpp, a STAND-IN for libcapjwt.so that marks every job accepted: the
 // signatures are never checked here, so this binary measures host time only and
 // is never a verifier.  Not part of the product; not loaded by any test.
 //
