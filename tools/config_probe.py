@@ -1,5 +1,5 @@
 """One BASELINE config line alone, measured as bench.py measures it -- for
-kernel A/Bs through CAPJWT_LIB.  usage: python tools/config_probe.py ps512|eddsa_es384"""
+kernel A/Bs through CAPJWT_LIB.  usage: python tools/config_probe.py ps512|eddsa_es384|rs256_3072"""
 import json
 import os
 import sys
@@ -24,6 +24,13 @@ def main():
                                  [bench.ALG_IDS["PS512"]] * len(pool), [0] * len(pool), np.ones(len(pool), bool),
                                  131072, 10, 3, False, 1,
                                  kernels={"rsa4096_modexp": bench.rsa_modexp_mads_per_token(148, 4)})
+    elif which == "rs256_3072":        # the RSA-3K class alone (configs[4] holds RSA-3072 kids)
+        ctx.load_keys(bench.abi_keys(["rsa3072-a"]))
+        pool = bench.gen_tokens("RS256", 4096, bench.golden_keypaths(["rsa3072-a"]), th, "probe")
+        line = bench.config_line(ctx, "rs256_3072", "RS256 RSA-3072 probe", pool,
+                                 [bench.ALG_IDS["RS256"]] * len(pool), [0] * len(pool), np.ones(len(pool), bool),
+                                 1 << 19, 10, 3, False, 1,
+                                 kernels={"rsa3072_modexp": bench.rsa_modexp_mads_per_token(112, 4)})
     else:
         ctx.load_keys(bench.abi_keys(["ed-a", "p384-a"]))
         pe = bench.gen_tokens("EdDSA", 8192, bench.golden_keypaths(["ed-a"]), th, "probe")
