@@ -72,13 +72,40 @@ def p256_point_mads_per_token(wq=None):
     return ec_point_mads_per_token(10, 4, 0, 26, wq or P256_WQ, 256, 10 * 4, merged=True)
 
 
+# key comb-table width tiers, widest first (kernels/ecdsa.hpp EC_*_WQ, ed25519.hpp ED_WA)
+WIDTH_TIERS = {"p256": (26, 24, 22, 20), "p384": (24, 20, 18, 16), "ed25519": (20, 18, 16), "p521": (20, 18, 16)}
+_TAB = {"p256": (257, 80), "p384": (385, 128), "p521": (522, 160), "ed25519": (254, 128)}   # (bits + 1, entry bytes)
+
+
+def table_bytes(cls, w):
+    """Bytes of one key comb table: ceil((bits + 1) / W) windows x 2^(W-1) entries."""
+    bits, entry = _TAB[cls]
+    return -(-bits // w) * (1 << (w - 1)) * entry
+
+
+def key_widths(counts, budget):
+    """jg_runtime.cpp key_widths: one budget over all curves' key tables.  Every
+    key starts at its curve's narrowest width; then P-256, P-384, Ed25519,
+    P-521 in that order each take the widest tier that still fits."""
+    w = {c: t[-1] for c, t in WIDTH_TIERS.items()}
+    used = sum(counts.get(c, 0) * table_bytes(c, w[c]) for c in w)
+    for c in ("p256", "p384", "ed25519", "p521"):
+        n = counts.get(c, 0)
+        if not n:
+            continue
+        for t in WIDTH_TIERS[c]:
+            extra = n * (table_bytes(c, t) - table_bytes(c, w[c]))
+            if used + extra <= budget:
+                w[c] = t
+                used += extra
+                break
+    return w
+
+
 def p256_key_w(nkeys, budget):
-    """ecdsa.hpp ec_key_w for P-256: the widest key comb whose tables for
-    `nkeys` keys fit `budget` bytes (W = 26 / 24 / 22 / 20)."""
-    for w in (26, 24, 22, 20):
-        if nkeys * (-(-257 // w)) * (1 << (w - 1)) * 80 <= budget:
-            return w
-    return 20
+    """The P-256 key comb width of a load holding `nkeys` P-256 keys and
+    nothing else (W = 26 / 24 / 22 / 20)."""
+    return key_widths({"p256": nkeys}, budget)["p256"]
 
 
 def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged):
@@ -102,11 +129,9 @@ def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged)
 
 
 def p384_key_w(nkeys, budget):
-    """ecdsa.hpp ec_key_w for P-384 (W = 24 / 20 / 18 / 16)."""
-    for w in (24, 20, 18, 16):
-        if nkeys * (-(-385 // w)) * (1 << (w - 1)) * 128 <= budget:
-            return w
-    return 16
+    """The P-384 key comb width of a load holding `nkeys` P-384 keys and
+    nothing else (W = 24 / 20 / 18 / 16)."""
+    return key_widths({"p384": nkeys}, budget)["p384"]
 
 
 P384_BUDGET = 32 << 30    # main() sets the run's table budget
@@ -519,6 +544,40 @@ def tamper(pool, algs, keyidx, keys_meta, frac, seed=1):
     return pool, algs, keyidx, good
 
 
+RSA_ALGS = ("RS256", "RS384", "RS512", "PS256", "PS384", "PS512")
+
+
+def c5_pool(meta, total, threads, rank, ec_unique=True):
+    """configs[4]'s token list for one GPU: `total` tokens, every kid 1/32 of
+    them, in a fixed random order, 5 % tampered.  EC and Ed25519 tokens are all
+    unique (their comb-entry gathers would otherwise hit the Infinity Cache for
+    repeated tokens); RSA tokens cycle a per-kid pool of 1024 (512 for the
+    4096-bit kids), since the modexp reads only the token's own signature and
+    the key's modulus -- a repeat costs exactly what a new token costs.
+    ec_unique=False is round 2's layout (1024 per kid for every alg)."""
+    per = -(-total // len(meta))
+    pool, algs, keyidx = [], [], []
+    for ki, (kid, alg, pem, _, _) in enumerate(meta):
+        n = (512 if alg in ("RS512", "PS512") else 1024) if (alg in RSA_ALGS or not ec_unique) else per
+        toks = gen_tokens(alg, n, [pem], threads, f"c4r{rank}", kid_base=ki)
+        pool += [toks[i % n] for i in range(per)]
+        algs += [ALG_IDS[alg]] * per
+        keyidx += [ki] * per
+    order = np.random.default_rng(1).permutation(len(pool))[:total]
+    pool = [pool[i] for i in order]
+    algs = [algs[i] for i in order]
+    keyidx = [keyidx[i] for i in order]
+    return tamper(pool, algs, keyidx, meta, 0.05)
+
+
+def c5_pool_note(ec_unique):
+    if ec_unique:
+        return ("every EC / Ed25519 token unique over the 1,250,000-token share (the resident chunk is its first "
+                "262144); RSA tokens cycle 1024 (512 for 4096-bit kids) per kid: the modexp has no data-dependent "
+                "gathers, so repeats cost the same")
+    return "1024 (512) unique tokens per kid replicated (round-2 layout)"
+
+
 def roofline_line(kernel_ms, per_gpu, kernels):
     """{kernel: roofline} for each (key, mads-per-token | ('hbm', bytes-per-token))."""
     out = {}
@@ -589,33 +648,41 @@ def run_configs(ctx, args, threads, rank, world, dist):
         max(1, args.steps // 2), 1, dist, world,
         kernels={"rsa4096_modexp": rsa_modexp_mads_per_token(148, 4),
                  "rsa4096_prep": ("hbm", prep_bytes_per_token(939, 132))})
-    # configs[3]: EdDSA Ed25519 + ES384 P-384 mixed, 1M tokens per GPU
+    # configs[3]: EdDSA Ed25519 + ES384 P-384 mixed, 1M tokens per GPU, every
+    # token unique (a replicated pool lets repeated comb-entry gathers hit the
+    # 256 MiB Infinity Cache; `pool_ab` measures the old 16384-token pool beside it)
     ctx.load_keys(abi_keys(["ed-a", "p384-a"]))
-    pe = gen_tokens("EdDSA", 8192, golden_keypaths(["ed-a"]), threads, f"c3r{rank}")
-    p3 = gen_tokens("ES384", 8192, golden_keypaths(["p384-a"]), threads, f"c3r{rank}", kid_base=1)
+    c4w = ctx.table_widths()                  # [Ed25519 key, P-384 key]
+    c4n = args.c4_pool // 2
+    pe = gen_tokens("EdDSA", c4n, golden_keypaths(["ed-a"]), threads, f"c3r{rank}")
+    p3 = gen_tokens("ES384", c4n, golden_keypaths(["p384-a"]), threads, f"c3r{rank}", kid_base=1)
     pool = [t for pair in zip(pe, p3) for t in pair]
     algs = [ALG_IDS["EdDSA"], ALG_IDS["ES384"]] * len(pe)
-    out["eddsa_es384_mixed"] = config_line(
+    c4_kernels = {"p384_point": p384_point_mads_per_token(c4w[1]), "ed25519_point": ed25519_point_mads_per_token(c4w[0]),
+                  "p384_prep": ("hbm", prep_bytes_per_token(384, 49)),
+                  "ed25519_prep": ("hbm", prep_bytes_per_token(342, 16))}
+    line = config_line(
         ctx, "eddsa_es384_mixed", "EdDSA Ed25519 + ES384 P-384 50/50 mixed batch, 1M tokens per GPU (configs[3])",
         pool, algs, [0, 1] * len(pe), np.ones(len(pool), bool), 1 << 20, max(1, args.steps // 2), 1, dist, world,
-        kernels={"p384_point": p384_point_mads_per_token(), "ed25519_point": ed25519_point_mads_per_token(),
-                 "p384_prep": ("hbm", prep_bytes_per_token(384, 49)),
-                 "ed25519_prep": ("hbm", prep_bytes_per_token(342, 16))})
+        kernels=c4_kernels)
+    if not args.no_ab and len(pool) > 16384:
+        sub = 16384
+        ab = config_line(ctx, "eddsa_es384_mixed_ab", "pool A/B", pool[:sub], algs[:sub], [0, 1] * (sub // 2),
+                         np.ones(sub, bool), 1 << 20, max(1, args.steps // 2), 1, dist, world, kernels=c4_kernels)
+        line["pool_ab"] = {"replicated_pool": sub, "value": ab["value"], "kernel_ms": ab["kernel_ms"],
+                           "roofline": ab.get("roofline"),
+                           "note": "same 1M-token batch from a 16384-token pool replicated 64x (round-2 layout); "
+                                   "`value` above uses unique tokens"}
+    out["eddsa_es384_mixed"] = line
+    del pool, pe, p3
     # configs[4]: all 10 algs, 32 kids, ~5 % tampered; the 10M stream in 256k-token chunks (one chunk per step)
     meta = bench_keys()
+    # one table budget over every curve (jg_set_table_budget): enough for the
+    # 32 kids' widest tiers (P-256 W = 26, P-384 24, P-521 20, Ed25519 20: 171 GB)
+    ctx.set_table_budget(int(args.c5_table_budget_gb * (1 << 30)))
     ctx.load_keys([m[3] for m in meta])
-    pool, algs, keyidx = [], [], []
-    for ki, (kid, alg, pem, _, _) in enumerate(meta):
-        n = 512 if alg in ("RS512", "PS512") else 1024
-        toks = gen_tokens(alg, n, [pem], threads, f"c4r{rank}", kid_base=ki)
-        pool += toks
-        algs += [ALG_IDS[alg]] * n
-        keyidx += [ki] * n
-    order = np.random.default_rng(1).permutation(len(pool))
-    pool = [pool[i] for i in order]
-    algs = [algs[i] for i in order]
-    keyidx = [keyidx[i] for i in order]
-    pool, algs, keyidx, good = tamper(pool, algs, keyidx, meta, 0.05)
+    c5w = ctx.table_widths()
+    pool, algs, keyidx, good = c5_pool(meta, 10_000_000 // 8, threads, rank, args.c5_unique)
     # kernel class of each kid's key (ecdsa/rsa/ed25519 classes of the runtime)
     def key_class(jwk):
         if jwk["kty"] == "RSA":
@@ -627,15 +694,22 @@ def run_configs(ctx, args, threads, rank, world, dist):
         return "ed25519"
     kcls = [key_class(m[4]) for m in meta]
     present = set(kcls)
+    wof = {c: next(w for w, k in zip(c5w, kcls) if k == c) for c in ("p256", "p384", "ed25519") if c in kcls}
     work = {"rsa2048_modexp": rsa_modexp_mads_per_token(74, 2), "rsa3072_modexp": rsa_modexp_mads_per_token(112, 4),
-            "rsa4096_modexp": rsa_modexp_mads_per_token(148, 4), "p256_point": p256_point_mads_per_token(),
-            "p384_point": p384_point_mads_per_token(nkeys=3), "ed25519_point": ed25519_point_mads_per_token()}
+            "rsa4096_modexp": rsa_modexp_mads_per_token(148, 4), "p256_point": p256_point_mads_per_token(wof.get("p256")),
+            "p384_point": p384_point_mads_per_token(wof.get("p384")),
+            "ed25519_point": ed25519_point_mads_per_token(wof.get("ed25519", 20))}
+    chunk = 262144
     line = config_line(
         ctx, "mixed_10alg_32kid", "all 10 algs, 32 kids, 5% tampered, 10M stream on 8 GPUs in 262144-token chunks "
-        "(configs[4]); one chunk per step per GPU", pool, algs, keyidx, good, 262144, max(1, args.steps // 2), 1,
-        dist, world, kernels={k: v for k, v in work.items() if k.split("_")[0] in present}, class_of_key=kcls)
+        "(configs[4]); one chunk per step per GPU", pool[:chunk], algs[:chunk], keyidx[:chunk], good[:chunk], chunk,
+        max(1, args.steps // 2), 1, dist, world, kernels={k: v for k, v in work.items() if k.split("_")[0] in present},
+        class_of_key=kcls)
+    line["pool"] = c5_pool_note(args.c5_unique)
+    line["table_budget_GiB"] = args.c5_table_budget_gb
+    line["key_comb_w"] = {m[0]: w for m, w in zip(meta, c5w) if w}
     # the same workload as a real stream: this GPU's 1/8 share of the 10M
-    # tokens (1,310,720) through jg_verify_batch from pinned host memory (H2D,
+    # tokens (1,250,000) through jg_verify_batch from pinned host memory (H2D,
     # plan, kernels, verdicts back), chunks overlapping
     share = 10_000_000 // 8
     arena, toks = pack(pool, algs, keyidx, share)
@@ -668,6 +742,14 @@ def main():
     ap.add_argument("--no-ab", action="store_true", help="skip the replicated-pool A/B line")
     ap.add_argument("--no-rs256", action="store_true")
     ap.add_argument("--no-configs", action="store_true")
+    ap.add_argument("--configs-only", action="store_true",
+                    help="only the `configs` lines (profiling runs of configs[2..4]); not a bench line")
+    ap.add_argument("--c4-pool", type=int, default=1 << 20,
+                    help="unique tokens of configs[3] (EdDSA + ES384; default: the whole 1M batch)")
+    ap.add_argument("--c5-table-budget-gb", type=float, default=160.0,
+                    help="configs[4] table budget over all curves (160 GiB: every kid at its widest tier)")
+    ap.add_argument("--c5-legacy-pool", dest="c5_unique", action="store_false",
+                    help="configs[4] from 1024 unique tokens per kid (round-2 layout)")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -702,13 +784,23 @@ def main():
         # process holds its own tables, so keep them at the 32 GiB default
         budget = min(budget, 32 << 30)
     ctx.set_table_budget(budget)
-    global P256_WQ, P384_BUDGET
-    P256_WQ = p256_key_w(4, budget)
+    global P384_BUDGET
     P384_BUDGET = budget
+    if args.configs_only:
+        res = {"configs_only": True, "configs": run_configs(ctx, args, host_threads, rank, world, dist)}
+        ctx.close()
+        if rank == 0:
+            print(json.dumps(res))
+        if dist:
+            import torch.distributed as td
+            td.destroy_process_group()
+        return
 
     # ---- ES256, P-256 JWKS with 4 kids (configs[1]): 1M unique OpenSSL-signed tokens
     kids = ["p256-a", "p256-b", "p256-c", "p256-d"]
     ctx.load_keys(abi_keys(kids))
+    global P256_WQ
+    P256_WQ = min(ctx.table_widths())         # the key comb width the library gave the 4 kids
     npool = min(args.pool or args.tokens, args.tokens)
     pool = gen_tokens("ES256", npool, golden_keypaths(kids), host_threads, f"r{rank}")
     arena, toks = pack(pool, [ALG_IDS["ES256"]] * npool, np.arange(npool) % len(kids), args.tokens)

@@ -2,4 +2,11 @@
 jwt.KeySet / jwt.Validator path.  The product is libcapjwt.so
 (include/jg.h); this package holds its Python binding and the Python mirror of
 cap's jwt API."""
-from . import _lib  # noqa: F401
+import os as _os
+
+# tools/sanitize/run.sh: load an ASan/UBSan build of the host extension
+# (_capjwt_host) from this directory instead of the regular one
+if _os.environ.get("CAPJWT_HOST_EXT_DIR"):
+    __path__.insert(0, _os.environ["CAPJWT_HOST_EXT_DIR"])
+
+from . import _lib  # noqa: F401,E402

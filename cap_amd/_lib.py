@@ -21,7 +21,8 @@ CURVE_IDS = {"P-256": 1, "P-384": 2, "P-521": 3}
 EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_last_error",
            "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_enqueue", "jg_batch_sync",
            "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
-           "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_table_budget"]
+           "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_table_budget", "jg_keys_wait_tables",
+           "jg_keys_table_widths", "jg_debug_fail_alloc"]
 
 
 class JgKey(ctypes.Structure):
@@ -76,6 +77,9 @@ def lib():
         L.jg_set_chunk.argtypes = [vp, sz]
         L.jg_set_table_budget.argtypes = [vp, ctypes.c_uint64]
         L.jg_hash_batch.argtypes = [vp, vp, sz, vp, sz, vp]
+        L.jg_keys_wait_tables.argtypes = [vp]
+        L.jg_keys_table_widths.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        L.jg_debug_fail_alloc.argtypes = [vp, ctypes.c_int]
         L.jg_version.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -150,7 +154,9 @@ class Context:
     def error(self):
         return (lib().jg_last_error(self.h) or b"").decode()
 
-    def load_keys(self, keys):
+    def load_keys(self, keys, wait_tables=True):
+        """jg_keys_load; with wait_tables (default) also jg_keys_wait_tables, so
+        every key runs at its budgeted comb width when this returns."""
         arr = (JgKey * max(1, len(keys)))()
         keep = []
         for i, k in enumerate(keys):
@@ -168,6 +174,27 @@ class Context:
         rc = lib().jg_keys_load(self.h, arr, len(keys))
         if rc != 0:
             raise JgError(f"jg_keys_load rc={rc}: {self.error()}")
+        if wait_tables:
+            self.wait_tables()
+
+    def wait_tables(self):
+        """jg_keys_wait_tables: True when every table reached its budgeted width."""
+        rc = lib().jg_keys_wait_tables(self.h)
+        if rc < 0:
+            raise JgError(f"jg_keys_wait_tables rc={rc}")
+        return rc == 0
+
+    def table_widths(self):
+        """jg_keys_table_widths: comb width per loaded key (0 = none)."""
+        n = lib().jg_keys_table_widths(self.h, None, 0)
+        arr = (ctypes.c_int * max(1, n))()
+        lib().jg_keys_table_widths(self.h, arr, n)
+        return list(arr[:n])
+
+    def debug_fail_alloc(self, n):
+        """jg_debug_fail_alloc: the n-th device allocation of later key loads fails (0 = off)."""
+        if lib().jg_debug_fail_alloc(self.h, int(n)) != 0:
+            raise JgError("jg_debug_fail_alloc failed")
 
     def verify(self, arena: Arena):
         n = len(arena.toks)
@@ -183,7 +210,7 @@ class Context:
             raise JgError("jg_set_chunk: chunk must be >= 64 jobs")
 
     def set_table_budget(self, nbytes):
-        """jg_set_table_budget: HBM for P-256 key comb tables (applies at the next load_keys)."""
+        """jg_set_table_budget: HBM for all key comb tables (applies at the next load_keys)."""
         if lib().jg_set_table_budget(self.h, int(nbytes)) != 0:
             raise JgError("jg_set_table_budget failed")
 

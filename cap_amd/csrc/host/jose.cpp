@@ -419,14 +419,19 @@ bool parse_pkix_public_key(std::string_view der, PublicKey* out, std::string* er
   std::string_view spki, alg, bits;
   if (!d.read(0x30, &spki) || !d.empty()) return bad("x509: malformed public key");
   Der s = Der::of(spki);
-  if (!s.read(0x30, &alg) || !s.read(0x03, &bits) || !s.empty()) return bad("x509: malformed public key");
+  // encoding/asn1 (ParsePKIXPublicKey) and cryptobyte (ParseCertificate) both
+  // ignore elements after the ones they read, in the SubjectPublicKeyInfo and
+  // in its AlgorithmIdentifier ("We allow extra bytes at the end of the
+  // SEQUENCE because adding elements to the end has been used in X.509")
+  if (!s.read(0x30, &alg) || !s.read(0x03, &bits)) return bad("x509: malformed public key");
   Der a = Der::of(alg);
   std::string_view oid, params;
   if (!a.read(0x06, &oid)) return bad("x509: malformed public key algorithm identifier");
   const bool has_params = !a.empty();
   const unsigned ptag = has_params ? *a.p : 0;
-  if (has_params && (!a.skip_any() || !a.empty())) return bad("x509: malformed public key algorithm identifier");
-  if (has_params) params = std::string_view((const char*)alg.data() + 2 + oid.size(), alg.size() - 2 - oid.size());
+  const unsigned char* pstart = a.p;
+  if (has_params && !a.skip_any()) return bad("x509: malformed public key algorithm identifier");
+  if (has_params) params = std::string_view((const char*)pstart, (size_t)(a.p - pstart));   // the first element only
   if (bits.empty() || bits[0] != 0) return bad("x509: malformed public key");   // unused bits must be 0
   const std::string_view key = bits.substr(1);
   if (oid == kOidRSA) {

@@ -33,6 +33,7 @@
 #include <deque>
 #include <functional>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
@@ -71,7 +72,17 @@ bool pipe_trace() {
   static const bool on = std::getenv("CAPJWT_PIPE_TRACE") != nullptr;
   return on;
 }
-hipEvent_t g_trace_ref = nullptr;     // first chunk's H2D start (trace only)
+hipEvent_t g_trace_ref = nullptr;
+
+// CAPJWT_RELEASE_GTABLES=1: free a device's fixed-base tables when the last
+// context using them is destroyed (default: kept for the process, ~31 GB per device)
+bool release_gtables() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_RELEASE_GTABLES");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}     // first chunk's H2D start (trace only)
 
 double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -201,6 +212,80 @@ struct HostKey {
   int nlimbs = 0;                 // RSA: limbs of the key's modexp layout
 };
 
+// Device memory with shared ownership.  Comb tables are shared by key content
+// between key loads (a JWKS refresh that keeps a key keeps its table: no copy,
+// no rebuild), and a load's key blob is shared by its later width upgrades.
+// Freed when the last holder lets go; hipFree waits for the device's streams,
+// so a generation still referenced by queued kernels is never freed under them.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int dev = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (!p) return;
+    int cur = 0;
+    const bool had = hipGetDevice(&cur) == hipSuccess;
+    (void)hipSetDevice(dev);
+    (void)hipFree(p);
+    if (had) (void)hipSetDevice(cur);
+  }
+  template <class T>
+  T* as() const { return (T*)p; }
+};
+using DevBufP = std::shared_ptr<DevBuf>;
+
+// hipMalloc into a DevBuf.  `fail` (jg_debug_fail_alloc): a countdown of
+// allocations after which one fails as if the device were out of memory.
+DevBufP dev_alloc(int dev, size_t bytes, std::atomic<int>* fail = nullptr) {
+  if (fail) {
+    int f = fail->load();
+    while (f > 0 && !fail->compare_exchange_weak(f, f - 1)) {}
+    if (f == 1) throw std::runtime_error("hipMalloc: out of memory (jg_debug_fail_alloc)");
+  }
+  auto b = std::make_shared<DevBuf>();
+  b->dev = dev;
+  b->bytes = std::max<size_t>(bytes, 16);
+  HIPCHK(hipSetDevice(dev));
+  HIPCHK(hipMalloc(&b->p, b->bytes));
+  return b;
+}
+
+// One device's copy of a key table generation: the DevKey records, the key
+// blob (moduli, R^2, Montgomery coordinates), the class table of k_plan_fill,
+// and the comb tables the records point at.  Immutable once published; a
+// width upgrade publishes a new generation sharing the blob.
+struct DevGen {
+  DevBufP dkeys, blob, dcls;
+  std::vector<DevBufP> tabs;      // comb tables the keys' `tab` addresses point into
+  std::vector<DevKey> mirror;     // host copy of dkeys (after key prep: validity, tables)
+  std::vector<uint8_t> kw;        // per key: comb width of its table (0 = none)
+  DevKey* keys() const { return dkeys ? dkeys->as<DevKey>() : nullptr; }
+  uint32_t* keyblob() const { return blob ? blob->as<uint32_t>() : nullptr; }
+  const uint8_t* cls() const { return dcls ? dcls->as<uint8_t>() : nullptr; }
+};
+using DevGenP = std::shared_ptr<const DevGen>;
+
+// The key table as every verification sees it: immutable, published whole.
+// Submissions capture the state current at submit time and run entirely
+// against it, so a key load never drains or blocks queued work; the previous
+// state lives until the last chunk using it has completed.
+struct KeyState {
+  std::vector<HostKey> keys;
+  std::vector<uint8_t> cls_tab;          // [key * NALG + alg] -> kernel class of the job
+  std::vector<int32_t> cls_keys[NCLS];   // keys of each class, in index order
+  int rsa4k_limbs = 148;                 // largest RSA-4K+ layout among the valid keys
+  int rsa4k_layouts = 1;                 // RSA-4K+ layouts present (bit i: rsa4k_layout_limbs(i))
+  uint64_t epoch = 0;                    // changes with the key list (dispatch plans are per epoch)
+  std::string content;                   // the load's key bytes + budget: an identical reload is a no-op
+  std::vector<std::string> tab_id;       // per key: content id of its comb table ("" = none)
+  std::vector<uint8_t> want_w;           // per key: the comb width the table budget gives it
+  std::vector<DevGenP> dev;              // per device slot
+};
+using KeyStateP = std::shared_ptr<const KeyState>;
+
 // Fixed-base tables of the curve generators / Ed25519 base point depend only
 // on (device, curve): every jg_ctx of the process shares one copy per device,
 // built on first use and kept for the life of the process (they are constants
@@ -272,6 +357,7 @@ struct Plan {
   int64_t pss_tokens = 0;         // PSS scratch tokens: the RSA classes' ranges back to back
   int64_t pss_off[NCLS] = {};
   int64_t nkeys = 0;              // key table size at plan time (prep midstate slots)
+  std::vector<int64_t> kstart;    // per key: first padded slot of its run (runs of one class are contiguous)
 };
 
 struct PlanScratch {              // reused across chunks
@@ -313,6 +399,7 @@ struct Slot {
   uint64_t reserved_epoch = ~0ull; // key table they were sized against
   bool inflight = false;
   std::shared_ptr<Ticket> ticket;
+  KeyStateP ks;                    // key state of the chunk in flight (kept alive until it completes)
   uint8_t* out = nullptr;
   size_t n = 0;
 };
@@ -324,7 +411,7 @@ struct Item {                     // one device's share of a submission
   const jg_tok* toks = nullptr;   // the caller's array, [lo, hi)
   size_t lo = 0, hi = 0;
   uint8_t* out = nullptr;         // the caller's verdicts (index space of toks)
-  uint64_t epoch = 0;
+  KeyStateP ks;                   // the key table current at submit time
   const uint8_t* dev_arena = nullptr;   // device view of a page-locked arena (kernels read it over PCIe)
   size_t chunk = 0, nchunks = 0;
   std::vector<size_t> cuts;       // chunk boundaries (chunk_cuts)
@@ -332,20 +419,18 @@ struct Item {                     // one device's share of a submission
 
 struct Device {
   int id = 0;
-  int ec_wq[NCLS] = {};           // comb width of the loaded EC key tables per curve
-  int ed_wa = 16;                 // comb width of the loaded Ed25519 key tables
-  Lane lane0;                     // resident batches, key loads, hashing
+  Lane lane0;                     // resident batches, hashing
+  hipStream_t kstream = nullptr;  // key loads (staging, narrow tables): beside the verify streams
+  hipStream_t ustream = nullptr;  // background width upgrades of key comb tables
   uint32_t* gtab[NCLS] = {};
   uint32_t* btab = nullptr;
   std::shared_ptr<SharedTable> tab_ref[NCLS];   // keeps gtab / btab alive
-  // comb tables of the current key blob by key content (class, coordinates):
-  // a reload (JWKS refresh) copies the tables of keys it already had instead
-  // of rebuilding them (D2D copy ~0.2 ms vs ~80 ms per P-256 key)
-  std::unordered_map<std::string, std::pair<uint64_t, uint64_t>> tab_cache;   // id -> (word offset, words)
-  DevKey* dkeys = nullptr;
-  uint32_t* dblob = nullptr;
-  int32_t* didx = nullptr;
-  std::mutex mu;                  // device state + lane0 + slots
+  // comb tables by (key content id, width), shared by every generation that
+  // uses them: a reload (JWKS refresh) reuses the tables of keys it already had
+  // (no copy, no build) and builds only new keys' tables
+  std::mutex tmu;
+  std::map<std::string, std::weak_ptr<DevBuf>> tcache;
+  std::mutex mu;                  // lane0 + slots
   // streaming pipeline: H2D copies of every chunk back to back on one copy
   // stream (full link bandwidth, no sharing between slots), each slot's
   // kernels on its own stream once its copy event fires
@@ -359,7 +444,6 @@ struct Device {
   std::deque<Item> q;
   bool stop = false, busy = false;
   PlanScratch plan;               // worker scratch of the host plan
-  uint8_t* dcls = nullptr;        // device copy of the context's class table (k_plan_fill)
 };
 
 }  // namespace
@@ -372,7 +456,9 @@ struct jg_batch {
   Bufs* b = nullptr;
   Plan plan;
   size_t arena_len = 0;
-  uint64_t epoch = 0;
+  size_t dslot = 0;
+  uint64_t epoch = 0;             // key-list epoch the plan was built for
+  KeyStateP ks_run;               // key state of the last run (alive while its kernels may run)
   bool timing = true;
   // timing marks of the most recent run: events are created once and
   // re-recorded every run (no per-run event churn)
@@ -392,16 +478,32 @@ struct jg_ticket {
 
 struct jg_ctx {
   std::vector<std::unique_ptr<Device>> devs;
-  std::vector<HostKey> keys;
-  std::vector<uint8_t> cls_tab;   // [key * NALG + alg] -> kernel class of the job
-  std::vector<int32_t> cls_keys[NCLS];   // keys of each class, in index order
-  int rsa4k_limbs = 148;          // largest RSA-4K+ layout among the valid keys
-  int rsa4k_layouts = 1;          // RSA-4K+ layouts present (bit i: rsa4k_layout_limbs(i))
-  bool failed = false;            // the last key load failed half-way: nothing verifies
   std::atomic<size_t> chunk{chunk_jobs()};   // jobs per pipeline chunk
-  std::atomic<uint64_t> table_budget{default_table_budget()};   // HBM for P-256 key comb tables
-  uint64_t epoch = 0;
-  std::shared_mutex key_mu;       // key table: exclusive in jg_keys_load, shared by submitters
+  std::atomic<uint64_t> table_budget{default_table_budget()};   // HBM for key comb tables, all curves
+  std::atomic<int> fail_alloc{0};            // jg_debug_fail_alloc countdown
+  // the published key table (KeyState): swapped whole under ks_mu
+  std::mutex ks_mu;
+  KeyStateP ks;
+  KeyStateP state() {
+    std::lock_guard<std::mutex> g(ks_mu);
+    return ks;
+  }
+  void publish(KeyStateP n) {
+    KeyStateP old;
+    {
+      std::lock_guard<std::mutex> g(ks_mu);
+      old = std::move(ks);
+      ks = std::move(n);
+    }
+    // `old` (and, if nothing else holds it, its device memory) dies here, outside the lock
+  }
+  std::mutex load_mu;             // serialises key loads and upgrade publications
+  // background widening of comb tables (narrow table first, wide one swapped in)
+  std::thread upgrader;
+  std::mutex up_mu;
+  std::condition_variable up_cv, up_idle_cv;
+  bool up_stop = false, up_pending = false, up_busy = false;
+  std::string up_warn;            // a width upgrade that did not fit free HBM
   std::mutex err_mu;
   std::string err;
   void set_err(const std::string& s) {
@@ -446,34 +548,34 @@ int alg_family(int alg) {         // 1 RSA, 2 EC, 3 Ed, 0 none
 }
 
 // kernel class of a job (key_idx already range-checked)
-inline int classify(const jg_ctx* ctx, const jg_tok& t) {
-  return t.alg < NALG ? ctx->cls_tab[(size_t)t.key_idx * NALG + t.alg] : CLS_REJECT;
+inline int classify(const KeyState& K, const jg_tok& t) {
+  return t.alg < NALG ? K.cls_tab[(size_t)t.key_idx * NALG + t.alg] : CLS_REJECT;
 }
 
-void rebuild_class_tables(jg_ctx* ctx) {
-  const size_t nk = ctx->keys.size();
-  ctx->cls_tab.assign(nk * NALG, (uint8_t)CLS_REJECT);
-  for (auto& v : ctx->cls_keys) v.clear();
-  ctx->rsa4k_limbs = rsa4k_layout_limbs(0);
-  ctx->rsa4k_layouts = 1;
+void rebuild_class_tables(KeyState& K) {
+  const size_t nk = K.keys.size();
+  K.cls_tab.assign(nk * NALG, (uint8_t)CLS_REJECT);
+  for (auto& v : K.cls_keys) v.clear();
+  K.rsa4k_limbs = rsa4k_layout_limbs(0);
+  K.rsa4k_layouts = 1;
   for (size_t k = 0; k < nk; ++k) {
-    const HostKey& hk = ctx->keys[k];
-    if (hk.valid && hk.cls != CLS_REJECT) ctx->cls_keys[hk.cls].push_back((int32_t)k);
+    const HostKey& hk = K.keys[k];
+    if (hk.valid && hk.cls != CLS_REJECT) K.cls_keys[hk.cls].push_back((int32_t)k);
     if (hk.valid && hk.cls == CLS_RSA4K) {
-      ctx->rsa4k_limbs = std::max(ctx->rsa4k_limbs, hk.nlimbs);
+      K.rsa4k_limbs = std::max(K.rsa4k_limbs, hk.nlimbs);
       for (int i = 0; i < RSA4K_NLAYOUT; ++i)
-        if (hk.nlimbs == rsa4k_layout_limbs(i)) ctx->rsa4k_layouts |= 1 << i;
+        if (hk.nlimbs == rsa4k_layout_limbs(i)) K.rsa4k_layouts |= 1 << i;
     }
     for (int a = 0; a < NALG; ++a)
-      if (hk.valid && alg_family(a) == hk.kind) ctx->cls_tab[k * NALG + a] = (uint8_t)hk.cls;
+      if (hk.valid && alg_family(a) == hk.kind) K.cls_tab[k * NALG + a] = (uint8_t)hk.cls;
   }
 }
 
 // Reject a job list that names a key outside the table or a byte span outside
 // the arena (the prep kernel reads the device copy at those offsets).
-bool check_jobs(const jg_ctx* ctx, size_t arena_len, const jg_tok* toks, size_t ntok, std::string* err,
+bool check_jobs(const KeyState& K, size_t arena_len, const jg_tok* toks, size_t ntok, std::string* err,
                 size_t base = 0) {
-  const size_t nk = ctx->keys.size();
+  const size_t nk = K.keys.size();
   for (size_t i = 0; i < ntok; ++i) {
     const jg_tok& t = toks[i];
     if (t.key_idx >= nk) {
@@ -524,12 +626,12 @@ const uint8_t* device_view(const void* p) {
 // per-job part of plan_layout (one pass; `visit(i)` runs on every job too):
 // bucket counts into X.total, (class, alg) pairs seen into *seen (bit c*16+alg)
 template <class Visit>
-void plan_count(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, PlanScratch& X, bool keep_cls, uint64_t* seen,
+void plan_count(const KeyState& K, const jg_tok* toks, size_t ntok, PlanScratch& X, bool keep_cls, uint64_t* seen,
                 Visit&& visit) {
-  const size_t nk = ctx->keys.size(), NB = nk + 1, RB = nk;
+  const size_t nk = K.keys.size(), NB = nk + 1, RB = nk;
   X.total.assign(NB, 0);
   if (keep_cls) X.tcls.resize(ntok);
-  const uint8_t* ctab = ctx->cls_tab.data();
+  const uint8_t* ctab = K.cls_tab.data();
   int64_t* tot = X.total.data();
   uint64_t lo = 0, hi = 0;
   for (size_t i = 0; i < ntok; ++i) {
@@ -547,16 +649,16 @@ void plan_count(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, PlanScratch&
   seen[1] = hi;
 }
 
-void plan_layout(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, Plan& P, PlanScratch& X, bool keep_cls,
+void plan_layout(const KeyState& K, const jg_tok* toks, size_t ntok, Plan& P, PlanScratch& X, bool keep_cls,
                  const uint64_t* seen_in = nullptr) {
-  const size_t nk = ctx->keys.size();
+  const size_t nk = K.keys.size();
   const size_t NB = nk + 1, RB = nk;
   uint64_t seen[2];
   if (seen_in) {
     seen[0] = seen_in[0];
     seen[1] = seen_in[1];
   } else {
-    plan_count(ctx, toks, ntok, X, keep_cls, seen, [](size_t) {});
+    plan_count(K, toks, ntok, X, keep_cls, seen, [](size_t) {});
   }
   X.start.assign(NB, 0);
   const int64_t* tot = X.total.data();
@@ -577,21 +679,22 @@ void plan_layout(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, Plan& P, Pl
       X.start[RB] = pos;
       pos += (tot[RB] + WAVE - 1) / WAVE * WAVE;
     } else {
-      for (int32_t k : ctx->cls_keys[cc]) {
+      for (int32_t k : K.cls_keys[cc]) {
         X.start[(size_t)k] = pos;
         pos += (tot[(size_t)k] + WAVE - 1) / WAVE * WAVE;
       }
     }
     P.ranges[cc].end = pos;
   }
+  P.kstart.assign(X.start.begin(), X.start.begin() + (int64_t)nk);
   P.npad = pos > 0 ? pos : WAVE;
   P.ntok = (int64_t)ntok;
   P.sig_rows = 1;
   P.scratch_rows = 1;
   P.pss_tokens = 0;
-  P.rsa4k_limbs = ctx->rsa4k_limbs;
-  P.rsa4k_layouts = ctx->rsa4k_layouts;
-  P.nkeys = (int64_t)ctx->keys.size();
+  P.rsa4k_limbs = K.rsa4k_limbs;
+  P.rsa4k_layouts = K.rsa4k_layouts;
+  P.nkeys = (int64_t)K.keys.size();
   for (int c = 1; c < NCLS; ++c) {
     if (P.ranges[c].end <= P.ranges[c].begin) continue;
     P.sig_rows = std::max(P.sig_rows, cls_rows_sig(c, P.rsa4k_limbs));
@@ -614,9 +717,9 @@ inline std::pair<int64_t, int64_t> pad_range(const PlanScratch& X, size_t b, con
 }
 
 // Host placement (resident batches): JobDev array + perm in padded order.
-void plan_fill_host(const jg_ctx* ctx, const jg_tok* toks, size_t ntok, const Plan& P, PlanScratch& X, JobDev* jobs,
+void plan_fill_host(const KeyState& K, const jg_tok* toks, size_t ntok, const Plan& P, PlanScratch& X, JobDev* jobs,
                     int32_t* perm) {
-  const size_t nk = ctx->keys.size(), NB = nk + 1, RB = nk;
+  const size_t nk = K.keys.size(), NB = nk + 1, RB = nk;
   for (size_t b = 0; b < NB; ++b) {
     const auto r = pad_range(X, b, P, RB);
     const JobDev pad{0, 0, 0, job_pack(b == RB ? 0u : (uint32_t)b, JOB_PAD, 0)};
@@ -740,7 +843,29 @@ bool pipeline_fanout() {
   return on;
 }
 
-void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks, bool fanout = true) {
+// Runs of consecutive keys of class c (the plan's key order) whose comb tables
+// have one width: fn(begin, end, w) per run, over padded slots.  All of a
+// curve's keys share one width except while a background upgrade is widening
+// some of them (one launch chain per width then).
+template <class Fn>
+void width_runs(const KeyState& K, const DevGen& G, const Plan& P, int c, Fn&& fn) {
+  const ClassRange r = P.ranges[c];
+  int64_t beg = r.begin;
+  int w = -1;
+  for (int32_t k : K.cls_keys[c]) {
+    const int kw = G.kw[(size_t)k];
+    if (w >= 0 && kw != w) {
+      const int64_t kb = P.kstart[(size_t)k];
+      if (kb > beg) fn(beg, kb, w);
+      beg = kb;
+    }
+    w = kw;
+  }
+  if (w >= 0 && r.end > beg) fn(beg, r.end, w);
+}
+
+void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, const Plan& P, jg_batch* marks,
+              bool fanout = true) {
   const bool timed = marks && marks->timing;
   int nact = 0;
   for (int c = 1; c < NCLS; ++c) nact += P.ranges[c].end > P.ranges[c].begin;
@@ -752,8 +877,8 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks, bool 
   PrepArgs pa{};
   pa.arena = (const uint8_t*)B->arena.p;
   pa.jobs = (const JobDev*)B->jobs.p;
-  pa.keys = d->dkeys;
-  pa.keyblob = d->dblob;
+  pa.keys = G.keys();
+  pa.keyblob = G.keyblob();
   pa.sigw = (uint32_t*)B->sigw.p;
   pa.dig = (uint32_t*)B->dig.p;
   pa.status = (uint8_t*)B->status.p;
@@ -804,9 +929,13 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks, bool 
       ea.gtab = d->gtab[c];
       ea.exc_list = (int32_t*)B->exc.p + r.begin;
       ea.exc_count = (uint32_t*)B->exc_cnt.p + c;
-      ea.npad = np; ea.begin = r.begin; ea.end = r.end;
-      ea.wq = d->ec_wq[c];
-      launch_ec(c, ea, s, marker(marks, c));
+      ea.npad = np;
+      ea.exc_reset = 1;
+      width_runs(K, G, P, c, [&](int64_t b, int64_t e, int w) {
+        ea.begin = b; ea.end = e; ea.wq = w;
+        launch_ec(c, ea, s, marker(marks, c));
+        ea.exc_reset = 0;          // later runs of the class append to its exception list
+      });
     } else {
       if (!d->btab) throw std::runtime_error("Ed25519 base table missing");
       EdArgs ea{};
@@ -815,9 +944,11 @@ void run_plan(Device* d, Lane* L, Bufs* B, const Plan& P, jg_batch* marks, bool 
       ea.verdict_pad = (uint8_t*)B->vpad.p;
       ea.xyz = rows;
       ea.btab = d->btab;
-      ea.npad = np; ea.begin = r.begin; ea.end = r.end;
-      ea.wa = d->ed_wa;
-      launch_ed(ea, s, marker(marks, c));
+      ea.npad = np;
+      width_runs(K, G, P, c, [&](int64_t b, int64_t e, int w) {
+        ea.begin = b; ea.end = e; ea.wa = w;
+        launch_ed(ea, s, marker(marks, c));
+      });
     }
     if (conc) {
       HIPCHK(hipEventRecord(L->ev_done[c], s));
@@ -861,6 +992,7 @@ void finish_slot(Slot& S) {
   S.inflight = false;
   auto t = std::move(S.ticket);
   S.ticket.reset();
+  S.ks.reset();                    // may free a replaced key state (after this chunk completed)
   t->done_chunks(1);
 }
 
@@ -871,16 +1003,16 @@ void finish_slot(Slot& S) {
 // and class mix never reallocate in the stream (a hipFree synchronises the
 // device, a hipHostMalloc page-locks): ~1 GB of device scratch per slot at
 // C = 64 k for a context with RSA-4K keys, far less for ES256 alone.
-void reserve_slot(const jg_ctx* ctx, Slot& S, size_t C, size_t nbuckets, double bytes_per_job) {
+void reserve_slot(const KeyState& K, Slot& S, size_t C, size_t nbuckets, double bytes_per_job) {
   const PlanBlock L(nbuckets, C);
   S.h_meta.get(L.bytes);
   S.h_verdict.get(C);
   int sig_rows = 1, scratch_rows = 1;
   bool rsa = false;
   for (int c = 1; c < NCLS; ++c) {
-    if (ctx->cls_keys[c].empty()) continue;
-    sig_rows = std::max(sig_rows, cls_rows_sig(c, ctx->rsa4k_limbs));
-    scratch_rows = std::max(scratch_rows, cls_rows_scratch(c, ctx->rsa4k_limbs));
+    if (K.cls_keys[c].empty()) continue;
+    sig_rows = std::max(sig_rows, cls_rows_sig(c, K.rsa4k_limbs));
+    scratch_rows = std::max(scratch_rows, cls_rows_scratch(c, K.rsa4k_limbs));
     rsa = rsa || c <= CLS_RSA4K;
   }
   const size_t npad = C + (size_t)WAVE * nbuckets;
@@ -897,28 +1029,30 @@ void reserve_slot(const jg_ctx* ctx, Slot& S, size_t C, size_t nbuckets, double 
   B->rows.get(sizeof(uint32_t) * (size_t)scratch_rows * npad);
   if (rsa) B->pss.get(C * 2048);
   B->exc.get(sizeof(int32_t) * npad);
-  B->mid.get(sizeof(uint32_t) * PREP_MID_WORDS * std::max<size_t>(ctx->keys.size(), 1));
+  B->mid.get(sizeof(uint32_t) * PREP_MID_WORDS * std::max<size_t>(K.keys.size(), 1));
   S.reserved = C;
-  S.reserved_epoch = ctx->epoch;
+  S.reserved_epoch = K.epoch;
 }
 
-void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok* toks, size_t n, uint8_t* out) {
+void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_tok* toks, size_t n, uint8_t* out) {
   const auto t_start = std::chrono::steady_clock::now();
-  if (S.reserved != it.chunk || S.reserved_epoch != ctx->epoch) {
+  const KeyState& K = *it.ks;
+  const DevGen& G = *K.dev[dslot];
+  if (S.reserved != it.chunk || S.reserved_epoch != K.epoch) {
     double bpj = 0;
     for (size_t i = 0; i < std::min<size_t>(n, 256); ++i) bpj += (double)(tok_end(toks[i]) - toks[i].off);
-    reserve_slot(ctx, S, std::max(it.chunk, n), ctx->keys.size() + 1, n ? bpj / (double)std::min<size_t>(n, 256) : 512.0);
+    reserve_slot(K, S, std::max(it.chunk, n), K.keys.size() + 1, n ? bpj / (double)std::min<size_t>(n, 256) : 512.0);
   }
   // One pass over the caller's jobs: the arena span they use, the bucket
   // counts of the plan, and their copy into the pinned plan block.  The span
   // is DMAed straight from a pinned caller arena when it is compact, else
   // repacked job by job into pinned staging.
-  const size_t NB = ctx->keys.size() + 1;
+  const size_t NB = K.keys.size() + 1;
   const PlanBlock L(NB, n);
   uint8_t* hb = (uint8_t*)S.h_meta.get(L.bytes);
   jg_tok* ht = (jg_tok*)(hb + L.toks_off);
   uint64_t amin = UINT64_MAX, amax = 0, need = 0, seen[2];
-  plan_count(ctx, toks, n, d->plan, false, seen, [&](size_t i) {
+  plan_count(K, toks, n, d->plan, false, seen, [&](size_t i) {
     const jg_tok& t = toks[i];
     const uint64_t e = tok_end(t);
     amin = std::min<uint64_t>(amin, t.off);
@@ -960,7 +1094,7 @@ void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok
     src = h;
   }
   Plan P;
-  plan_layout(ctx, ht, n, P, d->plan, false, seen);
+  plan_layout(K, ht, n, P, d->plan, false, seen);
   uint64_t* cur = (uint64_t*)(hb + L.cur_off);
   int64_t* pad = (int64_t*)(hb + L.pad_off);
   for (size_t k = 0; k < NB; ++k) {
@@ -998,7 +1132,7 @@ void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok
     fa.toks = (const jg_tok*)(hbd + L.toks_off);
     fa.n = (int64_t)n;
     fa.base = dbase;
-    fa.cls_tab = d->dcls;
+    fa.cls_tab = G.cls();
     fa.nkeys = (int32_t)(NB - 1);
     fa.cursor = (unsigned long long*)(dm + L.cur_off);
     fa.pad = (const int64_t*)(dm + L.pad_off);
@@ -1006,7 +1140,7 @@ void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok
     fa.perm = (int32_t*)S.bufs.perm.p;
     launch_plan_fill(fa, s);
   }
-  run_plan(d, &LN, &S.bufs, P, nullptr, pipeline_fanout());
+  run_plan(d, K, G, &LN, &S.bufs, P, nullptr, pipeline_fanout());
   if (tr) HIPCHK(hipEventRecord(S.tr_c, s));
   S.h_verdict.get(std::max<size_t>(n, 1));
   launch_copy(S.bufs.verdict.p, S.h_verdict.dp, n, s);
@@ -1014,18 +1148,17 @@ void enqueue_chunk(jg_ctx* ctx, Device* d, Slot& S, const Item& it, const jg_tok
   HIPCHK(hipEventRecord(S.done, s));
   if (tr) S.host_ms[2] = ms_since(t_enq);
   S.ticket = it.t;
+  S.ks = it.ks;
   S.out = out;
   S.n = n;
   S.inflight = true;
 }
 
-void process_item(jg_ctx* ctx, Device* d, Item& it) {
+void process_item(Device* d, size_t dslot, Item& it) {
   size_t enq = 0;
   try {
     std::lock_guard<std::mutex> g(d->mu);
     HIPCHK(hipSetDevice(d->id));
-    if (ctx->failed || ctx->epoch != it.epoch)
-      throw std::runtime_error("key table reloaded (or its load failed) while the batch was queued");
     if (pipe_trace()) {
       if (!g_trace_ref) HIPCHK(hipEventCreate(&g_trace_ref));
       HIPCHK(hipEventRecord(g_trace_ref, d->copy));
@@ -1033,7 +1166,7 @@ void process_item(jg_ctx* ctx, Device* d, Item& it) {
     for (size_t c = 0; c + 1 < it.cuts.size(); ++c) {
       const size_t lo = it.cuts[c], hi = it.cuts[c + 1];
       std::string bad;
-      if (!check_jobs(ctx, it.arena_len, it.toks + lo, hi - lo, &bad, lo)) {
+      if (!check_jobs(*it.ks, it.arena_len, it.toks + lo, hi - lo, &bad, lo)) {
         it.t->fail(-1, bad);
         break;
       }
@@ -1042,7 +1175,7 @@ void process_item(jg_ctx* ctx, Device* d, Item& it) {
       const auto tw = std::chrono::steady_clock::now();
       finish_slot(S);                 // the slot's previous chunk (NSLOT chunks ago)
       const double wait_ms = pipe_trace() ? ms_since(tw) : 0.0;
-      enqueue_chunk(ctx, d, S, it, it.toks + lo, hi - lo, it.out + lo);
+      enqueue_chunk(d, dslot, S, it, it.toks + lo, hi - lo, it.out + lo);
       S.host_ms[0] = wait_ms;
       S.chunk_no = (int)enq;
       ++enq;
@@ -1054,7 +1187,7 @@ void process_item(jg_ctx* ctx, Device* d, Item& it) {
   }
 }
 
-void worker_loop(jg_ctx* ctx, Device* d) {
+void worker_loop(Device* d, size_t dslot) {
   (void)hipSetDevice(d->id);
   std::unique_lock<std::mutex> lk(d->qmu);
   while (true) {
@@ -1063,7 +1196,7 @@ void worker_loop(jg_ctx* ctx, Device* d) {
       d->q.pop_front();
       d->busy = true;
       lk.unlock();
-      process_item(ctx, d, it);
+      process_item(d, dslot, it);
       lk.lock();
       continue;
     }
@@ -1092,30 +1225,15 @@ void worker_loop(jg_ctx* ctx, Device* d) {
   }
 }
 
-void wait_idle(Device* d) {
-  std::unique_lock<std::mutex> lk(d->qmu);
-  d->idle_cv.wait(lk, [&] { return d->q.empty() && !d->busy; });
-}
 
 // ---------------------------------------------------------------- keys
 struct StagedKeys {
-  int ec_wq[NCLS] = {};             // comb width of this load's EC key tables per curve (ecdsa.hpp ec_key_w)
-  int ed_wa = 16;                  // comb width of this load's Ed25519 key tables (ed25519.hpp ed_key_w)
   std::vector<DevKey> dk;
-  std::vector<uint32_t> blob;      // host-initialised part of the device key blob
-  uint64_t tab_words = 0;          // device-only tail: comb tables (built on the GPU)
-  std::vector<int32_t> rsa_idx, ec_idx[NCLS], ed_idx, tab_keys;
+  std::vector<uint32_t> blob;       // host-initialised key blob (moduli, coordinates)
+  std::vector<int32_t> rsa_idx, ec_idx[NCLS], ed_idx;
   std::vector<std::string> tab_id;  // per key: content id of its comb table ("" = none)
+  std::vector<uint8_t> want_w;      // per key: comb width the table budget gives it (0 = none)
 };
-
-// comb tables never exist on the host: offsets are relative to the device-only
-// tail until build_keys rebases them past the host part
-uint64_t tab_alloc(StagedKeys& S, int key, uint64_t words) {
-  const uint64_t off = S.tab_words;
-  S.tab_words += (words + 3) & ~uint64_t(3);
-  S.tab_keys.push_back(key);
-  return off;
-}
 
 uint64_t blob_alloc(std::vector<uint32_t>& blob, size_t words) {
   const uint64_t off = (blob.size() + 3) & ~size_t(3);          // 16-byte aligned
@@ -1123,25 +1241,82 @@ uint64_t blob_alloc(std::vector<uint32_t>& blob, size_t words) {
   return off;
 }
 
-// Host part of a key load.  Touches no context state (the caller commits `hk`
-// only after every device has loaded the new table); `warn` collects
+// width tiers of a table class, widest first (ecdsa.hpp EC_*_WQ, ed25519.hpp ED_WA)
+std::vector<int> width_tiers(int c) {
+  switch (c) {
+    case CLS_P256: return {EC_P256_WQ, EC_P256_WQ + 4};
+    case CLS_P384: return {EC_P384_WQ, EC_P384_WQ + 4};
+    case CLS_P521: return {EC_P521_WQ, EC_P521_WQ + 3};
+    case CLS_ED25519: return {ED_WA, ED_WA + 3};
+    default: return {};
+  }
+}
+int narrow_w(int c) { return width_tiers(c).back(); }
+uint64_t table_bytes(int c, int w) {
+  return 4u * (uint64_t)(c == CLS_ED25519 ? ed_table_words_w(w) : ec_table_words_w(c, w));
+}
+
+// Key comb widths per class from ONE budget over every curve's key tables:
+// each key starts at its class's narrowest width (always allowed, whatever the
+// budget); then P-256, P-384, Ed25519 and P-521 in that order (ES256 first:
+// BASELINE's headline) each take the widest tier whose extra bytes, for all
+// of the class's keys, still fit what is left.
+void key_widths(const int count[NCLS], uint64_t budget, int w[NCLS]) {
+  uint64_t used = 0;
+  for (int c = 0; c < NCLS; ++c) {
+    w[c] = 0;
+    if (c >= CLS_P256) {
+      w[c] = narrow_w(c);
+      used += (uint64_t)count[c] * table_bytes(c, w[c]);
+    }
+  }
+  for (int c : {(int)CLS_P256, (int)CLS_P384, (int)CLS_ED25519, (int)CLS_P521}) {
+    if (!count[c]) continue;
+    for (int t : width_tiers(c)) {
+      const uint64_t extra = (uint64_t)count[c] * (table_bytes(c, t) - table_bytes(c, narrow_w(c)));
+      if (used + extra <= budget) {
+        w[c] = t;
+        used += extra;
+        break;
+      }
+    }
+  }
+}
+
+// The bytes of a key list (plus the budget, which decides table widths): a
+// load whose content equals the current table's is a no-op.
+std::string key_content(const jg_key* keys, int nkeys, uint64_t budget) {
+  std::string s;
+  auto put = [&](const void* p, size_t n) { s.append((const char*)p, n); };
+  put(&budget, sizeof budget);
+  for (int i = 0; i < nkeys; ++i) {
+    const jg_key& k = keys[i];
+    const uint8_t has = (k.n ? 1 : 0) | (k.x ? 2 : 0) | (k.y ? 4 : 0);
+    put(&k.kind, 4); put(&k.curve, 4); put(&k.n_len, 4); put(&k.e, 8); put(&k.coord_len, 4); put(&has, 1);
+    if (k.n && k.n_len > 0) put(k.n, (size_t)k.n_len);
+    const size_t cl = k.coord_len > 0 ? (size_t)k.coord_len : 0;
+    if (k.x) put(k.x, cl);
+    if (k.y && k.kind == JG_KEY_EC) put(k.y, cl);
+  }
+  return s;
+}
+
+// Host part of a key load.  Touches no context state; `warn` collects
 // informational messages for jg_last_error.
 void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys& S, std::vector<HostKey>& hks,
                 std::string* warn) {
   hks.assign((size_t)nkeys, HostKey{});
   S.dk.assign((size_t)nkeys, DevKey{});
   S.tab_id.assign((size_t)nkeys, std::string());
-  // EC key tables: per curve, the widest comb whose tables for every key of
-  // that curve in the load fit the context's table budget (fewer additions)
-  int nec[4] = {};
-  for (int i = 0; i < nkeys; ++i)
-    if (keys[i].kind == JG_KEY_EC && keys[i].curve >= JG_P256 && keys[i].curve <= JG_P521) ++nec[keys[i].curve];
-  S.ec_wq[CLS_P256] = ec_key_w(CLS_P256, nec[JG_P256], table_budget);
-  S.ec_wq[CLS_P384] = ec_key_w(CLS_P384, nec[JG_P384], table_budget);
-  S.ec_wq[CLS_P521] = ec_key_w(CLS_P521, nec[JG_P521], table_budget);
-  int ned = 0;
-  for (int i = 0; i < nkeys; ++i) ned += keys[i].kind == JG_KEY_ED25519;
-  S.ed_wa = ed_key_w(ned, table_budget);
+  S.want_w.assign((size_t)nkeys, 0);
+  int count[NCLS] = {};
+  for (int i = 0; i < nkeys; ++i) {
+    const jg_key& k = keys[i];
+    if (k.kind == JG_KEY_EC && k.curve >= JG_P256 && k.curve <= JG_P521) ++count[CLS_P256 + k.curve - JG_P256];
+    if (k.kind == JG_KEY_ED25519) ++count[CLS_ED25519];
+  }
+  int wq[NCLS];
+  key_widths(count, table_budget, wq);
   for (int i = 0; i < nkeys; ++i) {
     const jg_key& k = keys[i];
     HostKey& hk = hks[i];
@@ -1188,7 +1363,6 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
       K.cls = cls;
       K.kbytes = cb;
       K.aux_off = blob_alloc(S.blob, 2 * L);
-      K.tab_off = tab_alloc(S, i, (uint64_t)ec_table_words_w(cls, S.ec_wq[cls]));
       const size_t cl = k.coord_len > 0 ? (size_t)k.coord_len : 0;
       // crypto/ecdsa pointFromAffine: coordinates must fit the curve's bit size
       bool ok = k.x && k.y && cl > 0 && bitlen_be(k.x, cl) <= (cls == CLS_P521 ? 521 : cb * 8) &&
@@ -1197,6 +1371,7 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
         be_to_limbs(k.x, cl, S.blob.data() + K.aux_off, L);
         be_to_limbs(k.y, cl, S.blob.data() + K.aux_off + L, L);
         S.tab_id[i] = std::string("E") + (char)cls + std::string((const char*)S.blob.data() + 4 * K.aux_off, 8 * L);
+        S.want_w[i] = (uint8_t)wq[cls];
       }
       K.valid = ok;
       if (ok) S.ec_idx[cls].push_back(i);
@@ -1206,12 +1381,12 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
       K.cls = CLS_ED25519;
       K.kbytes = 32;
       K.aux_off = blob_alloc(S.blob, 8 + 2 * ED_L);
-      K.tab_off = tab_alloc(S, i, (uint64_t)ed_table_words_w(S.ed_wa));
       // crypto/ed25519.Verify panics on len(pub) != 32; go-jose never hands it one
       const bool ok = k.x && k.coord_len == 32;
       if (ok) {
         std::memcpy(S.blob.data() + K.aux_off, k.x, 32);
         S.tab_id[i] = std::string("D") + std::string((const char*)k.x, 32);
+        S.want_w[i] = (uint8_t)wq[CLS_ED25519];
       }
       K.valid = ok;
       if (ok) S.ed_idx.push_back(i);
@@ -1224,19 +1399,16 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
   for (int c = CLS_P256; c <= CLS_P521; ++c)
     if ((int)S.ec_idx[c].size() > ec_max_keys(c))
       throw std::runtime_error(std::string(cls_name(c)) + ": at most " + std::to_string(ec_max_keys(c)) +
-                               " keys per table (comb tables are " +
-                               std::to_string(ec_table_words_w(c, S.ec_wq[c]) * 4 >> 20) + " MiB each)");
+                               " keys per table");
   if ((int)S.ed_idx.size() > ED_MAX_KEYS)
-    throw std::runtime_error("Ed25519: at most " + std::to_string(ED_MAX_KEYS) + " keys per table (comb tables are " +
-                             std::to_string(ed_table_words_w(S.ed_wa) * 4 >> 20) + " MiB each)");
+    throw std::runtime_error("Ed25519: at most " + std::to_string(ED_MAX_KEYS) + " keys per table");
   blob_alloc(S.blob, 0);                                      // align the host part
-  for (int k : S.tab_keys) S.dk[k].tab_off += S.blob.size();
 }
 
-// the process-wide table of (device, class), built on this device's stream
-// and complete before any other context can see it
+// the process-wide table of (device, class), built on stream s and complete
+// before any other context can see it
 template <class Build>
-std::shared_ptr<SharedTable> shared_table(Device* d, int cls, size_t bytes, Build&& build) {
+std::shared_ptr<SharedTable> shared_table(Device* d, int cls, size_t bytes, hipStream_t s, Build&& build) {
   std::lock_guard<std::mutex> g(g_tab_mu);
   const auto key = std::make_pair(d->id, cls);
   if (auto t = g_tabs[key]) return t;
@@ -1245,7 +1417,7 @@ std::shared_ptr<SharedTable> shared_table(Device* d, int cls, size_t bytes, Buil
   try {
     build(t->p);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(d->lane0.stream));
+    HIPCHK(hipStreamSynchronize(s));
   } catch (...) {
     (void)hipFree(t->p);          // a failed build is not cached
     throw;
@@ -1256,106 +1428,319 @@ std::shared_ptr<SharedTable> shared_table(Device* d, int cls, size_t bytes, Buil
 
 void ensure_tables(Device* d, const StagedKeys& S) {
   HIPCHK(hipSetDevice(d->id));
+  const hipStream_t s = d->kstream;
   for (int c = CLS_P256; c <= CLS_P521; ++c) {
     if (S.ec_idx[c].empty() || d->gtab[c]) continue;
-    d->tab_ref[c] = shared_table(d, c, sizeof(uint32_t) * ec_table_words(c, true),
-                                 [&](uint32_t* t) { launch_ec_gtable(c, t, d->lane0.stream); });
+    d->tab_ref[c] = shared_table(d, c, sizeof(uint32_t) * ec_table_words(c, true), s,
+                                 [&](uint32_t* t) { launch_ec_gtable(c, t, s); });
     d->gtab[c] = d->tab_ref[c]->p;
   }
   if (!S.ed_idx.empty() && !d->btab) {
-    d->tab_ref[CLS_ED25519] = shared_table(d, CLS_ED25519, sizeof(uint32_t) * ed_table_words(true),
-                                           [&](uint32_t* t) { launch_ed_btable(t, d->lane0.stream); });
+    d->tab_ref[CLS_ED25519] = shared_table(d, CLS_ED25519, sizeof(uint32_t) * ed_table_words(true), s,
+                                           [&](uint32_t* t) { launch_ed_btable(t, s); });
     d->btab = d->tab_ref[CLS_ED25519]->p;
   }
 }
 
-void load_keys_device(Device* d, const StagedKeys& S) {
-  HIPCHK(hipSetDevice(d->id));
-  for (int c = 0; c < NCLS; ++c) d->ec_wq[c] = S.ec_wq[c];
-  d->ed_wa = S.ed_wa;
-  hipStream_t s = d->lane0.stream;
-  d->lane0.sync();
-  if (d->copy) (void)hipStreamSynchronize(d->copy);
-  for (auto& ln : d->lanes) ln.sync();
-  if (d->dkeys) (void)hipFree(d->dkeys);
-  if (d->didx) (void)hipFree(d->didx);
-  d->dkeys = nullptr; d->didx = nullptr;
-  uint32_t* old_blob = d->dblob;                   // kept until its reusable tables are copied
-  auto old_cache = std::move(d->tab_cache);
-  d->tab_cache.clear();
-  d->dblob = nullptr;
-  try {
-    const size_t nk = std::max<size_t>(S.dk.size(), 1);
-    HIPCHK(hipMalloc(&d->dkeys, sizeof(DevKey) * nk));
-    HIPCHK(hipMalloc(&d->dblob, sizeof(uint32_t) * std::max<uint64_t>(S.blob.size() + S.tab_words, 4)));
-    if (!S.dk.empty()) HIPCHK(hipMemcpyAsync(d->dkeys, S.dk.data(), sizeof(DevKey) * S.dk.size(), hipMemcpyHostToDevice, s));
-    if (!S.blob.empty())
-      HIPCHK(hipMemcpyAsync(d->dblob, S.blob.data(), sizeof(uint32_t) * S.blob.size(), hipMemcpyHostToDevice, s));
-    // per table class: keys to stage (all) and keys whose tables must be built
-    // (the rest are copied from the previous blob, same key content)
-    auto split = [&](const std::vector<int32_t>& keys, uint64_t words, std::vector<int32_t>& build) {
-      for (int32_t i : keys) {
-        const std::string& id = S.tab_id[(size_t)i];
-        const uint64_t off = S.dk[(size_t)i].tab_off;
-        auto it = id.empty() ? old_cache.end() : old_cache.find(id);
-        if (old_blob && it != old_cache.end() && it->second.second == words) {
-          HIPCHK(hipMemcpyAsync(d->dblob + off, old_blob + it->second.first, sizeof(uint32_t) * words,
-                                hipMemcpyDeviceToDevice, s));
-        } else {
-          build.push_back(i);
-        }
-        if (!id.empty()) d->tab_cache[id] = {off, words};
-      }
-    };
-    std::vector<int32_t> build_ec[NCLS], build_ed;
-    for (int c = CLS_P256; c <= CLS_P521; ++c)
-      split(S.ec_idx[c], (uint64_t)ec_table_words_w(c, S.ec_wq[c]), build_ec[c]);
-    split(S.ed_idx, (uint64_t)ed_table_words_w(S.ed_wa), build_ed);
-    // one index array: rsa | p256 | p384 | p521 | ed | builds p256 | p384 | p521 | ed
-    std::vector<int32_t> idx;
-    std::vector<size_t> at;
-    auto push = [&](const std::vector<int32_t>& v) { at.push_back(idx.size()); idx.insert(idx.end(), v.begin(), v.end()); };
-    push(S.rsa_idx);
-    for (int c = CLS_P256; c <= CLS_P521; ++c) push(S.ec_idx[c]);
-    push(S.ed_idx);
-    for (int c = CLS_P256; c <= CLS_P521; ++c) push(build_ec[c]);
-    push(build_ed);
-    HIPCHK(hipMalloc(&d->didx, sizeof(int32_t) * std::max<size_t>(idx.size(), 1)));
-    if (!idx.empty()) HIPCHK(hipMemcpyAsync(d->didx, idx.data(), sizeof(int32_t) * idx.size(), hipMemcpyHostToDevice, s));
-    ensure_tables(d, S);
-    if (!S.dk.empty()) launch_rsa_keyprep(d->dkeys, d->dblob, (int)S.dk.size(), s);
-    for (int c = CLS_P256; c <= CLS_P521; ++c)
-      launch_ec_keyprep(c, S.ec_wq[c], d->dkeys, d->dblob, d->didx + at[1 + c - CLS_P256], (int)S.ec_idx[c].size(),
-                        d->didx + at[5 + c - CLS_P256], (int)build_ec[c].size(), s);
-    launch_ed_keyprep(S.ed_wa, d->dkeys, d->dblob, d->didx + at[4], (int)S.ed_idx.size(), d->didx + at[8],
-                      (int)build_ed.size(), s);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s));
-  } catch (...) {
-    (void)hipStreamSynchronize(s);
-    if (old_blob) (void)hipFree(old_blob);
-    d->tab_cache.clear();
-    throw;
+// HBM kept free for chunk scratch when key tables are sized against free memory
+constexpr uint64_t HBM_RESERVE = uint64_t(2) << 30;
+
+uint64_t free_hbm(int dev) {
+  size_t fr = 0, tot = 0;
+  HIPCHK(hipSetDevice(dev));
+  HIPCHK(hipMemGetInfo(&fr, &tot));
+  return fr;
+}
+
+// Launch the comb-table builds of keys (index list on the device at `didx`,
+// grouped by class and width) on stream s.
+void build_tables(const std::map<std::pair<int, int>, std::vector<int32_t>>& groups, DevKey* keys, uint32_t* blob,
+                  int32_t* didx, hipStream_t s) {
+  std::vector<int32_t> all;
+  std::vector<std::pair<size_t, size_t>> span;
+  for (const auto& g : groups) {
+    span.emplace_back(all.size(), g.second.size());
+    all.insert(all.end(), g.second.begin(), g.second.end());
   }
-  if (old_blob) (void)hipFree(old_blob);
+  if (all.empty()) return;
+  HIPCHK(hipMemcpyAsync(didx, all.data(), sizeof(int32_t) * all.size(), hipMemcpyHostToDevice, s));
+  size_t i = 0;
+  for (const auto& g : groups) {
+    const int c = g.first.first, w = g.first.second;
+    int32_t* ix = didx + span[i].first;
+    const int n = (int)span[i].second;
+    if (c == CLS_ED25519) launch_ed_keytables(w, keys, blob, ix, n, s);
+    else launch_ec_keytables(c, w, keys, blob, ix, n, s);
+    ++i;
+  }
+  HIPCHK(hipGetLastError());
+  // the index list is host memory that dies with the caller: wait here
+  HIPCHK(hipStreamSynchronize(s));
+}
+
+// Stage a key load on one device, beside running verifications (its own
+// stream; no drain): upload, key prep (R^2 / n', on-curve checks, Ed25519
+// decoding), then a comb table per valid EC / Ed25519 key -- the table of the
+// same key content and width when this device already has one (a JWKS
+// refresh), else a new one.  With `narrow_first` a key that has no table at
+// its budgeted width gets the widest table it already has, or a new table at
+// the narrowest width (P-256: 545 MB, ~0.1 s), so it verifies at once; the
+// upgrader builds the wide table later (jg_keys_wait_tables).  Throws on any
+// failure; the device state and the published key table are then untouched.
+std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S, bool narrow_first) {
+  HIPCHK(hipSetDevice(d->id));
+  const hipStream_t s = d->kstream;
+  const size_t nk = S.dk.size();
+  auto g = std::make_shared<DevGen>();
+  g->mirror = S.dk;
+  g->kw.assign(nk, 0);
+  ensure_tables(d, S);
+  g->dkeys = dev_alloc(d->id, sizeof(DevKey) * std::max<size_t>(nk, 1), &ctx->fail_alloc);
+  g->blob = dev_alloc(d->id, sizeof(uint32_t) * std::max<size_t>(S.blob.size(), 4), &ctx->fail_alloc);
+  // key prep index lists: p256 | p384 | p521 | ed
+  std::vector<int32_t> idx;
+  size_t at[4];
+  for (int c = CLS_P256; c <= CLS_P521; ++c) {
+    at[c - CLS_P256] = idx.size();
+    idx.insert(idx.end(), S.ec_idx[c].begin(), S.ec_idx[c].end());
+  }
+  at[3] = idx.size();
+  idx.insert(idx.end(), S.ed_idx.begin(), S.ed_idx.end());
+  DevBufP didx = dev_alloc(d->id, sizeof(int32_t) * std::max<size_t>(idx.size() + nk, 1), &ctx->fail_alloc);
+  int32_t* di = didx->as<int32_t>();
+  DevKey* dk = g->keys();
+  uint32_t* blob = g->keyblob();
+  if (nk) HIPCHK(hipMemcpyAsync(dk, S.dk.data(), sizeof(DevKey) * nk, hipMemcpyHostToDevice, s));
+  if (!S.blob.empty()) HIPCHK(hipMemcpyAsync(blob, S.blob.data(), sizeof(uint32_t) * S.blob.size(), hipMemcpyHostToDevice, s));
+  if (!idx.empty()) HIPCHK(hipMemcpyAsync(di, idx.data(), sizeof(int32_t) * idx.size(), hipMemcpyHostToDevice, s));
+  if (nk) launch_rsa_keyprep(dk, blob, (int)nk, s);
+  for (int c = CLS_P256; c <= CLS_P521; ++c)
+    launch_ec_keyprep(c, dk, blob, di + at[c - CLS_P256], (int)S.ec_idx[c].size(), s);
+  launch_ed_keyprep(dk, blob, di + at[3], (int)S.ed_idx.size(), s);
+  HIPCHK(hipGetLastError());
+  if (nk) HIPCHK(hipMemcpyAsync(g->mirror.data(), dk, sizeof(DevKey) * nk, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+
+  // comb tables of the keys that prepped valid
+  struct Req { int cls, w; DevBufP buf; std::string id; };
+  std::map<std::string, Req> fresh;               // new tables by id + width
+  std::vector<std::pair<size_t, std::string>> use;   // key -> id + width of its table
+  {
+    std::lock_guard<std::mutex> tg(d->tmu);
+    auto cached = [&](const std::string& id, int w) -> DevBufP {
+      auto it = d->tcache.find(id + (char)w);
+      return it == d->tcache.end() ? nullptr : it->second.lock();
+    };
+    for (size_t i = 0; i < nk; ++i) {
+      if (S.tab_id[i].empty() || !g->mirror[i].valid) continue;
+      const int c = S.dk[i].cls, wt = S.want_w[i];
+      int w = wt;
+      DevBufP t = cached(S.tab_id[i], wt);
+      if (!t && narrow_first)
+        for (int ww : width_tiers(c))
+          if (ww < wt && (t = cached(S.tab_id[i], ww))) { w = ww; break; }
+      if (t) {
+        g->mirror[i].tab = (uint64_t)(uintptr_t)t->p;
+        g->mirror[i].tab_w = w;
+        g->kw[i] = (uint8_t)w;
+        g->tabs.push_back(std::move(t));
+        continue;
+      }
+      if (narrow_first) w = narrow_w(c);
+      const std::string key = S.tab_id[i] + (char)w;
+      fresh.emplace(key, Req{c, w, nullptr, S.tab_id[i]});
+      use.emplace_back(i, key);
+    }
+  }
+  // size the new tables against free HBM (the previous generation stays live
+  // until this one is published): narrow widths until they fit
+  auto need = [&] {
+    uint64_t b = 0;
+    for (const auto& f : fresh) b += table_bytes(f.second.cls, f.second.w);
+    return b;
+  };
+  const uint64_t fr = free_hbm(d->id);
+  while (!fresh.empty() && need() + HBM_RESERVE > fr) {
+    Req* widest = nullptr;
+    for (auto& f : fresh)
+      if (f.second.w > narrow_w(f.second.cls) && (!widest || table_bytes(f.second.cls, f.second.w) > table_bytes(widest->cls, widest->w)))
+        widest = &f.second;
+    if (!widest) {
+      throw std::runtime_error("key comb tables need " + std::to_string(need() >> 20) + " MiB but only " +
+                               std::to_string(fr >> 20) + " MiB of HBM is free on device " + std::to_string(d->id) +
+                               " (the previous key table stays in force)");
+    }
+    const auto tiers = width_tiers(widest->cls);
+    for (size_t t = 0; t + 1 < tiers.size(); ++t)
+      if (tiers[t] == widest->w) { widest->w = tiers[t + 1]; break; }
+  }
+  std::map<std::pair<int, int>, std::vector<int32_t>> groups;
+  std::map<std::string, int32_t> first;          // one build per distinct (id, width)
+  for (auto& f : fresh) f.second.buf = dev_alloc(d->id, table_bytes(f.second.cls, f.second.w), &ctx->fail_alloc);
+  for (const auto& u : use) {
+    const Req& r = fresh.at(u.second);
+    const size_t i = u.first;
+    g->mirror[i].tab = (uint64_t)(uintptr_t)r.buf->p;
+    g->mirror[i].tab_w = r.w;
+    g->kw[i] = (uint8_t)r.w;
+    g->tabs.push_back(r.buf);
+    if (first.emplace(u.second, (int32_t)i).second) groups[{r.cls, r.w}].push_back((int32_t)i);
+  }
+  if (nk) HIPCHK(hipMemcpyAsync(dk, g->mirror.data(), sizeof(DevKey) * nk, hipMemcpyHostToDevice, s));
+  build_tables(groups, dk, blob, di, s);          // synchronises s
+  {
+    std::lock_guard<std::mutex> tg(d->tmu);
+    for (auto it = d->tcache.begin(); it != d->tcache.end();)
+      it = it->second.expired() ? d->tcache.erase(it) : std::next(it);
+    for (const auto& f : fresh) d->tcache[f.second.id + (char)f.second.w] = f.second.buf;   // at its final width
+  }
+  return g;
+}
+
+void upload_cls(jg_ctx* ctx, Device* d, DevGen& g, const std::vector<uint8_t>& cls_tab) {
+  g.dcls = dev_alloc(d->id, std::max<size_t>(cls_tab.size(), 16), &ctx->fail_alloc);
+  if (!cls_tab.empty()) HIPCHK(hipMemcpy(g.dcls->p, cls_tab.data(), cls_tab.size(), hipMemcpyHostToDevice));
+}
+
+// CAPJWT_TABLES_SYNC=1: jg_keys_load builds every comb table at its budgeted
+// width before returning (A/B of the narrow-first staging)
+bool tables_sync() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_TABLES_SYNC");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+bool needs_upgrade(const KeyState& K) {
+  for (size_t k = 0; k < K.keys.size(); ++k)
+    if (K.keys[k].valid && !K.tab_id[k].empty() && K.want_w[k] > K.dev[0]->kw[k]) return true;
+  return false;
+}
+
+// One step of the background upgrader: build the budgeted-width table of ONE
+// key that runs on a narrower one, on every device (the upgrade stream, beside
+// verification), then publish a generation whose records point at it.  The
+// key list is unchanged, so staged batches and queued work stay valid.
+// Returns false when nothing is left to widen.
+bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
+  KeyStateP cur = ctx->state();
+  if (!cur || cur->dev.empty()) return false;
+  size_t k = 0;
+  for (; k < cur->keys.size(); ++k)
+    if (cur->keys[k].valid && !cur->tab_id[k].empty() && cur->want_w[k] > cur->dev[0]->kw[k] &&
+        !skip.count(cur->tab_id[k] + (char)cur->want_w[k]))
+      break;
+  if (k == cur->keys.size()) return false;
+  const std::string key = cur->tab_id[k] + (char)cur->want_w[k];
+  const int cls = cur->keys[k].cls, w = cur->want_w[k];
+  std::vector<DevBufP> built(ctx->devs.size());
+  for (size_t i = 0; i < ctx->devs.size(); ++i) {
+    Device* d = ctx->devs[i].get();
+    {
+      std::lock_guard<std::mutex> tg(d->tmu);
+      auto it = d->tcache.find(key);
+      if (it != d->tcache.end()) built[i] = it->second.lock();
+    }
+    if (built[i]) continue;
+    if (table_bytes(cls, w) + HBM_RESERVE > free_hbm(d->id)) {
+      skip.insert(key);
+      std::lock_guard<std::mutex> g(ctx->up_mu);
+      ctx->up_warn = "a " + std::to_string(table_bytes(cls, w) >> 20) + " MiB comb table (W = " + std::to_string(w) +
+                     ") does not fit free HBM on device " + std::to_string(d->id) + "; key " + std::to_string(k) +
+                     " keeps its narrower table";
+      return true;
+    }
+    HIPCHK(hipSetDevice(d->id));
+    const DevGen& G = *cur->dev[i];
+    DevBufP t = dev_alloc(d->id, table_bytes(cls, w));
+    // a one-record key array pointing at the new table (the blob is the generation's)
+    DevKey rec = G.mirror[k];
+    rec.tab = (uint64_t)(uintptr_t)t->p;
+    rec.tab_w = w;
+    DevBufP tmp = dev_alloc(d->id, sizeof(DevKey) + 16);
+    const int32_t zero = 0;
+    HIPCHK(hipMemcpyAsync(tmp->p, &rec, sizeof(DevKey), hipMemcpyHostToDevice, d->ustream));
+    HIPCHK(hipMemcpyAsync((char*)tmp->p + sizeof(DevKey), &zero, sizeof zero, hipMemcpyHostToDevice, d->ustream));
+    std::map<std::pair<int, int>, std::vector<int32_t>> groups;
+    groups[{cls, w}].push_back(0);
+    build_tables(groups, tmp->as<DevKey>(), G.keyblob(), (int32_t*)((char*)tmp->p + sizeof(DevKey)), d->ustream);
+    built[i] = t;
+  }
+  // publish against whatever state is current now (a load may have replaced
+  // the one the build started from: every key with this content gets the table)
+  std::lock_guard<std::mutex> lg(ctx->load_mu);
+  KeyStateP now = ctx->state();
+  auto ns = std::make_shared<KeyState>(*now);
+  bool any = false;
+  for (size_t i = 0; i < ctx->devs.size() && i < ns->dev.size(); ++i) {
+    Device* d = ctx->devs[i].get();
+    auto g = std::make_shared<DevGen>(*ns->dev[i]);
+    bool hit = false;
+    for (size_t j = 0; j < ns->keys.size(); ++j) {
+      if (ns->tab_id[j] + (char)w != key || ns->want_w[j] != w || g->kw[j] >= w || !ns->keys[j].valid) continue;
+      g->mirror[j].tab = (uint64_t)(uintptr_t)built[i]->p;
+      g->mirror[j].tab_w = w;
+      g->kw[j] = (uint8_t)w;
+      hit = true;
+    }
+    {
+      std::lock_guard<std::mutex> tg(d->tmu);
+      d->tcache[key] = built[i];
+    }
+    if (!hit) continue;
+    any = true;
+    g->tabs.push_back(built[i]);
+    g->dkeys = dev_alloc(d->id, sizeof(DevKey) * std::max<size_t>(g->mirror.size(), 1));
+    if (!g->mirror.empty())
+      HIPCHK(hipMemcpy(g->dkeys->p, g->mirror.data(), sizeof(DevKey) * g->mirror.size(), hipMemcpyHostToDevice));
+    ns->dev[i] = g;
+  }
+  if (any) ctx->publish(ns);
+  return true;
+}
+
+void upgrade_loop(jg_ctx* ctx) {
+  std::set<std::string> skip;     // tables that did not fit (retried after the next key load)
+  std::unique_lock<std::mutex> lk(ctx->up_mu);
+  while (true) {
+    ctx->up_cv.wait(lk, [&] { return ctx->up_stop || ctx->up_pending; });
+    if (ctx->up_stop) break;
+    ctx->up_pending = false;
+    ctx->up_busy = true;
+    skip.clear();
+    lk.unlock();
+    try {
+      while (upgrade_one(ctx, skip)) {
+        std::lock_guard<std::mutex> g(ctx->up_mu);
+        if (ctx->up_stop) break;
+      }
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> g(ctx->up_mu);
+      ctx->up_warn = std::string("comb table upgrade failed (keys keep their narrower tables): ") + e.what();
+    }
+    lk.lock();
+    ctx->up_busy = false;
+    ctx->up_idle_cv.notify_all();
+  }
 }
 
 thread_local std::string g_tls_err;
 
 
 // Split jobs [0, ntok) over the context's devices by the cost model and queue
-// each device's share.  Caller holds key_mu (shared) and has validated the jobs.
-std::shared_ptr<Ticket> submit_locked(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok* toks,
-                                      size_t ntok, uint8_t* out) {
+// each device's share, every item running against the key state `ks`.
+std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_t* arena, size_t arena_len,
+                                  const jg_tok* toks, size_t ntok, uint8_t* out) {
   auto t = std::make_shared<Ticket>();
   const size_t nd = ctx->devs.size();
   std::vector<size_t> cut(nd + 1, 0);
   cut[nd] = ntok;
   if (nd > 1) {
     std::vector<double> pre(ntok + 1, 0.0);
-    const size_t nk = ctx->keys.size();
+    const size_t nk = ks->keys.size();
     for (size_t i = 0; i < ntok; ++i)
-      pre[i + 1] = pre[i] + (toks[i].key_idx < nk ? cls_cost(classify(ctx, toks[i])) : 0.0);
+      pre[i + 1] = pre[i] + (toks[i].key_idx < nk ? cls_cost(classify(*ks, toks[i])) : 0.0);
     size_t j = 0;
     for (size_t k = 1; k < nd; ++k) {
       const double target = pre[ntok] * (double)k / (double)nd;
@@ -1376,7 +1761,7 @@ std::shared_ptr<Ticket> submit_locked(jg_ctx* ctx, const uint8_t* arena, size_t 
     it.lo = cut[k];
     it.hi = cut[k + 1];
     it.out = out;
-    it.epoch = ctx->epoch;
+    it.ks = ks;
     it.dev_arena = dview;
     it.chunk = C;
     it.cuts = chunk_cuts(it.lo, it.hi, C);
@@ -1434,10 +1819,16 @@ jg_ctx* jg_create(const int* devices, int ndev) {
         HIPCHK(hipEventCreate(&s.tr_b));
         HIPCHK(hipEventCreate(&s.tr_c));
       }
+      HIPCHK(hipStreamCreateWithFlags(&d->kstream, hipStreamNonBlocking));
+      HIPCHK(hipStreamCreateWithFlags(&d->ustream, hipStreamNonBlocking));
       ctx->devs.push_back(std::move(d));
     }
+    auto ks = std::make_shared<KeyState>();        // no keys yet: every job is out of range
+    for (size_t i = 0; i < ctx->devs.size(); ++i) ks->dev.push_back(std::make_shared<DevGen>());
+    ctx->ks = ks;
     jg_ctx* c = ctx.release();
-    for (auto& d : c->devs) d->worker = std::thread(worker_loop, c, d.get());
+    for (size_t i = 0; i < c->devs.size(); ++i) c->devs[i]->worker = std::thread(worker_loop, c->devs[i].get(), i);
+    c->upgrader = std::thread(upgrade_loop, c);
     return c;
   } catch (const std::exception& e) {
     g_tls_err = e.what();
@@ -1447,6 +1838,12 @@ jg_ctx* jg_create(const int* devices, int ndev) {
 
 void jg_destroy(jg_ctx* ctx) {
   if (!ctx) return;
+  {
+    std::lock_guard<std::mutex> g(ctx->up_mu);
+    ctx->up_stop = true;
+  }
+  ctx->up_cv.notify_all();
+  if (ctx->upgrader.joinable()) ctx->upgrader.join();
   for (auto& d : ctx->devs) {
     {
       std::lock_guard<std::mutex> g(d->qmu);
@@ -1468,13 +1865,29 @@ void jg_destroy(jg_ctx* ctx) {
       (void)hipStreamSynchronize(d->copy);
       (void)hipStreamDestroy(d->copy);
     }
-    for (auto& t : d->tab_ref) t.reset();         // shared fixed-base tables: last holder frees
-    if (d->dkeys) (void)hipFree(d->dkeys);
-    if (d->dblob) (void)hipFree(d->dblob);
-    if (d->didx) (void)hipFree(d->didx);
-    if (d->dcls) (void)hipFree(d->dcls);
+    for (hipStream_t* st : {&d->kstream, &d->ustream})
+      if (*st) {
+        (void)hipStreamSynchronize(*st);
+        (void)hipStreamDestroy(*st);
+        *st = nullptr;
+      }
+    // this context's hold on the fixed-base tables; the process cache (g_tabs)
+    // keeps them for later contexts unless CAPJWT_RELEASE_GTABLES=1
+    for (auto& t : d->tab_ref) t.reset();
+    if (release_gtables()) {
+      std::lock_guard<std::mutex> g(g_tab_mu);
+      for (auto it = g_tabs.begin(); it != g_tabs.end();) {
+        if (it->first.first == d->id && it->second && it->second.use_count() == 1) {
+          (void)hipFree(it->second->p);
+          it = g_tabs.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
     d->lane0.destroy();
   }
+  ctx->publish(nullptr);                           // key generations: device memory freed here
   delete ctx;
 }
 
@@ -1482,51 +1895,68 @@ int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys) {
   if (!ctx || nkeys < 0 || (nkeys > 0 && !keys)) return -1;
   if (nkeys > 65535) { ctx->set_err("at most 65535 keys"); return -1; }
   try {
-    std::unique_lock<std::shared_mutex> kl(ctx->key_mu);    // no new submissions
-    for (auto& d : ctx->devs) wait_idle(d.get());            // queued work runs against the old table
-    std::vector<std::unique_lock<std::mutex>> dl;
-    for (auto& d : ctx->devs) dl.emplace_back(d->mu);
+    std::lock_guard<std::mutex> lg(ctx->load_mu);
+    std::string content = key_content(keys, nkeys, ctx->table_budget.load());
+    KeyStateP cur = ctx->state();
+    if (cur && cur->epoch > 0 && cur->content == content) return 0;   // unchanged key set: no device work
     StagedKeys S;
-    std::vector<HostKey> hk;
+    auto ns = std::make_shared<KeyState>();
     std::string warn;
-    build_keys(keys, nkeys, ctx->table_budget.load(), S, hk, &warn);   // throws before any device state changes
-    try {
-      for (auto& d : ctx->devs) load_keys_device(d.get(), S);
-      // device-side validity (on-curve, Ed25519 decoding) back into the host view
-      Device* d0 = ctx->devs[0].get();
-      std::vector<DevKey> back(S.dk.size());
-      if (!back.empty()) {
-        HIPCHK(hipSetDevice(d0->id));
-        HIPCHK(hipMemcpy(back.data(), d0->dkeys, sizeof(DevKey) * back.size(), hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < back.size(); ++i) hk[i].valid = hk[i].valid && back[i].valid;
-      }
-    } catch (...) {
-      // some device may hold part of the new table: nothing verifies until a
-      // load succeeds, and batches staged before now are stale
-      ctx->keys.clear();
-      rebuild_class_tables(ctx);
-      ctx->failed = true;
-      ++ctx->epoch;
-      throw;
+    build_keys(keys, nkeys, ctx->table_budget.load(), S, ns->keys, &warn);   // throws before any device work
+    // stage on every device beside running work; any failure throws and
+    // leaves the published table (and what verifies against it) untouched
+    std::vector<std::shared_ptr<DevGen>> gens;
+    for (auto& d : ctx->devs) gens.push_back(stage_device(ctx, d.get(), S, !tables_sync()));
+    // device-side validity (on-curve, Ed25519 decoding) back into the host view
+    for (size_t i = 0; i < ns->keys.size(); ++i) ns->keys[i].valid = ns->keys[i].valid && gens[0]->mirror[i].valid;
+    rebuild_class_tables(*ns);
+    for (size_t i = 0; i < gens.size(); ++i) upload_cls(ctx, ctx->devs[i].get(), *gens[i], ns->cls_tab);
+    ns->tab_id = std::move(S.tab_id);
+    ns->want_w = std::move(S.want_w);
+    ns->epoch = (cur ? cur->epoch : 0) + 1;
+    ns->content = std::move(content);
+    for (auto& g : gens) ns->dev.push_back(std::move(g));
+    const bool up = needs_upgrade(*ns);
+    ctx->publish(std::move(ns));
+    if (up) {
+      std::lock_guard<std::mutex> g(ctx->up_mu);
+      ctx->up_pending = true;
+      ctx->up_cv.notify_all();
     }
-    ctx->keys = std::move(hk);
-    rebuild_class_tables(ctx);
-    for (auto& d : ctx->devs) {
-      HIPCHK(hipSetDevice(d->id));
-      if (d->dcls) (void)hipFree(d->dcls);
-      d->dcls = nullptr;
-      HIPCHK(hipMalloc(&d->dcls, std::max<size_t>(ctx->cls_tab.size(), 16)));
-      if (!ctx->cls_tab.empty())
-        HIPCHK(hipMemcpy(d->dcls, ctx->cls_tab.data(), ctx->cls_tab.size(), hipMemcpyHostToDevice));
-    }
-    ctx->failed = false;
-    ++ctx->epoch;
     if (!warn.empty()) ctx->set_err(warn);
     return 0;
   } catch (const std::exception& e) {
     ctx->set_err(e.what());
     return -2;
   }
+}
+
+int jg_keys_wait_tables(jg_ctx* ctx) {
+  if (!ctx) return -1;
+  std::unique_lock<std::mutex> lk(ctx->up_mu);
+  ctx->up_idle_cv.wait(lk, [&] { return !ctx->up_pending && !ctx->up_busy; });
+  if (!ctx->up_warn.empty()) {
+    const std::string w = std::move(ctx->up_warn);
+    ctx->up_warn.clear();
+    lk.unlock();
+    ctx->set_err(w);
+    return 1;
+  }
+  return 0;
+}
+
+int jg_keys_table_widths(jg_ctx* ctx, int* widths, int cap) {
+  if (!ctx || cap < 0 || (cap > 0 && !widths)) return -1;
+  KeyStateP ks = ctx->state();
+  const int n = (int)ks->keys.size();
+  for (int i = 0; i < n && i < cap; ++i) widths[i] = ks->dev.empty() || ks->dev[0]->kw.empty() ? 0 : ks->dev[0]->kw[(size_t)i];
+  return n;
+}
+
+int jg_debug_fail_alloc(jg_ctx* ctx, int n) {
+  if (!ctx || n < 0) return -1;
+  ctx->fail_alloc.store(n);
+  return 0;
 }
 
 int jg_submit(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok* toks, size_t ntok,
@@ -1539,11 +1969,9 @@ int jg_submit(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok*
       *out = new jg_ticket{std::make_shared<Ticket>()};
       return 0;
     }
-    std::shared_lock<std::shared_mutex> kl(ctx->key_mu);
-    if (ctx->failed) { ctx->set_err("the last jg_keys_load failed; no key table is loaded"); return -2; }
     // jobs are validated chunk by chunk by the device workers, ahead of each
-    // chunk's upload (a bad job fails the ticket with -1 from jg_wait)
-    auto t = submit_locked(ctx, arena, arena_len, toks, ntok, verdict_out);
+    // chunk's upload (a bad job fails the ticket with -1 from jg_wait; jg.h)
+    auto t = submit_to(ctx, ctx->state(), arena, arena_len, toks, ntok, verdict_out);
     *out = new jg_ticket{std::move(t)};
     return 0;
   } catch (const std::exception& e) {
@@ -1585,12 +2013,12 @@ int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t ar
   if (device_slot < 0 || device_slot >= (int)ctx->devs.size()) return -1;
   if (ntok > (size_t)INT32_MAX / 2) { ctx->set_err("batch too large"); return -1; }
   try {
-    std::shared_lock<std::shared_mutex> kl(ctx->key_mu);
-    if (ctx->failed) { ctx->set_err("the last jg_keys_load failed; no key table is loaded"); return -2; }
+    KeyStateP ks = ctx->state();
     std::string err;
-    if (!check_jobs(ctx, arena_len, toks, ntok, &err)) { ctx->set_err(err); return -1; }
+    if (!check_jobs(*ks, arena_len, toks, ntok, &err)) { ctx->set_err(err); return -1; }
     auto b = std::make_unique<jg_batch>();
     b->ctx = ctx;
+    b->dslot = (size_t)device_slot;
     b->dev = ctx->devs[device_slot].get();
     b->lane = &b->dev->lane0;
     b->own = std::make_unique<Bufs>();
@@ -1604,15 +2032,15 @@ int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t ar
     }
     std::vector<JobDev> jobs;
     std::vector<int32_t> perm;
-    plan_layout(ctx, toks, ntok, b->plan, X, true);
+    plan_layout(*ks, toks, ntok, b->plan, X, true);
     jobs.resize(b->plan.npad);
     perm.resize(b->plan.npad);
-    plan_fill_host(ctx, toks, ntok, b->plan, X, jobs.data(), perm.data());
+    plan_fill_host(*ks, toks, ntok, b->plan, X, jobs.data(), perm.data());
     upload(b->b, b->lane->stream, b->plan, arena, arena_len, jobs.data(), perm.data());
     // the host vectors die here: the copies above must complete first
     HIPCHK(hipStreamSynchronize(b->lane->stream));
     b->arena_len = arena_len;
-    b->epoch = ctx->epoch;
+    b->epoch = ks->epoch;
     *out = b.release();
     return 0;
   } catch (const std::exception& e) {
@@ -1622,12 +2050,17 @@ int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t ar
 }
 
 namespace {
+// A resident batch runs against the current key state when its key list is
+// the one it was planned for (a comb-width upgrade since staging is fine: the
+// run picks up the wider tables); a reload with another key list invalidates it.
 void run_resident(jg_ctx* ctx, jg_batch* b, bool timed) {
   HIPCHK(hipSetDevice(b->dev->id));
-  if (b->epoch != ctx->epoch) throw std::runtime_error("key table reloaded since this batch was staged");
+  KeyStateP ks = ctx->state();
+  if (b->epoch != ks->epoch) throw std::runtime_error("key table reloaded since this batch was staged");
   b->timing = timed;
   b->marks_used = 0;
-  run_plan(b->dev, b->lane, b->b, b->plan, b);
+  run_plan(b->dev, *ks, *ks->dev[b->dslot], b->lane, b->b, b->plan, b);
+  b->ks_run = std::move(ks);
 }
 }  // namespace
 

@@ -51,6 +51,9 @@ __host__ __device__ inline uint32_t job_siglen(const JobDev& j) { return j.meta 
 __host__ __device__ inline bool job_live(const JobDev& j) { return job_alg(j) != (int)JOB_PAD; }
 
 // Device view of one loaded key (arrays live in the key blob, word offsets).
+// A key's comb table is its own device allocation, shared by content between
+// key loads (a JWKS refresh that keeps a key keeps its table): `tab` is its
+// device address and `tab_w` its comb width.
 struct DevKey {
   int32_t kind;        // jg_key_kind
   int32_t cls;         // Cls of (this key, a matching alg)
@@ -61,11 +64,12 @@ struct DevKey {
   uint32_t nlimbs;     // RSA: limb count used (74/112/148)
   uint64_t n_off;      // RSA: n (28-bit limbs)        -- word offset in blob
   uint64_t rr_off;     // RSA: R^2 mod n (28-bit limbs)
-  uint64_t tab_off;    // EC: comb table of Q / Ed: comb table of -A
+  uint64_t tab;        // EC: comb table of Q / Ed: comb table of -A (device address, 0 = none)
   uint64_t aux_off;    // EC: Q affine Montgomery (x,y) / Ed: raw public key words
   int32_t embits;      // RSA: bitlen(n) - 1
-  int32_t pad_;
+  int32_t tab_w;       // EC / Ed: comb width of `tab`
 };
+__host__ __device__ inline const uint32_t* key_table(const DevKey& K) { return (const uint32_t*)K.tab; }
 
 // Timing hook: the runtime records a HIP event on the batch's stream after
 // each kernel a launcher enqueues (names: "<class>_<kernel>").

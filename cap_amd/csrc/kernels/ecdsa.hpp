@@ -21,7 +21,8 @@ struct EcArgs {
   int32_t* exc_list;          // padded indices needing the exact path
   uint32_t* exc_count;
   int64_t npad, begin, end;
-  int32_t wq;                 // comb width of the keys' tables (P-256: 20 / 22 / 24, else 16)
+  int32_t wq;                 // comb width of the launch's key tables (every key of [begin, end) has it)
+  int32_t exc_reset;          // zero *exc_count first (the class's first launch)
 };
 
 // table geometry per curve: words per entry (x,y Montgomery limbs, 16-B aligned)
@@ -62,30 +63,25 @@ constexpr int64_t ec_table_words_w(int cls, int w) {
 }
 constexpr int64_t ec_table_words(int cls, bool gen) { return ec_table_words_w(cls, ec_comb_w(cls, gen)); }
 // Key-table width tiers (HBM for fewer additions, as the generators' wide
-// windows do): the widest W whose tables for all `nkeys` keys of the curve fit
-// `budget` bytes.  P-256: W = 26 (10 windows, 26.8 GB per key: 20 additions
-// per token with the W = 26 generator), 24 (11 windows, 7.4 GB), 22 (12,
-// 2.0 GB), 20 (13, 545 MB); P-384: 24 (17 windows, 18.3 GB), 20 (20 windows,
-// 1.34 GB), 18 (22, 369 MB), 16 (25, 105 MB); P-521: 20 (27, 2.26 GB), 18 (29,
-// 608 MB), 16 (33, 173 MB).  The narrowest width is always allowed.  The
-// budget applies to each curve.
+// windows do), widest first.  P-256: W = 26 (10 windows, 26.8 GB per key: 20
+// additions per token with the W = 26 generator), 24 (11 windows, 7.4 GB), 22
+// (12, 2.0 GB), 20 (13, 545 MB); P-384: 24 (17 windows, 18.3 GB), 20 (20
+// windows, 1.34 GB), 18 (22, 369 MB), 16 (25, 105 MB); P-521: 20 (27, 2.26 GB),
+// 18 (29, 608 MB), 16 (33, 173 MB).  The runtime picks one width per curve
+// from the context's table budget, a single total over every curve's key
+// tables (jg_runtime.cpp key_widths); the narrowest width is always allowed.
 constexpr int EC_P256_WQ[4] = {26, 24, 22, 20};
 constexpr int EC_P384_WQ[4] = {24, 20, 18, 16};
 constexpr int EC_P521_WQ[3] = {20, 18, 16};
-inline int ec_key_w(int cls, int nkeys, uint64_t budget) {
-  const int* t = cls == jgk::CLS_P256 ? EC_P256_WQ : cls == jgk::CLS_P384 ? EC_P384_WQ : EC_P521_WQ;
-  const int nt = cls == jgk::CLS_P521 ? 3 : 4;
-  for (int i = 0; i < nt; ++i)
-    if ((uint64_t)nkeys * (uint64_t)ec_table_words_w(cls, t[i]) * 4u <= budget) return t[i];
-  return t[nt - 1];
-}
 
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);
-// key staging: validate each listed key (plain 28-bit limbs x,y at aux_off), write
-// Montgomery affine coordinates back to aux_off and build its comb table.
-// tidx[0..tn): the subset of idx whose tables are (re)built; the others' tables
-// are copied from a previous load by the runtime.
-void launch_ec_keyprep(int cls, int wq, jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n,
-                       const int32_t* tidx, int tn, hipStream_t s);
+// key staging: validate each listed key (plain 28-bit limbs x,y at aux_off:
+// coordinates < p, on the curve) and write its Montgomery affine coordinates
+// back to aux_off
+void launch_ec_keyprep(int cls, jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);
+// comb tables (width wq) of the valid keys tidx[0..tn), written at each key's
+// `tab` (ec_table_words_w(cls, wq) words); after launch_ec_keyprep
+void launch_ec_keytables(int cls, int wq, jgk::DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn,
+                         hipStream_t s);
 // generator table for a curve into `tab` (ec_table_words(cls) words)
 void launch_ec_gtable(int cls, uint32_t* tab, hipStream_t s);

@@ -394,7 +394,7 @@ __global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
   if (!job_live(jb)) return;
   if (a.status[p] != ST_OK) { a.verdict_pad[p] = 0; return; }
   const int kidx = __builtin_amdgcn_readfirstlane(job_key(jb));
-  const uint32_t* __restrict__ qtab = a.keyblob + a.keys[kidx].tab_off;
+  const uint32_t* __restrict__ qtab = key_table(a.keys[kidx]);
   const uint32_t* __restrict__ gtab = a.gtab;
 
   uint32_t X[L], Y[L], Z[L];
@@ -674,7 +674,7 @@ __global__ void k_ec_table_base_keys(const DevKey* keys, uint32_t* blob, const i
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
   const uint32_t* aux = blob + K.aux_off;
-  window_base<CV, W>(blob + K.tab_off + (int64_t)w * NE * STRIDE, aux, aux + CV::Fp::L, w);
+  window_base<CV, W>((uint32_t*)K.tab + (int64_t)w * NE * STRIDE, aux, aux + CV::Fp::L, w);
 }
 
 template <class CV>
@@ -686,7 +686,7 @@ __global__ void k_ec_table_keys(const DevKey* keys, uint32_t* blob, const int32_
   if (k >= n || e >= NWIN * NE || e % NE == 0) return;
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
-  uint32_t* tab = blob + K.tab_off;
+  uint32_t* tab = (uint32_t*)K.tab;
   table_entry<CV, W>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
 }
 
@@ -715,7 +715,7 @@ template <class CV>
 void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   dim3 g((unsigned)waves), b(WAVE);
-  (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
+  if (a.exc_reset) (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
   // tokens per thread for the batched inversion: keep >= ~8 waves per CU
   const int64_t n = a.end - a.begin;
   int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * 8 * WAVE)));
@@ -728,13 +728,18 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   mk("exact");
 }
 
+// key staging: validate + Montgomery form (width-independent)
 template <class CV>
-void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx, int tn,
-                   hipStream_t s) {
+void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_ec_keyprep<CV>, dim3((n + 63) / 64), dim3(64), 0, s, keys, blob, idx, n);
+}
+
+// comb tables of keys tidx[0..tn) at CV::WQ, written to each key's `tab`
+template <class CV>
+void keytables_chain(DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
   constexpr int NWIN = ec_windows_w(CV::CLS, CV::WQ), NE = 1 << (CV::WQ - 1);
-  dim3 b(64);
-  if (n > 0) hipLaunchKernelGGL(k_ec_keyprep<CV>, dim3((n + 63) / 64), b, 0, s, keys, blob, idx, n);
   if (tn <= 0) return;
+  dim3 b(64);
   hipLaunchKernelGGL(k_ec_table_base_keys<CV>, dim3((NWIN + 63) / 64, tn), b, 0, s, keys, blob, tidx, tn);
   hipLaunchKernelGGL(k_ec_table_keys<CV>, dim3((NWIN * NE + 63) / 64, tn), b, 0, s, keys, blob, tidx, tn);
 }

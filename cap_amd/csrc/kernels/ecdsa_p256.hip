@@ -9,12 +9,15 @@ void launch_ec_p256(const EcArgs& a, hipStream_t s, const Marker& mk) {
   else launch_chain<CurveP256W<20>>(a, s, mk);
 }
 
-void launch_ec_keyprep_p256(int wq, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx,
-                          int tn, hipStream_t s) {
-  if (wq == 26) keyprep_chain<CurveP256W<26>>(keys, blob, idx, n, tidx, tn, s);
-  else if (wq == 24) keyprep_chain<CurveP256W<24>>(keys, blob, idx, n, tidx, tn, s);
-  else if (wq == 22) keyprep_chain<CurveP256W<22>>(keys, blob, idx, n, tidx, tn, s);
-  else keyprep_chain<CurveP256W<20>>(keys, blob, idx, n, tidx, tn, s);
+void launch_ec_keyprep_p256(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
+  keyprep_chain<CurveP256W<20>>(keys, blob, idx, n, s);
+}
+
+void launch_ec_keytables_p256(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
+  if (wq == 26) keytables_chain<CurveP256W<26>>(keys, blob, tidx, tn, s);
+  else if (wq == 24) keytables_chain<CurveP256W<24>>(keys, blob, tidx, tn, s);
+  else if (wq == 22) keytables_chain<CurveP256W<22>>(keys, blob, tidx, tn, s);
+  else keytables_chain<CurveP256W<20>>(keys, blob, tidx, tn, s);
 }
 
 void launch_ec_gtable_p256(uint32_t* tab, hipStream_t s) { gtable_chain<CurveP256W<20>>(tab, s); }

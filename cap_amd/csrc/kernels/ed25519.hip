@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
   EPt P;
 #pragma unroll
   for (int j = 0; j < L; ++j) { P.X[j] = 0; P.T[j] = 0; P.Y[j] = Fp::ONE[j]; P.Z[j] = Fp::ONE[j]; }
-  const uint32_t* __restrict__ atab = a.keyblob + K.tab_off;
+  const uint32_t* __restrict__ atab = key_table(K);
 #pragma unroll 1
   for (int w = 0; w < NW; ++w) {
     int e1 = 0, e2 = 0;                       // uniform select: no dynamic register indexing
@@ -373,7 +373,7 @@ __global__ void k_ed_table_base_keys(const DevKey* keys, uint32_t* blob, const i
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
   const uint32_t* aux = blob + K.aux_off + 8;
-  window_base(blob + K.tab_off + (int64_t)w * NE * ED_STRIDE, aux, aux + L, W * w);
+  window_base((uint32_t*)K.tab + (int64_t)w * NE * ED_STRIDE, aux, aux + L, W * w);
 }
 
 template <int W>
@@ -384,7 +384,7 @@ __global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_
   if (k >= n || e >= NWIN * NE || e % NE == 0) return;
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
-  uint32_t* tab = blob + K.tab_off;
+  uint32_t* tab = (uint32_t*)K.tab;
   table_entry<W>(tab + (int64_t)e * ED_STRIDE, tab + (int64_t)(e / NE) * NE * ED_STRIDE, e % NE + 1);
 }
 
@@ -415,10 +415,12 @@ void ed_tables(DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStr
 }
 }  // namespace
 
-void launch_ed_keyprep(int wa, DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx, int tn,
-                       hipStream_t s) {
+void launch_ed_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_ed_decode, dim3((n + 63) / 64), dim3(64), 0, s, keys, blob, idx, n);
+}
+
+void launch_ed_keytables(int wa, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
   if (tn <= 0) return;
   if (wa == 20) ed_tables<20>(keys, blob, tidx, tn, s);
   else if (wa == 18) ed_tables<18>(keys, blob, tidx, tn, s);

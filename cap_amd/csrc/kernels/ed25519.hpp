@@ -19,7 +19,7 @@ struct EdArgs {
                               // k_ed_finish's prefix products
   const uint32_t* btab;       // comb table of the base point B (Niels form)
   int64_t npad, begin, end;
-  int32_t wa;                 // comb width of the keys' tables (ed_key_w: 20 / 18 / 16)
+  int32_t wa;                 // comb width of the launch's key tables (ED_WA: 20 / 18 / 16)
 };
 
 constexpr int ED_L = 10;
@@ -29,7 +29,7 @@ constexpr int ED_STRIDE = 32;                   // 3 x 10 limbs, padded to 16 B
 // the wider window: B W=20 (13 windows, 872 MB), keys W=16 (16 windows, 67 MB
 // each) -> 29 additions per token (66 at W=8).
 // Key tables take a wider window when few keys share the context's table
-// budget (ed_key_w, as ecdsa.hpp ec_key_w): W = 20 (13 windows, 872 MB per
+// budget (ED_WA, picked with the EC tiers of ecdsa.hpp): W = 20 (13 windows, 872 MB per
 // key: 26 additions per token), 18 (15 windows, 252 MB), 16 (16, 67 MB).
 constexpr int ed_comb_w(bool base) { return base ? 20 : 16; }
 constexpr int ed_windows_w(int w) { return (253 + 1 + w - 1) / w; }
@@ -37,16 +37,13 @@ constexpr int ed_entries(bool base) { return 1 << (ed_comb_w(base) - 1); }
 constexpr int ed_windows(bool base) { return ed_windows_w(ed_comb_w(base)); }
 constexpr int64_t ed_table_words_w(int w) { return (int64_t)ed_windows_w(w) * (1 << (w - 1)) * ED_STRIDE; }
 constexpr int64_t ed_table_words(bool base) { return ed_table_words_w(ed_comb_w(base)); }
-inline int ed_key_w(int nkeys, uint64_t budget) {
-  for (int w : {20, 18})
-    if ((uint64_t)nkeys * (uint64_t)ed_table_words_w(w) * 4u <= budget) return w;
-  return 16;
-}
+constexpr int ED_WA[3] = {20, 18, 16};   // key-table width tiers, widest first (budget: jg_runtime.cpp key_widths)
 constexpr int ED_MAX_KEYS = 256;
 
 void launch_ed(const EdArgs& a, hipStream_t s, const jgk::Marker& mk);
-// key staging: decode each listed key's 32 public-key bytes (words at aux_off),
-// mark validity and build the comb table of -A at tab_off
-void launch_ed_keyprep(int wa, jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, const int32_t* tidx,
-                       int tn, hipStream_t s);
+// key staging: decode each listed key's 32 public-key bytes (words at
+// aux_off) and mark validity
+void launch_ed_keyprep(jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);
+// comb tables of -A (width wa) of the valid keys tidx[0..tn), at each key's `tab`
+void launch_ed_keytables(int wa, jgk::DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s);
 void launch_ed_btable(uint32_t* tab, hipStream_t s);

@@ -84,15 +84,41 @@ typedef struct jg_batch jg_batch;
 jg_ctx* jg_create(const int* devices, int ndev);
 void jg_destroy(jg_ctx* ctx);
 
-/* Replace the key table (copied; may be reloaded on JWKS refresh).  Invalid
- * keys (off-curve EC point, Ed25519 point that does not decode, even or
- * unusable RSA modulus, e out of range) load fine and verify nothing -- the
- * same outcome Go produces per token.  Returns 0, -1 on bad arguments, or -2
- * when the table cannot be staged (e.g. more than 256 EC keys of one curve):
- * the previous table then stays in force, unless a device failed half-way, in
- * which case no table is loaded and verification returns -2 until a load
- * succeeds. */
+/* Replace the key table (copied; may be reloaded on JWKS refresh -- go-oidc
+ * RemoteKeySet updateKeys behind jwt/keyset.go:127).  Invalid keys (off-curve
+ * EC point, Ed25519 point that does not decode, even or unusable RSA modulus,
+ * e out of range) load fine and verify nothing -- the same outcome Go produces
+ * per token.
+ *  - A key list identical to the loaded one (same bytes, same table budget)
+ *    returns 0 at once: no device work, nothing drained, staged batches stay
+ *    valid.
+ *  - Otherwise the new table is staged beside running verifications (no
+ *    drain): work submitted before the call finishes against the old table,
+ *    work submitted after it returns runs against the new one.  A key that was
+ *    already loaded keeps its comb table (shared by content, no copy); a new
+ *    EC / Ed25519 key gets a narrow table first (P-256 W = 20: 545 MB, about
+ *    0.1 s) so it verifies as soon as this returns, and its budgeted wide table
+ *    is built in the background and swapped in when complete
+ *    (jg_keys_wait_tables).  CAPJWT_TABLES_SYNC=1 builds full width here.
+ * Returns 0, -1 on bad arguments, or -2 when the table cannot be staged (more
+ * than 256 EC keys of one curve, not enough free HBM for the new tables, a
+ * device allocation or kernel failure): the previous table then stays in force
+ * on every device, as go-oidc keeps its cached keys when updateKeys fails. */
 int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys);
+
+/* Block until the background comb-table widening of the last jg_keys_load has
+ * finished (every key verifying with its budgeted table width).  Returns 0, 1
+ * when some table stayed narrower because it did not fit free HBM (see
+ * jg_last_error), -1 on bad arguments. */
+int jg_keys_wait_tables(jg_ctx* ctx);
+
+/* Comb width of each loaded key's table on the context's first device (0 for
+ * RSA and invalid keys): widths[0..min(n, cap)).  Returns n, the key count. */
+int jg_keys_table_widths(jg_ctx* ctx, int* widths, int cap);
+
+/* Test hook: the n-th device allocation of later key loads (counting from 1)
+ * fails as if hipMalloc ran out of memory; 0 disables.  Returns 0 or -1. */
+int jg_debug_fail_alloc(jg_ctx* ctx, int n);
 
 /* Verify ntok jobs, blocking (= jg_submit + jg_wait).  Host buffers; copied to
  * the device(s) in chunks whose H2D copies overlap the kernels of the previous
@@ -107,13 +133,18 @@ int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys);
 int jg_verify_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
                     const jg_tok* toks, size_t ntok, uint8_t* verdict_out);
 
-/* Asynchronous form: jg_submit validates the jobs (same return codes), queues
- * them on the context's devices and returns at once with a ticket; arena, toks
- * and verdict_out must stay valid and unmodified until jg_wait(ticket)
- * returns.  Consecutive submissions pipeline back to back on each device.
- * jg_wait blocks until every verdict is written, frees the ticket and returns
- * 0 or -2.  A batch runs entirely against the key table current at submit
- * time: a jg_keys_load waits for queued work to drain first. */
+/* Asynchronous form: jg_submit checks its arguments, queues the jobs on the
+ * context's devices and returns at once with a ticket (-1 on bad arguments, -2
+ * on an infrastructure error); arena, toks and verdict_out must stay valid and
+ * unmodified until jg_wait(ticket) returns.  Consecutive submissions pipeline
+ * back to back on each device.  The jobs themselves are validated by the
+ * device workers chunk by chunk, in the same pass that plans each chunk, so a
+ * bad job (a key_idx outside the table, a span past arena_len) is reported by
+ * jg_wait: it returns -1 and verdict_out is then only partly written (chunks
+ * before the bad one are verified; the rest are not).  jg_wait blocks until
+ * the batch is complete, frees the ticket and returns 0, -1 or -2.  A batch
+ * runs entirely against the key table current at submit time, even when a
+ * jg_keys_load replaces it while the batch is queued. */
 typedef struct jg_ticket jg_ticket;
 int jg_submit(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok* toks, size_t ntok,
               uint8_t* verdict_out, jg_ticket** ticket);
@@ -123,14 +154,20 @@ int jg_wait(jg_ctx* ctx, jg_ticket* ticket);
  * CAPJWT_CHUNK; >= 64).  Applies to later submissions.  Returns 0 or -1. */
 int jg_set_chunk(jg_ctx* ctx, size_t jobs);
 
-/* HBM (bytes per device, per curve) the context may spend on the comb tables
- * of its EC keys (default 32 GiB, or CAPJWT_TABLE_BUDGET_GB).  The next
- * jg_keys_load gives each curve's keys the widest comb window whose tables for
- * all of them fit: P-256 W = 26 (26.8 GB per key, 20 point additions per
- * token), 24 (7.4 GB, 21), 22 (2.0 GB) or 20 (545 MB); P-384 W = 24 (18.3 GB),
- * 20, 18 or 16; P-521 W = 20, 18 or 16 -- HBM traded for
- * fewer additions, as the shared generator tables do.  The narrowest width is
- * always allowed.  Returns 0 or -1. */
+/* HBM (bytes per device, one total over all curves) the context may spend on
+ * the comb tables of its EC and Ed25519 keys (default 32 GiB, or
+ * CAPJWT_TABLE_BUDGET_GB).  The next jg_keys_load first gives every key its
+ * curve's narrowest table (always allowed: P-256 W = 20, 545 MB; P-384 16,
+ * 105 MB; P-521 16, 173 MB; Ed25519 16, 67 MB), then widens P-256, P-384,
+ * Ed25519 and P-521 in that order, each curve to the widest width whose tables
+ * for all of its keys still fit what is left: P-256 W = 26 (26.8 GB per key,
+ * 20 point additions per token), 24 (7.4 GB, 21) or 22 (2.0 GB); P-384 W = 24
+ * (18.3 GB), 20 (1.34 GB) or 18; Ed25519 20 (872 MB) or 18; P-521 20 (2.26 GB)
+ * or 18 -- HBM traded for fewer additions, as the shared generator tables do.
+ * New tables are also sized against free HBM: a load narrows them rather than
+ * fail.  Besides the budget, each device holds the generator / base-point
+ * tables (about 31 GB with all four curves) for the life of the process
+ * (CAPJWT_RELEASE_GTABLES=1 frees them with the last context).  Returns 0 or -1. */
 int jg_set_table_budget(jg_ctx* ctx, uint64_t bytes);
 
 const char* jg_last_error(jg_ctx* ctx);

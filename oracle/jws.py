@@ -198,14 +198,31 @@ def _der(b, i, tag):
         if nb == 0 or nb > 4 or j + nb > len(b):
             return None
         ln = int.from_bytes(b[j:j + nb], "big")
+        if ln < 128 or b[j] == 0:                    # DER: non-minimal length (asn1 / cryptobyte reject)
+            return None
         j += nb
     if j + ln > len(b):
         return None
     return b[j:j + ln], j + ln
 
 
+class UnknownAlgorithm(Exception):
+    """x509: unknown public key algorithm (x509.ParseCertificate leaves
+    PublicKey nil for it instead of failing)"""
+
+
 def spki_key(spki: bytes):
     """x509.ParsePKIXPublicKey subset -> Key or None."""
+    try:
+        return spki_key_ex(spki)
+    except UnknownAlgorithm:
+        return None
+
+
+def spki_key_ex(spki: bytes):
+    """Key, None for a malformed SubjectPublicKeyInfo or an invalid key of a
+    known algorithm (Go's parsePublicKey errors), UnknownAlgorithm raised for an
+    algorithm OID Go does not know."""
     r = _der(spki, 0, 0x30)
     if not r:
         return None
@@ -222,7 +239,14 @@ def spki_key(spki: bytes):
     if not o:
         return None
     oid, j = o
-    params = alg[j:]
+    # AlgorithmIdentifier.Parameters: the first element after the OID (Go
+    # ignores any further ones, as it ignores elements after the BIT STRING)
+    params = b""
+    if j < len(alg):
+        pr = _der(alg, j, alg[j])
+        if not pr:
+            return None
+        params = alg[j:pr[1]]
     if oid == bytes.fromhex("2a864886f70d010101"):
         if params != b"\x05\x00":
             return None
@@ -252,20 +276,26 @@ def spki_key(spki: bytes):
         if params or len(key) != 32:
             return None
         return Key("OKP", crv="Ed25519", x=key)
-    return None
+    raise UnknownAlgorithm()
 
 
 def cert_key(der: bytes):
     """Certificate -> its SubjectPublicKeyInfo's Key (or "unknown")."""
     c = _der(der, 0, 0x30)
-    if not c:
+    if not c or c[1] != len(der):                    # x509: trailing data
         return None
+    # Certificate ::= SEQUENCE { tbsCertificate, signatureAlgorithm, signatureValue BIT STRING }
     t = _der(c[0], 0, 0x30)
-    if not t:
+    sa = t and _der(c[0], t[1], 0x30)
+    sv = sa and _der(c[0], sa[1], 0x03)
+    if not sv or sv[1] != len(c[0]):
         return None
     tbs, i = t[0], 0
     if tbs[:1] == b"\xa0":
-        i = _der(tbs, 0, 0xA0)[1]
+        v = _der(tbs, 0, 0xA0)
+        if not v:                                    # x509: malformed version
+            return None
+        i = v[1]
     for tag in (0x02, 0x30, 0x30, 0x30, 0x30):
         r = _der(tbs, i, tag)
         if not r:
@@ -274,7 +304,13 @@ def cert_key(der: bytes):
     s = _der(tbs, i, 0x30)
     if not s:
         return None
-    return spki_key(tbs[i:s[1]]) or "unknown"
+    # x509.ParseCertificate: an invalid key of a known algorithm (an EC point
+    # off the curve, RSA without NULL parameters, ...) fails the parse; an
+    # unknown algorithm parses with PublicKey nil
+    try:
+        return spki_key_ex(tbs[i:s[1]])
+    except UnknownAlgorithm:
+        return "unknown"
 
 
 def ec_on_curve(crv, x: bytes, y: bytes) -> bool:

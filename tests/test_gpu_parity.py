@@ -200,21 +200,33 @@ def test_rsa_keys_above_4096_bits():
         assert out[s] == want, t["name"]
 
 
-@pytest.mark.parametrize("tier", ["w26", "w24", "w22", "w20"])
+@pytest.mark.parametrize("tier", [26, 24, 22, 20])
 def test_p256_key_table_widths(tier):
     """The P-256 key comb width follows the table budget (jg_set_table_budget,
-    ecdsa.hpp ec_key_w): W = 26 / 24 / 22 / 20 give the same verdicts (the w26
-    budget also gives the P-384 keys their W = 24 tier) as the oracle
-    on every golden token against every key, and on a random ES256 batch."""
+    one total over every curve, jg_runtime.cpp key_widths): W = 26 / 24 / 22 /
+    20 give the same verdicts as the oracle on every golden token against every
+    key, and the library reports the width the budget buys (bench.key_widths)."""
+    import bench
     from cap_amd import _lib
     from oracle import jws
     keys, toks = H.golden()
-    n256 = sum(1 for k in keys if k.get("kty") == "EC" and k.get("crv") == "P-256")
-    assert n256 >= 2
-    per_key = {"w26": 10 * (1 << 25) * 80, "w24": 11 * (1 << 23) * 80, "w22": 12 * (1 << 21) * 80, "w20": 0}[tier]
+    crv = {"P-256": "p256", "P-384": "p384", "P-521": "p521"}
+    cls = [crv.get(k.get("crv")) if k.get("kty") == "EC" else ("ed25519" if k.get("kty") == "OKP" else None)
+           for k in keys]
+    counts = {c: cls.count(c) for c in ("p256", "p384", "p521", "ed25519")}
+    assert counts["p256"] >= 2
+    narrow = sum(n * bench.table_bytes(c, bench.WIDTH_TIERS[c][-1]) for c, n in counts.items())
+    budget = narrow + counts["p256"] * (bench.table_bytes("p256", tier) - bench.table_bytes("p256", 20))
+    assert bench.key_widths(counts, budget)["p256"] == tier
     ctx = _lib.Context()
-    ctx.set_table_budget(n256 * per_key)
+    ctx.set_table_budget(budget)
     ctx.load_keys([H.abi_key(k) for k in keys])
+    widths = ctx.table_widths()
+    want_w = bench.key_widths(counts, budget)
+    for k, c, w in zip(keys, cls, widths):
+        if c is not None and w:
+            assert w == want_w[c], (k["kid"], w, want_w[c])
+    assert [w for c, w in zip(cls, widths) if c == "p256"] == [tier] * counts["p256"]
     kid_index = {k["kid"]: i for i, k in enumerate(keys)}
     okeys = {k["kid"]: jws.Key.from_fixture(k) for k in keys}
     sel = [t for t in toks if t["alg"] in ("ES256", "ES384", "ES512")]

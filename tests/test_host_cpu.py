@@ -18,6 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 H = pytest.importorskip("cap_amd._capjwt_host")
 
 SECOND = 1_000_000_000
+# mutation-fuzz rounds scale with CAPJWT_FUZZ_SCALE (tools/sanitize/run.sh runs 10x under ASan + UBSan)
+FUZZ = max(1, int(os.environ.get("CAPJWT_FUZZ_SCALE", "1")))
 
 
 @pytest.fixture(scope="module")
@@ -82,7 +84,7 @@ def test_json_duplicate_members_replace_in_place(n, dups):
 def test_b64url_decode_fuzz():
     rnd = random.Random(1)
     alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_=+/\r\n. "
-    for _ in range(3000):
+    for _ in range(3000 * FUZZ):
         s = "".join(rnd.choice(alpha) for _ in range(rnd.randint(0, 13)))
         assert H.b64url_decode(s) == jws.b64url_decode(s), s
 
@@ -290,6 +292,81 @@ def test_parse_public_key_pem(golden, cases):
     for bad in [b"", b"garbage", b"-----BEGIN PUBLIC KEY-----\nAAAA\n-----END PUBLIC KEY-----\n"]:
         with pytest.raises(ValueError):
             H.parse_public_key_pem(bad)
+
+
+def _mutate_bytes(rnd, b, alpha):
+    b = bytearray(b)
+    for _ in range(rnd.randint(1, 4)):
+        op = rnd.random()
+        i = rnd.randrange(len(b) + 1)
+        if op < 0.45 and b:
+            b[min(i, len(b) - 1)] = rnd.choice(alpha)
+        elif op < 0.75:
+            b.insert(i, rnd.choice(alpha))
+        elif b:
+            del b[min(i, len(b) - 1):min(i, len(b) - 1) + rnd.randint(1, 8)]
+    return bytes(b)
+
+
+def test_json_mutation_fuzz():
+    """byte mutations of JSON documents (and of the claims payload shape):
+    accept / reject and the decoded value equal Go encoding/json's (oracle)"""
+    rnd = random.Random(11)
+    seeds = [d for d in JSON_DOCS if len(d) > 1] + [
+        b'{"aud":["www.example.com"],"exp":1611699344,"iat":1611699284,"iss":"https://example.com/",'
+        b'"jti":"7","nbf":1611699284,"sub":"alice@example.com","n":[1.5e3,-0,null,true,{"x":"\u00e9"}]}']
+    alpha = list(b'{}[]":,.-+0123456789eE\\u tnrfal\x00\x7f\xc3\xa9\xed\xa0\xff')
+    for _ in range(2000 * FUZZ):
+        doc = _mutate_bytes(rnd, rnd.choice(seeds), alpha)
+        v, err = H.json_loads(doc)
+        try:
+            want = jws.go_json(doc)
+            ok = True
+        except jws.GoJSONError:
+            ok = False
+        assert (err is None) == ok, (doc, err)
+        if ok:
+            assert v == want, doc
+
+
+def test_jwks_mutation_fuzz(golden, cases):
+    """byte mutations of a JWKS document (RSA / EC / OKP members, an x5c
+    certificate) and of the certificate's DER under x5c: the decoded key set,
+    or the rejection, equals go-jose's (oracle jwks_decode with its own DER walker)"""
+    rnd = random.Random(5)
+    raw = golden["keys_raw"]
+    d = next(x for x in raw if x["kid"] == "p256-a")
+    der = base64.b64decode("".join(l for l in cases["certs"]["p256-a"].splitlines() if "-----" not in l))
+    good = [_jwk(x) for x in raw if x["kid"] in ("rsa2048-a", "p384-a", "ed-a")]
+    doc = json.dumps({"keys": good + [_jwk(d, x5c=[base64.b64encode(der).decode()])]}).encode()
+    alpha = list(b'{}[]":,AQBxyz09-_=+/ \x00\xff')
+    for _ in range(400 * FUZZ):
+        _cmp_jwks(_mutate_bytes(rnd, doc, alpha))
+    for _ in range(400 * FUZZ):
+        bad = _mutate_bytes(rnd, der, list(range(256)))
+        _cmp_jwks(json.dumps({"keys": [_jwk(d, x5c=[base64.b64encode(bad).decode()])]}).encode())
+
+
+def test_pem_mutation_fuzz(golden, cases):
+    """byte mutations of PEM public keys and certificates: ParsePublicKeyPEM
+    (jwt/keyset.go:178-200) never crashes and rejects with ValueError; DER-level
+    mutations that still parse give the key of the oracle's DER walker"""
+    rnd = random.Random(9)
+    pems = [x["pem"].encode() for x in golden["keys_raw"] if x.get("pem")] + [p.encode() for p in cases["certs"].values()]
+    for _ in range(500 * FUZZ):
+        src = rnd.choice(pems)
+        if rnd.random() < 0.5:
+            bad = _mutate_bytes(rnd, src, list(b"ABCQ019+/=-\n "))
+        else:
+            lines = src.decode().splitlines()
+            body = base64.b64decode("".join(l for l in lines if "-----" not in l))
+            body = _mutate_bytes(rnd, body, list(range(256)))
+            b64 = base64.b64encode(body).decode()
+            bad = ("\n".join([lines[0]] + [b64[i:i + 64] for i in range(0, len(b64), 64)] + [lines[-1]]) + "\n").encode()
+        try:
+            H.parse_public_key_pem(bad)
+        except ValueError:
+            pass
 
 
 def test_x5c_certificate_must_match_key(golden, cases):
