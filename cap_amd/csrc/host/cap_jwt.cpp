@@ -545,6 +545,7 @@ class StaticKeySet final : public KeySet {
     eng_.load(keys_);
     for (const auto& k : keys_) fam_.push_back(key_family(k));
   }
+  void WaitTables() override { eng_.wait_tables(); }
   Results verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
     std::lock_guard<std::mutex> g(mu_);
     Verified V;
@@ -618,6 +619,7 @@ class JSONWebKeySet final : public KeySet {
   JSONWebKeySet(std::string url, std::string ca, Fetcher f, const std::vector<int>& devices)
       : url_(std::move(url)), ca_(std::move(ca)), fetch_(std::move(f)), eng_(devices) {}
 
+  void WaitTables() override { eng_.wait_tables(); }
   Results verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
     std::lock_guard<std::mutex> g(mu_);
     Verified V;
@@ -708,6 +710,12 @@ class JSONWebKeySet final : public KeySet {
       *err = "oidc: get keys failed: " + resp.status_text + " " + resp.body;
       return false;
     }
+    // an unchanged document (the usual refresh-on-miss answer for a tampered
+    // token): the cached keys stand as they are -- no decode, no device work
+    if (have_keys_ && resp.body == body_) {
+      expiry_ns_ = wall_now_ns() + (resp.max_age_s > 0 ? resp.max_age_s * kSecond : 0);
+      return true;
+    }
     std::vector<JSONWebKey> keys;
     std::string derr;
     if (!jwks_decode(resp.body, &keys, &derr)) {
@@ -732,6 +740,7 @@ class JSONWebKeySet final : public KeySet {
     }
     fam_ = std::move(fam);
     keys_ = std::move(keys);
+    body_ = std::move(resp.body);
     have_keys_ = true;
     expiry_ns_ = wall_now_ns() + (resp.max_age_s > 0 ? resp.max_age_s * kSecond : 0);
     return true;
@@ -743,6 +752,7 @@ class JSONWebKeySet final : public KeySet {
   std::mutex mu_;
   std::vector<JSONWebKey> keys_;
   std::vector<int> fam_;
+  std::string body_;              // the JWKS document keys_ came from
   bool have_keys_ = false;
   int64_t expiry_ns_ = 0;
 };
@@ -816,6 +826,8 @@ Engine::~Engine() {
   if (pinned_) jg_host_free(pinned_);
   if (ctx_) jg_destroy(ctx_);
 }
+
+void Engine::wait_tables() { (void)jg_keys_wait_tables(ctx_); }
 
 void Engine::load(const std::vector<PublicKey>& keys) {
   std::vector<jg_key> jk;

@@ -128,7 +128,8 @@ class Engine {
   ~Engine();
   Engine(const Engine&) = delete;
   Engine& operator=(const Engine&) = delete;
-  void load(const std::vector<PublicKey>& keys);      // jg_keys_load
+  void load(const std::vector<PublicKey>& keys);      // jg_keys_load (returns once the keys verify)
+  void wait_tables();                                 // jg_keys_wait_tables: wide comb tables in place
   // verify (arena entry, key, alg) jobs; verdicts[i] = 1 accept, 0 reject
   void verify(const uint8_t* arena, size_t arena_len, const void* jobs, size_t njobs, uint8_t* verdicts);
   // SHA-2 of (arena span, family) jobs: digests njobs x 64 bytes (jg_hash_batch)
@@ -173,6 +174,9 @@ class KeySet {
   // batch verify; `post` (may be null) continues each token's result with what
   // the parse learned (Validator::ValidateBatch)
   virtual Results verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) = 0;
+  // block until background comb-table widening of the last key load is done
+  // (keys verify before that, on narrower tables; a measurement hook)
+  virtual void WaitTables() {}
 };
 
 std::unique_ptr<KeySet> NewStaticKeySet(const std::vector<PublicKey>& keys, std::string* err,

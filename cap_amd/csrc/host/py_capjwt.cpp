@@ -294,6 +294,10 @@ PYBIND11_MODULE(_capjwt_host, m) {
           rs = s.ks->VerifySignatureBatch(views(v));
         }
         return results_py(rs);
+      })
+      .def("wait_tables", [](PyKeySet& s) {
+        py::gil_scoped_release rel;
+        s.ks->WaitTables();
       });
 
   m.def("new_static_keyset", [](const std::vector<PublicKey>& keys, const std::vector<int>& devices) {

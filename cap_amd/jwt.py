@@ -59,6 +59,11 @@ class KeySet:
     def VerifySignature(self, token, ctx=None):
         return tuple(self._impl.verify_signature(token))
 
+    def WaitTables(self):
+        """Block until the key comb tables of the last key (re)load reach their
+        budgeted width (keys verify before that, on narrower tables)."""
+        self._impl.wait_tables()
+
     def VerifySignatureBatch(self, tokens: Sequence, ctx=None):
         return [tuple(r) for r in self._impl.verify_signature_batch(list(tokens))]
 

@@ -8,6 +8,12 @@ print("pool_ab", d.get("pool_ab", {}).get("value", 0) / 1e6, d.get("pool_ab", {}
 print("rs256 %.1f M/s frac %.3f" % (d["rs256"]["value"] / 1e6, d["rs256"]["roofline"]["frac"]))
 for k, v in d["configs"].items():
     print(k, round(v["value"] / 1e6, 1), {a: round(b["frac"], 3) for a, b in v.get("roofline", {}).items()}, v.get("error"))
-print("e2e %.2f M/s" % (d["e2e"]["value"] / 1e6), "cpu port", d["cpu_baseline"]["value"], "openssl", {k: v["value"] for k, v in d["cpu_baseline_openssl"].items()})
-print("cpu rs256 port", d["cpu_baseline_rs256"]["value"], d["cpu_baseline_rs256"]["sample"][:80])
+print("e2e %.2f M/s" % (d["e2e"]["value"] / 1e6), "cpu_baseline", d["cpu_baseline"]["value"], d["cpu_baseline"].get("label", "")[:20],
+      "port", d.get("cpu_baseline_port", {}).get("value"), "openssl", {k: v["value"] for k, v in d.get("cpu_baseline_openssl", {}).items()})
+if "cpu_baseline_rs256_port" in d:
+    print("cpu rs256 port", d["cpu_baseline_rs256_port"]["value"])
+for k, v in d.get("configs", {}).items():
+    for sub in ("stream", "jwks_e2e", "refresh"):
+        if sub in v:
+            print(k, sub, {a: b for a, b in v[sub].items() if not isinstance(b, (dict, list, str))})
 print("speedup", d["speedup_vs_cpu"])

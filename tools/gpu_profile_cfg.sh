@@ -10,6 +10,8 @@ TAG=${1:-cfg}
 O=gpurun_out/$TAG
 mkdir -p "$O"
 ARGS="--configs-only --steps 4 --warmup 1 --no-ab"
+echo "[0/5] class costs $(date +%T)"
+timeout -k 10 300 python3 tools/class_costs.py "$O/class_costs.json" > "$O/class_costs.log" 2>&1 || { echo COSTS_FAIL; tail -20 "$O/class_costs.log"; exit 1; }
 echo "[1/5] bench configs $(date +%T)"
 timeout -k 10 300 python3 bench.py --configs-only --steps 8 --warmup 2 > "$O/bench.json" 2> "$O/bench.err" || { echo BENCH_FAIL; tail -20 "$O/bench.err"; exit 1; }
 echo "[2/5] kernel trace $(date +%T)"

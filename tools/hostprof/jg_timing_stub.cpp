@@ -16,6 +16,7 @@ jg_ctx* jg_create(const int*, int) { return new jg_ctx{0}; }
 void jg_destroy(jg_ctx* c) { delete c; }
 const char* jg_last_error(jg_ctx*) { return "stub"; }
 int jg_keys_load(jg_ctx*, const jg_key*, int) { return 0; }
+int jg_keys_wait_tables(jg_ctx*) { return 0; }
 void* jg_host_alloc(size_t n) { return std::malloc(n); }
 void jg_host_free(void* p) { std::free(p); }
 int jg_verify_batch(jg_ctx*, const uint8_t*, size_t, const jg_tok*, size_t n, uint8_t* verdicts) {
