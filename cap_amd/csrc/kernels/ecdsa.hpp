@@ -29,7 +29,15 @@ struct EcArgs {
 constexpr int ec_limbs(int cls) { return cls == jgk::CLS_P256 ? 10 : cls == jgk::CLS_P384 ? 15 : 20; }
 // 32-bit words of r (and of s) as prep leaves them: ceil(coordinate bytes / 4)
 constexpr int ec_sig_words(int cls) { return cls == jgk::CLS_P256 ? 8 : cls == jgk::CLS_P384 ? 12 : 17; }
-constexpr int ec_stride(int cls) { return (2 * ec_limbs(cls) + 3) & ~3; }
+// P-256 entries packed to 64 bytes (JG_EC_PACK64): x and y as 8 32-bit words
+// each (canonical Montgomery values < p < 2^256), unpacked to 28-bit limbs on
+// load -- a 64-B-aligned entry touches one 128-B line where the 80-B limb form
+// touched 1.5 on average.  Other curves keep the limb form.
+#ifndef JG_EC_PACK64
+#define JG_EC_PACK64 0
+#endif
+constexpr bool ec_packed(int cls) { return JG_EC_PACK64 && cls == jgk::CLS_P256; }
+constexpr int ec_stride(int cls) { return ec_packed(cls) ? 16 : (2 * ec_limbs(cls) + 3) & ~3; }
 constexpr int ec_order_bits(int cls) { return cls == jgk::CLS_P256 ? 256 : cls == jgk::CLS_P384 ? 384 : 521; }
 // Fixed-base comb over signed W-bit digits: u = sum_w d_w 2^(W w), d_w in
 // [-2^(W-1), 2^(W-1)), so a token costs ceil((bits+1)/W) mixed additions per

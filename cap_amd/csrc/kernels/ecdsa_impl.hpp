@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.hpp"
@@ -130,6 +131,31 @@ __device__ __forceinline__ bool ec_scalar_inputs(const EcArgs& a, int64_t p, uin
   return ok;
 }
 
+// r and e of a token that passed ec_scalar_inputs (pass 2 of the batched
+// scalar stage: the checks are done, only the values are needed)
+template <class CV>
+__device__ __forceinline__ void ec_scalar_re(const EcArgs& a, int64_t p, uint32_t* r, uint32_t* e) {
+  using Fn = typename CV::Fn;
+  constexpr int L = Fn::L;
+  constexpr int CB = CV::C::BYTES;
+  constexpr int CW = ec_sig_words(CV::CLS);
+  const int64_t np = a.npad;
+  uint32_t rw[CW];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) rw[q] = a.sigw[(int64_t)q * np + p];
+  mp::words_to_limbs<L, CW>(r, rw);
+  const int alg = job_alg(a.jobs[p]);
+  const int hl = es_hash_bytes(alg) < CB ? es_hash_bytes(alg) : CB;
+  uint32_t ew[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int src = hl / 4 - 1 - q;
+    ew[q] = src >= 0 ? a.dig[(int64_t)(src < 0 ? 0 : src) * np + p] : 0u;
+  }
+  mp::words_to_limbs<L, 16>(e, ew);
+  mp::csub<Fn>(e);
+}
+
 // Signed W-bit recoding: u = sum_w d_w 2^(W w), d_w in [-2^(W-1), 2^(W-1)),
 // one int32 row per window starting at digit row `row0`.
 template <class CV, int W, int NWIN>
@@ -147,14 +173,6 @@ __device__ __forceinline__ void store_digit_rows(const EcArgs& a, int64_t p, con
     v -= c << W;
     a.digs[(int64_t)(row0 + w) * a.npad + p] = (uint32_t)v;
   }
-}
-
-template <class CV>
-__device__ __forceinline__ void store_digits(const EcArgs& a, int64_t p, const uint32_t* u1, const uint32_t* u2) {
-  constexpr int WG = ec_comb_w(CV::CLS, true), NG = ec_windows(CV::CLS, true);
-  constexpr int WQ = CV::WQ, NQ = ec_windows_w(CV::CLS, CV::WQ);
-  store_digit_rows<CV, WG, NG>(a, p, u1, 0);
-  store_digit_rows<CV, WQ, NQ>(a, p, u2, NG);
 }
 
 // Batched scalar stage (Montgomery's trick): thread i owns the B tokens
@@ -215,11 +233,14 @@ __global__ void __launch_bounds__(64) JG_EC_SCALAR_ATTR k_ec_scalar_batch(EcArgs
     for (int k = 0; k < L; ++k) sm[k] = a.u2w[(int64_t)k * np + p];
     mp::mul<Fn>(w, inv, cprev);                  // s_j^-1 R
     mp::mul<Fn>(inv, inv, sm);
-    uint32_t r[L], s[L], e[L], u1[L], u2[L];
-    (void)ec_scalar_inputs<CV>(a, p, r, s, e);
+    uint32_t r[L], e[L], u1[L], u2[L];
+    ec_scalar_re<CV>(a, p, r, e);
+    constexpr int WG = ec_comb_w(CV::CLS, true), NG = ec_windows(CV::CLS, true);
+    constexpr int WQ = CV::WQ, NQ = ec_windows_w(CV::CLS, CV::WQ);
     mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
     mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
-    store_digits<CV>(a, p, u1, u2);       // (the rare exact path recomputes u1, u2 itself)
+    store_digit_rows<CV, WG, NG>(a, p, u1, 0);  // (the rare exact path recomputes u1, u2 itself)
+    store_digit_rows<CV, WQ, NQ>(a, p, u2, NG);
   }
 }
 
@@ -356,6 +377,39 @@ __device__ __forceinline__ void madd_z1(uint32_t* X, uint32_t* Y, uint32_t* Z, c
   y3_from<Fp>(Y, r, t, y1, hhh);
 }
 
+// A table entry (affine x, y; canonical Montgomery form): 2L limbs, or 16
+// packed words for P-256 (ecdsa.hpp ec_packed)
+template <class CV>
+__device__ __forceinline__ void load_entry(const uint32_t* __restrict__ ent, uint32_t* x, uint32_t* y) {
+  constexpr int L = CV::Fp::L;
+  if constexpr (ec_packed(CV::CLS)) {
+    const uint4* e4 = reinterpret_cast<const uint4*>(ent);
+    const uint4 a = e4[0], b = e4[1], c = e4[2], d = e4[3];
+    const uint32_t wx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const uint32_t wy[8] = {c.x, c.y, c.z, c.w, d.x, d.y, d.z, d.w};
+    mp::words_to_limbs<L, 8>(x, wx);
+    mp::words_to_limbs<L, 8>(y, wy);
+  } else {
+#pragma unroll
+    for (int j = 0; j < L; ++j) { x[j] = ent[j]; y[j] = ent[L + j]; }
+  }
+}
+
+template <class CV>
+__device__ __forceinline__ void store_entry(uint32_t* out, const uint32_t* x, const uint32_t* y) {
+  constexpr int L = CV::Fp::L;
+  if constexpr (ec_packed(CV::CLS)) {
+    uint32_t w[16];
+    mp::limbs_to_words<L, 8>(w, x);
+    mp::limbs_to_words<L, 8>(w + 8, y);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) out[j] = w[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < L; ++j) { out[j] = x[j]; out[L + j] = y[j]; }
+  }
+}
+
 // Z1ONE: the accumulator, if not empty, holds exactly one table entry (Z == 1)
 template <class CV, bool GEN, bool Z1ONE = false>
 __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z, bool& empty,
@@ -363,11 +417,14 @@ __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z
   using Fp = typename CV::Fp;
   constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS), NE = GEN ? ec_entries(CV::CLS, true) : 1 << (CV::WQ - 1);
   if (d == 0) return;
+#ifdef JG_AB_TINY_TABLE
+  const int ad = (((d < 0 ? -d : d) - 1) & 255) + 1;     // A/B only: every gather within 256 entries (wrong verdicts)
+#else
   const int ad = d < 0 ? -d : d;
+#endif
   const uint32_t* ent = tab + ((int64_t)w * NE + (ad - 1)) * STRIDE;
   uint32_t x2[L], y2[L];
-#pragma unroll
-  for (int j = 0; j < L; ++j) { x2[j] = ent[j]; y2[j] = ent[L + j]; }
+  load_entry<CV>(ent, x2, y2);
   if (d < 0) mp::neg<Fp>(y2, y2);
   if (empty) {
     mp::copy<Fp>(X, x2);
@@ -633,8 +690,7 @@ __device__ void store_affine(uint32_t* out, const JPt<typename CV::Fp>& P) {
   mp::mul<Fp>(x, P.X, zi2);
   mp::mul<Fp>(y, P.Y, zi3);
   mp::canon<Fp>(x); mp::canon<Fp>(y);
-#pragma unroll
-  for (int j = 0; j < L; ++j) { out[j] = x[j]; out[L + j] = y[j]; }
+  store_entry<CV>(out, x, y);
 }
 
 // window base 2^(W w) * B (= entry d = 1 of window w), affine Montgomery form
@@ -653,7 +709,9 @@ __device__ void table_entry(uint32_t* out, const uint32_t* base, int d) {
   using Fp = typename CV::Fp;
   constexpr int L = Fp::L;
   JPt<Fp> P, acc;
-  affine_point<CV>(P, base, base + L);
+  uint32_t bx[L], by[L];
+  load_entry<CV>(base, bx, by);
+  affine_point<CV>(P, bx, by);
   acc.inf = true;
   for (int bit = W - 1; bit >= 0; --bit) {
     jdbl<CV>(acc, acc);
@@ -717,8 +775,14 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   dim3 g((unsigned)waves), b(WAVE);
   if (a.exc_reset) (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
   // tokens per thread for the batched inversion: keep >= ~8 waves per CU
+  // (CAPJWT_EC_WAVES_PER_CU: A/B of that target)
   const int64_t n = a.end - a.begin;
-  int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * 8 * WAVE)));
+  static const int wpc = [] {
+    const char* e = std::getenv("CAPJWT_EC_WAVES_PER_CU");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 8;
+  }();
+  int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * wpc * WAVE)));
   const int64_t S = (n + B - 1) / B;
   hipLaunchKernelGGL(k_ec_scalar_batch<CV>, dim3((unsigned)((S + WAVE - 1) / WAVE)), b, 0, s, a, B);
   mk("scalar");

@@ -178,12 +178,15 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a) {
   if (valid) {
     // zero the rows this token may leave unwritten (scratch is reused across
     // batches); an RSA key reads the rows of its own layout (rsa_sig_rows_l)
-    int zr = a.zrows;
+    int zr = a.zrows, r0 = 0;
     if (layout == LAY_BE) {
       const int nl = (int)a.keys[__builtin_amdgcn_readfirstlane(job_key(jb))].nlimbs;
       zr = min(zr, (28 * nl - 1) / 32 + 2);
+      if (fast) r0 = (int)DW;                          // rows [0, DW) are all written below
+    } else if (layout == LAY_SPLIT_BE && fast && (ks >> 2) == (uint32_t)a.ec_words) {
+      zr = 0;                                          // r and s fill every row the curve reads
     }
-    for (int r = 0; r < zr; ++r) {
+    for (int r = r0; r < zr; ++r) {
       // ECDSA reads r from rows [0, ec_words) and s from [EC_S_ROW, EC_S_ROW + ec_words) only
       if (layout == LAY_SPLIT_BE && ((r >= a.ec_words && r < EC_S_ROW) || r >= EC_S_ROW + a.ec_words)) continue;
       bool written = false;

@@ -152,29 +152,61 @@ SHD void sha256_mem(uint32_t h[8], const MemString& m) {
 }
 
 // ---------------------------------------------------------------- SHA-512/384
+// ch / maj of 64-bit words as two v_bitop3_b32 each (truth tables 0xCA, 0xE8)
+template <unsigned TT>
+SHD uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+  return ((uint64_t)__builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), TT)
+          << 32) |
+         __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, TT);
+}
+
+// One SHA-512 round on the state held in named registers (the caller rotates
+// the names, so no moves between rounds).
+#define SHA512_ROUND(a, b, c, d, e, f, g, h, k, wi)                                                    \
+  do {                                                                                                  \
+    const uint64_t t1_ = (h) + xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41)) +                   \
+                         bitop3_64<0xCA>(e, f, g) + (k) + (wi);                                         \
+    (d) += t1_;                                                                                         \
+    (h) = t1_ + xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39)) + bitop3_64<0xE8>(a, b, c);       \
+  } while (0)
+
+// 8 rounds starting at round i0 (a multiple of 8) with message words w[j0..j0+8)
+#define SHA512_8ROUNDS(i0, j0)                                                                   \
+  do {                                                                                          \
+    SHA512_ROUND(A, B, C, D, E, F, G, H, K512[(i0) + 0], w[(j0) + 0]);                          \
+    SHA512_ROUND(H, A, B, C, D, E, F, G, K512[(i0) + 1], w[(j0) + 1]);                          \
+    SHA512_ROUND(G, H, A, B, C, D, E, F, K512[(i0) + 2], w[(j0) + 2]);                          \
+    SHA512_ROUND(F, G, H, A, B, C, D, E, K512[(i0) + 3], w[(j0) + 3]);                          \
+    SHA512_ROUND(E, F, G, H, A, B, C, D, K512[(i0) + 4], w[(j0) + 4]);                          \
+    SHA512_ROUND(D, E, F, G, H, A, B, C, K512[(i0) + 5], w[(j0) + 5]);                          \
+    SHA512_ROUND(C, D, E, F, G, H, A, B, K512[(i0) + 6], w[(j0) + 6]);                          \
+    SHA512_ROUND(B, C, D, E, F, G, H, A, K512[(i0) + 7], w[(j0) + 7]);                          \
+  } while (0)
+
+// Rounds 16..79 run as four 16-round blocks of a rolled loop whose body is
+// fully unrolled: the schedule index (i & 15) is then static, so w[] stays in
+// registers.  (An 80-round #pragma unroll is past LLVM's unroll budget; it
+// unrolled partially and indexed w[] with s_set_gpr_idx moves on every access.)
 SHD void sha512_compress(uint64_t h[8], uint64_t w[16]) {
-  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  uint64_t A = h[0], B = h[1], C = h[2], D = h[3], E = h[4], F = h[5], G = h[6], H = h[7];
+  SHA512_8ROUNDS(0, 0);
+  SHA512_8ROUNDS(8, 8);
+#pragma unroll 1
+  for (int r = 16; r < 80; r += 16) {
 #pragma unroll
-  for (int i = 0; i < 80; ++i) {
-    uint64_t wi;
-    if (i < 16) {
-      wi = w[i];
-    } else {
-      const uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
       const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
       const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
-      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-      w[i & 15] = wi;
+      w[j] += s0 + w[(j + 9) & 15] + s1;
     }
-    const uint64_t S1 = xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
-    const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t t1 = hh + S1 + ch + K512[i] + wi;
-    const uint64_t S0 = xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
-    const uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    SHA512_8ROUNDS(r, 0);
+    SHA512_8ROUNDS(r + 8, 8);
   }
-  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  h[0] += A; h[1] += B; h[2] += C; h[3] += D; h[4] += E; h[5] += F; h[6] += G; h[7] += H;
 }
+#undef SHA512_8ROUNDS
+#undef SHA512_ROUND
 
 SHD void sha512_init(uint64_t h[8], bool is384) {
   if (is384) {

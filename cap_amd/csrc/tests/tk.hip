@@ -118,10 +118,11 @@ __global__ void k_tk_entry(const int* wd, uint32_t* out, int n) {
   if (i >= n) return;
   uint32_t gx[L], gy[L];
   mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
-  uint32_t base[2 * L];
+  uint32_t base[2 * L], ent[2 * L];
   constexpr int W = ec_comb_w(CV::CLS, true);
   window_base<CV, W>(base, gx, gy, wd[2 * i]);
-  table_entry<CV, W>(out + (size_t)i * 2 * L, base, wd[2 * i + 1]);
+  table_entry<CV, W>(ent, base, wd[2 * i + 1]);
+  load_entry<CV>(ent, out + (size_t)i * 2 * L, out + (size_t)i * 2 * L + L);   // table format -> x, y limbs
 }
 
 template <class CV>
