@@ -145,20 +145,13 @@ int cls_rows_scratch(int c, int l4) {
     default: return 0;
   }
 }
-// relative device time per token (1 x MI355X kernel times, profiles/r01_s4_*),
-// for splitting a batch over devices
-double cls_cost(int c) {
-  switch (c) {
-    case CLS_RSA2K: return 3.6;
-    case CLS_RSA3K: return 8.0;
-    case CLS_RSA4K: return 16.0;
-    case CLS_P256: return 1.0;
-    case CLS_P384: return 3.6;
-    case CLS_P521: return 8.4;
-    case CLS_ED25519: return 1.9;
-    default: return 0.01;
-  }
-}
+// Relative device time per token by kernel class (ES256 = 1): every class
+// alone as a resident batch filling one MI355X, summed kernel time per token
+// (tools/class_costs.py -> profiles/r03_class_costs.json).  cap_amd/shard.py
+// CLASS_COST holds the same numbers (tests/test_shard_dist.py compares them).
+// The RSA-4K+ entry is the 148-limb layout; 296- and 592-limb keys scale it
+// by (limbs / 148)^2 (the modexp's MADs grow with the square of the width).
+constexpr double CLS_COST[NCLS] = {0.01, 4.0, 9.0, 16.0, 1.0, 3.4, 9.0, 1.3};
 
 // Grow-only buffers reallocate with 50 % headroom (2 MiB granules): a pipeline
 // slot whose chunks vary in size and class mix (scratch rows per class) grows
@@ -1739,8 +1732,18 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
   if (nd > 1) {
     std::vector<double> pre(ntok + 1, 0.0);
     const size_t nk = ks->keys.size();
-    for (size_t i = 0; i < ntok; ++i)
-      pre[i + 1] = pre[i] + (toks[i].key_idx < nk ? cls_cost(classify(*ks, toks[i])) : 0.0);
+    for (size_t i = 0; i < ntok; ++i) {
+      double w = 0.0;
+      if (toks[i].key_idx < nk) {
+        const int c = classify(*ks, toks[i]);
+        w = CLS_COST[c];
+        if (c == CLS_RSA4K) {
+          const double r = ks->keys[toks[i].key_idx].nlimbs / 148.0;
+          w *= r * r;
+        }
+      }
+      pre[i + 1] = pre[i] + w;
+    }
     size_t j = 0;
     for (size_t k = 1; k < nd; ++k) {
       const double target = pre[ntok] * (double)k / (double)nd;

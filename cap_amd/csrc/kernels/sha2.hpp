@@ -152,22 +152,14 @@ SHD void sha256_mem(uint32_t h[8], const MemString& m) {
 }
 
 // ---------------------------------------------------------------- SHA-512/384
-// ch / maj of 64-bit words as two v_bitop3_b32 each (truth tables 0xCA, 0xE8)
-template <unsigned TT>
-SHD uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
-  return ((uint64_t)__builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), TT)
-          << 32) |
-         __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, TT);
-}
-
 // One SHA-512 round on the state held in named registers (the caller rotates
 // the names, so no moves between rounds).
 #define SHA512_ROUND(a, b, c, d, e, f, g, h, k, wi)                                                    \
   do {                                                                                                  \
     const uint64_t t1_ = (h) + xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41)) +                   \
-                         bitop3_64<0xCA>(e, f, g) + (k) + (wi);                                         \
+                         (((e) & (f)) ^ (~(e) & (g))) + (k) + (wi);                                         \
     (d) += t1_;                                                                                         \
-    (h) = t1_ + xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39)) + bitop3_64<0xE8>(a, b, c);       \
+    (h) = t1_ + xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39)) + (((a) & (b)) ^ ((a) & (c)) ^ ((b) & (c)));       \
   } while (0)
 
 // 8 rounds starting at round i0 (a multiple of 8) with message words w[j0..j0+8)

@@ -28,6 +28,32 @@ def test_shard_bounds_cover_and_balance():
     assert shard.shard_bounds([], 2) == [0, 0, 0]
 
 
+def test_cost_table_matches_the_runtime():
+    """cap_amd/shard.py CLASS_COST == jg_runtime.cpp CLS_COST (class order)"""
+    import re
+    src = open(os.path.join(ROOT, "cap_amd", "csrc", "jg_runtime.cpp")).read()
+    m = re.search(r"CLS_COST\[NCLS\]\s*=\s*\{([^}]*)\}", src)
+    vals = [float(x) for x in m.group(1).split(",")]
+    order = ["reject", "rsa2048", "rsa3072", "rsa4096", "p256", "p384", "p521", "ed25519"]
+    assert vals == [shard.CLASS_COST[c] for c in order]
+    assert shard.token_cost("RS256", 8192) == shard.CLASS_COST["rsa4096"] * 4
+    assert shard.token_cost("PS512", 16384) == shard.CLASS_COST["rsa4096"] * 16
+
+
+def test_sorted_eddsa_es384_batch_splits_into_equal_time():
+    """BASELINE configs[3]: a 50/50 EdDSA / ES384 batch sorted by alg (the
+    worst case for a count split: all ES384 in the back half) is cut so every
+    rank gets the same predicted device time, not the same token count."""
+    n = 100000
+    algs = ["EdDSA"] * (n // 2) + ["ES384"] * (n // 2)
+    costs = [shard.token_cost(a) for a in algs]
+    for world in (2, 4, 8):
+        b = shard.shard_bounds(costs, world)
+        t = [sum(costs[b[r]:b[r + 1]]) for r in range(world)]
+        assert max(t) - min(t) <= 2 * max(costs), (world, t)
+        assert b[1] > n // world          # the cheap EdDSA front gets more tokens than n / world
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
