@@ -74,7 +74,8 @@ def p256_point_mads_per_token(wq=None):
 
 # key comb-table width tiers, widest first (kernels/ecdsa.hpp EC_*_WQ, ed25519.hpp ED_WA)
 WIDTH_TIERS = {"p256": (26, 24, 22, 20), "p384": (24, 20, 18, 16), "ed25519": (20, 18, 16), "p521": (20, 18, 16)}
-_TAB = {"p256": (257, 80), "p384": (385, 128), "p521": (522, 160), "ed25519": (254, 128)}   # (bits + 1, entry bytes)
+# (bits + 1, entry bytes): P-256 entries are packed to 64 B (ecdsa.hpp JG_EC_PACK64)
+_TAB = {"p256": (257, 64), "p384": (385, 128), "p521": (522, 160), "ed25519": (254, 128)}
 
 
 def table_bytes(cls, w):
@@ -251,6 +252,8 @@ def bench_keys():
 def measure(ctx, arena, toks, steps, warmup, dist):
     from cap_amd import _lib
     from cap_amd.shard import max_over_ranks
+    global LAST_WINDOW
+    w0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
     h = ctypes.c_void_p()
     L = _lib.lib()
     rc = L.jg_batch_stage(ctx.h, 0, arena, len(arena), toks.ctypes.data_as(ctypes.POINTER(_lib.JgTok)), len(toks),
@@ -291,7 +294,15 @@ def measure(ctx, arena, toks, steps, warmup, dist):
         elapsed = max_over_ranks(elapsed, device=COLL_DEVICE)
     b.free()
     kms = {k: float(np.mean(x)) for k, x in times.items()}
+    # the batch's launches, for tools/cfg_roofline_check.py: every kernel of
+    # this batch ran `runs` times inside [start, end] (CLOCK_BOOTTIME, the
+    # clock of rocprofv3's timestamps)
+    LAST_WINDOW = {"boottime_ns": [w0, time.clock_gettime_ns(time.CLOCK_BOOTTIME)],
+                   "runs": 1 + max(1, warmup) + steps}
     return elapsed, accepted, kms, v
+
+
+LAST_WINDOW = None
 
 
 def h2d_bandwidth(nbytes, iters=5):
@@ -622,7 +633,7 @@ def config_line(ctx, name, workload, pool, algs, keyidx, expected_good, per_gpu,
     want = int(np.tile(expected_good, reps)[:per_gpu].sum())
     line = {"workload": workload, "value": world * per_gpu * steps / el, "unit": "verified JWTs/s",
             "ms_per_step": el * 1000.0 / steps, "tokens_per_gpu": per_gpu, "unique_pool": len(pool),
-            "accepted": acc, "expected_accepted": want, "kernel_ms": kms}
+            "accepted": acc, "expected_accepted": want, "kernel_ms": kms, "trace_window": LAST_WINDOW}
     if acc != want:
         line["error"] = f"accepted {acc} != expected {want}"
     if kernels:
@@ -731,7 +742,8 @@ def run_configs(ctx, args, threads, rank, world, dist):
     st["workload"] = f"{share} tokens per GPU (10M / 8) streamed with H2D"
     line["stream"] = st
     del arena, toks
-    line["refresh"] = measure_refresh(ctx, meta, args.c5_table_budget_gb + 40)
+    if not args.no_refresh:
+        line["refresh"] = measure_refresh(ctx, meta, args.c5_table_budget_gb + 40)
     out["mixed_10alg_32kid"] = line
     C5_E2E.update(pool=pool, good=good, meta=meta)
     return out
@@ -849,6 +861,8 @@ def main():
     ap.add_argument("--c5-legacy-pool", dest="c5_unique", action="store_false",
                     help="configs[4] from 1024 unique tokens per kid (round-2 layout)")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-refresh", action="store_true", help="skip configs[4]'s JWKS refresh timings "
+                    "(profiling passes: they build key tables)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--table-budget-gb", type=float, default=110.0,
@@ -948,6 +962,20 @@ def main():
         result["error"] = f"only {acc}/{ntok} valid tokens accepted"
     if rank == 0 and world == 1:
         result["pcie"] = measure_pcie(ctx, arena, toks)
+    # the same batch at the library's default table budget (what a caller gets
+    # without jg_set_table_budget): the 4 kids' key tables at W = 24
+    if not args.no_ab and budget != (32 << 30):
+        ctx.set_table_budget(32 << 30)
+        ctx.load_keys(abi_keys(kids))
+        wdef = min(ctx.table_widths())
+        eld, accd, kmsd, _ = measure(ctx, arena, toks, max(1, args.steps // 2), 1, dist)
+        result["default_budget"] = {"table_budget_GiB": 32, "p256_key_comb_w": wdef,
+                                    "value": world * ntok * max(1, args.steps // 2) / eld, "kernel_ms": kmsd,
+                                    "accepted": accd,
+                                    "note": "same 1M-token batch with the library's default 32 GiB key-table budget "
+                                            "(no jg_set_table_budget call); `value` above uses the bench's budget"}
+        ctx.set_table_budget(budget)
+        ctx.load_keys(abi_keys(kids))
     del arena, toks
     # A/B: the same batch built from a 131072-token pool replicated 8x (round-1 default)
     if not args.no_ab and npool > (1 << 17):

@@ -150,8 +150,10 @@ int cls_rows_scratch(int c, int l4) {
 // (tools/class_costs.py -> profiles/r03_class_costs.json).  cap_amd/shard.py
 // CLASS_COST holds the same numbers (tests/test_shard_dist.py compares them).
 // The RSA-4K+ entry is the 148-limb layout; 296- and 592-limb keys scale it
-// by (limbs / 148)^2 (the modexp's MADs grow with the square of the width).
-constexpr double CLS_COST[NCLS] = {0.01, 4.0, 9.0, 16.0, 1.0, 3.4, 9.0, 1.3};
+// by (limbs / 148)^2 (the modexp's MADs grow with the square of the width;
+// measured 4.1x and 17.5x).  RSA entries average the PKCS#1 and PSS forms
+// (RS256 3.94 / PS256 4.50, RS512 15.0 / PS512 16.0).
+constexpr double CLS_COST[NCLS] = {0.01, 4.2, 9.0, 15.5, 1.0, 3.4, 6.6, 1.1};
 
 // Grow-only buffers reallocate with 50 % headroom (2 MiB granules): a pipeline
 // slot whose chunks vary in size and class mix (scratch rows per class) grows
@@ -208,12 +210,18 @@ struct HostKey {
 // Device memory with shared ownership.  Comb tables are shared by key content
 // between key loads (a JWKS refresh that keeps a key keeps its table: no copy,
 // no rebuild), and a load's key blob is shared by its later width upgrades.
-// Freed when the last holder lets go; hipFree waits for the device's streams,
-// so a generation still referenced by queued kernels is never freed under them.
+// Stream-ordered (hipMallocAsync / hipFreeAsync on the key streams): a
+// generation is released only once no queued work can reference it (pipeline
+// slots hold their key state until their chunk has completed, resident
+// batches until the next run or jg_batch_free), and the release must not wait
+// for the device -- hipFree synchronises every stream, so dropping an old key
+// table would stall behind a background comb-table build (~1 s) or the
+// verification pipeline.
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
   int dev = 0;
+  hipStream_t s = nullptr;        // the stream it was allocated on (and is freed on)
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
@@ -222,7 +230,7 @@ struct DevBuf {
     int cur = 0;
     const bool had = hipGetDevice(&cur) == hipSuccess;
     (void)hipSetDevice(dev);
-    (void)hipFree(p);
+    (void)hipFreeAsync(p, s);
     if (had) (void)hipSetDevice(cur);
   }
   template <class T>
@@ -232,7 +240,7 @@ using DevBufP = std::shared_ptr<DevBuf>;
 
 // hipMalloc into a DevBuf.  `fail` (jg_debug_fail_alloc): a countdown of
 // allocations after which one fails as if the device were out of memory.
-DevBufP dev_alloc(int dev, size_t bytes, std::atomic<int>* fail = nullptr) {
+DevBufP dev_alloc(int dev, hipStream_t s, size_t bytes, std::atomic<int>* fail = nullptr) {
   if (fail) {
     int f = fail->load();
     while (f > 0 && !fail->compare_exchange_weak(f, f - 1)) {}
@@ -240,9 +248,10 @@ DevBufP dev_alloc(int dev, size_t bytes, std::atomic<int>* fail = nullptr) {
   }
   auto b = std::make_shared<DevBuf>();
   b->dev = dev;
+  b->s = s;
   b->bytes = std::max<size_t>(bytes, 16);
   HIPCHK(hipSetDevice(dev));
-  HIPCHK(hipMalloc(&b->p, b->bytes));
+  HIPCHK(hipMallocAsync(&b->p, b->bytes, s));
   return b;
 }
 
@@ -1441,6 +1450,8 @@ constexpr uint64_t HBM_RESERVE = uint64_t(2) << 30;
 uint64_t free_hbm(int dev) {
   size_t fr = 0, tot = 0;
   HIPCHK(hipSetDevice(dev));
+  hipMemPool_t pool = nullptr;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) (void)hipMemPoolTrimTo(pool, 0);   // released tables
   HIPCHK(hipMemGetInfo(&fr, &tot));
   return fr;
 }
@@ -1488,8 +1499,8 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   g->mirror = S.dk;
   g->kw.assign(nk, 0);
   ensure_tables(d, S);
-  g->dkeys = dev_alloc(d->id, sizeof(DevKey) * std::max<size_t>(nk, 1), &ctx->fail_alloc);
-  g->blob = dev_alloc(d->id, sizeof(uint32_t) * std::max<size_t>(S.blob.size(), 4), &ctx->fail_alloc);
+  g->dkeys = dev_alloc(d->id, s, sizeof(DevKey) * std::max<size_t>(nk, 1), &ctx->fail_alloc);
+  g->blob = dev_alloc(d->id, s, sizeof(uint32_t) * std::max<size_t>(S.blob.size(), 4), &ctx->fail_alloc);
   // key prep index lists: p256 | p384 | p521 | ed
   std::vector<int32_t> idx;
   size_t at[4];
@@ -1499,7 +1510,7 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   }
   at[3] = idx.size();
   idx.insert(idx.end(), S.ed_idx.begin(), S.ed_idx.end());
-  DevBufP didx = dev_alloc(d->id, sizeof(int32_t) * std::max<size_t>(idx.size() + nk, 1), &ctx->fail_alloc);
+  DevBufP didx = dev_alloc(d->id, s, sizeof(int32_t) * std::max<size_t>(idx.size() + nk, 1), &ctx->fail_alloc);
   int32_t* di = didx->as<int32_t>();
   DevKey* dk = g->keys();
   uint32_t* blob = g->keyblob();
@@ -1569,7 +1580,7 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   }
   std::map<std::pair<int, int>, std::vector<int32_t>> groups;
   std::map<std::string, int32_t> first;          // one build per distinct (id, width)
-  for (auto& f : fresh) f.second.buf = dev_alloc(d->id, table_bytes(f.second.cls, f.second.w), &ctx->fail_alloc);
+  for (auto& f : fresh) f.second.buf = dev_alloc(d->id, s, table_bytes(f.second.cls, f.second.w), &ctx->fail_alloc);
   for (const auto& u : use) {
     const Req& r = fresh.at(u.second);
     const size_t i = u.first;
@@ -1591,8 +1602,10 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
 }
 
 void upload_cls(jg_ctx* ctx, Device* d, DevGen& g, const std::vector<uint8_t>& cls_tab) {
-  g.dcls = dev_alloc(d->id, std::max<size_t>(cls_tab.size(), 16), &ctx->fail_alloc);
-  if (!cls_tab.empty()) HIPCHK(hipMemcpy(g.dcls->p, cls_tab.data(), cls_tab.size(), hipMemcpyHostToDevice));
+  g.dcls = dev_alloc(d->id, d->kstream, std::max<size_t>(cls_tab.size(), 16), &ctx->fail_alloc);
+  if (!cls_tab.empty())
+    HIPCHK(hipMemcpyAsync(g.dcls->p, cls_tab.data(), cls_tab.size(), hipMemcpyHostToDevice, d->kstream));
+  HIPCHK(hipStreamSynchronize(d->kstream));
 }
 
 // CAPJWT_TABLES_SYNC=1: jg_keys_load builds every comb table at its budgeted
@@ -1646,12 +1659,12 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
     }
     HIPCHK(hipSetDevice(d->id));
     const DevGen& G = *cur->dev[i];
-    DevBufP t = dev_alloc(d->id, table_bytes(cls, w));
+    DevBufP t = dev_alloc(d->id, d->ustream, table_bytes(cls, w));
     // a one-record key array pointing at the new table (the blob is the generation's)
     DevKey rec = G.mirror[k];
     rec.tab = (uint64_t)(uintptr_t)t->p;
     rec.tab_w = w;
-    DevBufP tmp = dev_alloc(d->id, sizeof(DevKey) + 16);
+    DevBufP tmp = dev_alloc(d->id, d->ustream, sizeof(DevKey) + 16);
     const int32_t zero = 0;
     HIPCHK(hipMemcpyAsync(tmp->p, &rec, sizeof(DevKey), hipMemcpyHostToDevice, d->ustream));
     HIPCHK(hipMemcpyAsync((char*)tmp->p + sizeof(DevKey), &zero, sizeof zero, hipMemcpyHostToDevice, d->ustream));
@@ -1684,9 +1697,11 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
     if (!hit) continue;
     any = true;
     g->tabs.push_back(built[i]);
-    g->dkeys = dev_alloc(d->id, sizeof(DevKey) * std::max<size_t>(g->mirror.size(), 1));
+    g->dkeys = dev_alloc(d->id, d->ustream, sizeof(DevKey) * std::max<size_t>(g->mirror.size(), 1));
     if (!g->mirror.empty())
-      HIPCHK(hipMemcpy(g->dkeys->p, g->mirror.data(), sizeof(DevKey) * g->mirror.size(), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpyAsync(g->dkeys->p, g->mirror.data(), sizeof(DevKey) * g->mirror.size(), hipMemcpyHostToDevice,
+                            d->ustream));
+    HIPCHK(hipStreamSynchronize(d->ustream));
     ns->dev[i] = g;
   }
   if (any) ctx->publish(ns);
@@ -1855,6 +1870,7 @@ void jg_destroy(jg_ctx* ctx) {
     d->qcv.notify_all();
     if (d->worker.joinable()) d->worker.join();
   }
+  ctx->publish(nullptr);                           // key generations: freed on the key streams
   for (auto& d : ctx->devs) {
     (void)hipSetDevice(d->id);
     for (auto& l : d->lanes) l.destroy();
@@ -1890,7 +1906,6 @@ void jg_destroy(jg_ctx* ctx) {
     }
     d->lane0.destroy();
   }
-  ctx->publish(nullptr);                           // key generations: device memory freed here
   delete ctx;
 }
 
@@ -2063,6 +2078,7 @@ void run_resident(jg_ctx* ctx, jg_batch* b, bool timed) {
   b->timing = timed;
   b->marks_used = 0;
   run_plan(b->dev, *ks, *ks->dev[b->dslot], b->lane, b->b, b->plan, b);
+  if (b->ks_run && b->ks_run != ks) HIPCHK(hipStreamSynchronize(b->lane->stream));   // its kernels may read the old state
   b->ks_run = std::move(ks);
 }
 }  // namespace

@@ -29,12 +29,17 @@ struct EcArgs {
 constexpr int ec_limbs(int cls) { return cls == jgk::CLS_P256 ? 10 : cls == jgk::CLS_P384 ? 15 : 20; }
 // 32-bit words of r (and of s) as prep leaves them: ceil(coordinate bytes / 4)
 constexpr int ec_sig_words(int cls) { return cls == jgk::CLS_P256 ? 8 : cls == jgk::CLS_P384 ? 12 : 17; }
-// P-256 entries packed to 64 bytes (JG_EC_PACK64): x and y as 8 32-bit words
-// each (canonical Montgomery values < p < 2^256), unpacked to 28-bit limbs on
-// load -- a 64-B-aligned entry touches one 128-B line where the 80-B limb form
-// touched 1.5 on average.  Other curves keep the limb form.
+// P-256 entries packed to 64 bytes (JG_EC_PACK64, default on): x and y as 8
+// 32-bit words each (canonical Montgomery values < p < 2^256), unpacked to
+// 28-bit limbs on load (~2 VALU per limb).  A 64-B-aligned entry touches one
+// 128-B line where the 80-B limb form touched 1.5 on average, and every P-256
+// table is 20 % smaller (generator W = 26: 21.5 GB, a W = 26 key 21.5 GB, W =
+// 24 5.9 GB, W = 22 1.6 GB, W = 20 436 MB).  Measured: point kernel -0.6 %
+// (profiles/r03_s4_ab.json; the same A/B with every gather confined to 256
+// entries bounds what gather traffic costs at all: -7 %).  Other curves keep
+// the limb form (P-384's 128-B stride is already line-aligned).
 #ifndef JG_EC_PACK64
-#define JG_EC_PACK64 0
+#define JG_EC_PACK64 1
 #endif
 constexpr bool ec_packed(int cls) { return JG_EC_PACK64 && cls == jgk::CLS_P256; }
 constexpr int ec_stride(int cls) { return ec_packed(cls) ? 16 : (2 * ec_limbs(cls) + 3) & ~3; }

@@ -15,8 +15,8 @@ import numpy as np
 # profiles/r03_class_costs.json).  The same table as jg_runtime.cpp CLS_COST,
 # in its class order (reject, rsa2048, rsa3072, rsa4096, p256, p384, p521,
 # ed25519); tests/test_shard_dist.py checks they agree.
-CLASS_COST = {"reject": 0.01, "rsa2048": 4.0, "rsa3072": 9.0, "rsa4096": 16.0, "p256": 1.0, "p384": 3.4,
-              "p521": 9.0, "ed25519": 1.3}
+CLASS_COST = {"reject": 0.01, "rsa2048": 4.2, "rsa3072": 9.0, "rsa4096": 15.5, "p256": 1.0, "p384": 3.4,
+              "p521": 6.6, "ed25519": 1.1}
 
 
 def rsa_class(bits):

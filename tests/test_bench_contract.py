@@ -20,11 +20,13 @@ def _header_tiers():
 def test_p256_width_tiers_match_the_library():
     assert _header_tiers() == [26, 24, 22, 20]
     # the documented cut-offs (jg.h)
-    assert bench.p256_key_w(4, 110 * GiB) == 26
-    assert bench.p256_key_w(5, 110 * GiB) == 24
+    # 64-B packed entries (ecdsa.hpp JG_EC_PACK64): W = 26 is 21.5 GB per key
+    assert bench.table_bytes("p256", 26) == 10 * (1 << 25) * 64
+    assert bench.p256_key_w(5, 110 * GiB) == 26
+    assert bench.p256_key_w(6, 110 * GiB) == 24
     assert bench.p256_key_w(4, 32 * GiB) == 24
-    assert bench.p256_key_w(17, 32 * GiB) == 22
-    assert bench.p256_key_w(18, 32 * GiB) == 20
+    assert bench.p256_key_w(21, 32 * GiB) == 22
+    assert bench.p256_key_w(22, 32 * GiB) == 20
     assert bench.p256_key_w(1, 0) == 20
 
 

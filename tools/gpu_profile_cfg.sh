@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=${1:-cfg}
 O=gpurun_out/$TAG
 mkdir -p "$O"
-ARGS="--configs-only --steps 4 --warmup 1 --no-ab"
+ARGS="--configs-only --steps 4 --warmup 1 --no-ab --no-refresh"
 echo "[0/5] class costs $(date +%T)"
 timeout -k 10 300 python3 tools/class_costs.py "$O/class_costs.json" > "$O/class_costs.log" 2>&1 || { echo COSTS_FAIL; tail -20 "$O/class_costs.log"; exit 1; }
 echo "[1/5] bench configs $(date +%T)"
@@ -22,5 +22,7 @@ echo "[4/5] WRITE_SIZE $(date +%T)"
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$O/write" -o w --output-format csv -- python3 bench.py $ARGS > "$O/write.json" 2> "$O/write.err" || { echo WRITE_FAIL; tail -20 "$O/write.err"; exit 1; }
 echo "[5/5] SQ $(date +%T)"
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$O/sq" -o sq --output-format csv -- python3 bench.py $ARGS > "$O/sq.json" 2> "$O/sq.err" || { echo SQ_FAIL; tail -20 "$O/sq.err"; exit 1; }
+echo "[6/6] roofline check $(date +%T)"
+python3 tools/cfg_roofline_check.py "$O" "$O/roofline_check.json" || { echo CHECK_FAIL; exit 1; }
 echo "done $(date +%T)"
 find "$O" -name "*.csv" | head -40
