@@ -252,8 +252,7 @@ def bench_keys():
 def measure(ctx, arena, toks, steps, warmup, dist):
     from cap_amd import _lib
     from cap_amd.shard import max_over_ranks
-    global LAST_WINDOW
-    w0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
+    global LAST_WINDOW, LAST_SYNC_MS
     h = ctypes.c_void_p()
     L = _lib.lib()
     rc = L.jg_batch_stage(ctx.h, 0, arena, len(arena), toks.ctypes.data_as(ctypes.POINTER(_lib.JgTok)), len(toks),
@@ -266,10 +265,13 @@ def measure(ctx, arena, toks, steps, warmup, dist):
     pinned = _lib.PinnedBuffer(len(toks))
     # per-kernel device times: average over synchronous runs (the warmup)
     times = {}
+    w0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
     for _ in range(max(1, warmup)):
         b.run(want_verdicts=True)
         for name, ms in b.kernel_times():
             times.setdefault(name, []).append(ms)
+    w1 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
+    LAST_SYNC_MS = {k: float(np.mean(x)) for k, x in times.items()}
     if dist:
         import torch
         import torch.distributed as td
@@ -294,15 +296,15 @@ def measure(ctx, arena, toks, steps, warmup, dist):
         elapsed = max_over_ranks(elapsed, device=COLL_DEVICE)
     b.free()
     kms = {k: float(np.mean(x)) for k, x in times.items()}
-    # the batch's launches, for tools/cfg_roofline_check.py: every kernel of
-    # this batch ran `runs` times inside [start, end] (CLOCK_BOOTTIME, the
-    # clock of rocprofv3's timestamps)
-    LAST_WINDOW = {"boottime_ns": [w0, time.clock_gettime_ns(time.CLOCK_BOOTTIME)],
-                   "runs": 1 + max(1, warmup) + steps}
+    # the synchronous runs' launches, for tools/cfg_roofline_check.py: every
+    # kernel of this batch ran `runs` times inside [start, end] (CLOCK_BOOTTIME,
+    # the clock of rocprofv3's timestamps)
+    LAST_WINDOW = {"boottime_ns": [w0, w1], "runs": max(1, warmup)}
     return elapsed, accepted, kms, v
 
 
 LAST_WINDOW = None
+LAST_SYNC_MS = None
 
 
 def h2d_bandwidth(nbytes, iters=5):
@@ -628,12 +630,19 @@ def config_line(ctx, name, workload, pool, algs, keyidx, expected_good, per_gpu,
     class's tokens -- by alg family, or by `class_of_key[key index]` (kernel
     class name per key) where keys of one family fall into several classes."""
     arena, toks = pack(pool, algs, keyidx, per_gpu)
-    el, acc, kms, v = measure(ctx, arena, toks, steps, warmup, dist)
+    el, acc, _, v = measure(ctx, arena, toks, steps, warmup, dist)
+    # per-class kernel times from the synchronous runs of the batch: in the
+    # timed region steps are pipelined, so a class kernel there shares the
+    # chip with the previous step's kernels and its duration is no roofline
+    # time (round 3: C5's P-256 point ran 0.12 ms alone, 0.37-0.50 ms
+    # overlapped -- profiles/r03_s5_cfg_roofline_check.json)
+    kms = LAST_SYNC_MS
     reps = (per_gpu + len(pool) - 1) // len(pool)
     want = int(np.tile(expected_good, reps)[:per_gpu].sum())
     line = {"workload": workload, "value": world * per_gpu * steps / el, "unit": "verified JWTs/s",
             "ms_per_step": el * 1000.0 / steps, "tokens_per_gpu": per_gpu, "unique_pool": len(pool),
-            "accepted": acc, "expected_accepted": want, "kernel_ms": kms, "trace_window": LAST_WINDOW}
+            "accepted": acc, "expected_accepted": want, "kernel_ms": kms,
+            "kernel_ms_from": "synchronous runs of the batch (bench warmup), one at a time", "trace_window": LAST_WINDOW}
     if acc != want:
         line["error"] = f"accepted {acc} != expected {want}"
     if kernels:

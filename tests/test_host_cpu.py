@@ -314,7 +314,7 @@ def test_json_mutation_fuzz():
     rnd = random.Random(11)
     seeds = [d for d in JSON_DOCS if len(d) > 1] + [
         b'{"aud":["www.example.com"],"exp":1611699344,"iat":1611699284,"iss":"https://example.com/",'
-        b'"jti":"7","nbf":1611699284,"sub":"alice@example.com","n":[1.5e3,-0,null,true,{"x":"\u00e9"}]}']
+        b'"jti":"7","nbf":1611699284,"sub":"alice@example.com","n":[1.5e3,-0,null,true,{"x":"\\u00e9"}]}']
     alpha = list(b'{}[]":,.-+0123456789eE\\u tnrfal\x00\x7f\xc3\xa9\xed\xa0\xff')
     for _ in range(2000 * FUZZ):
         doc = _mutate_bytes(rnd, rnd.choice(seeds), alpha)

@@ -2,7 +2,8 @@
 (VERDICT r02 item 1): for every `configs.<name>.roofline.<mark>` of the bench
 line, the launches of that mark's kernel(s) inside the config's
 `trace_window` (bench.py measure(): CLOCK_BOOTTIME, the clock of rocprofv3's
-timestamps; `runs` executions of the resident batch) give
+timestamps, around the `runs` synchronous runs of the resident batch whose
+HIP-event times bench.py's config rooflines use) give
 
   rocprof ms per run  = summed kernel-trace durations / runs
   rocprof frac        = bench frac x bench ms / rocprof ms   (same work per run)
@@ -41,7 +42,7 @@ MARKS = {
     "rsa3072_modexp": ["void (anonymous namespace)::k_rsa_modexp<28, 4, 8>"],
     "rsa4096_modexp": ["void (anonymous namespace)::k_rsa_modexp<37, 4, 8>"],
     "rsa4096_prep": ["void (anonymous namespace)::k_prep<1, ", "(anonymous namespace)::k_prep_mid("],
-    "rsa4096_pad": ["(anonymous namespace)::k_rsa_pad<"],
+    "rsa4096_pad": ["void (anonymous namespace)::k_rsa_pad<"],
 }
 # marks reported beside the roofline ones (no roofline in bench.py)
 EXTRA = {"eddsa_es384_mixed": ["ed25519_finish"], "ps512_rsa4096": ["rsa4096_pad"]}
