@@ -73,7 +73,7 @@ def p256_point_mads_per_token(wq=None):
 
 
 # key comb-table width tiers, widest first (kernels/ecdsa.hpp EC_*_WQ, ed25519.hpp ED_WA)
-WIDTH_TIERS = {"p256": (26, 24, 22, 20), "p384": (24, 20, 18, 16), "ed25519": (20, 18, 16), "p521": (20, 18, 16)}
+WIDTH_TIERS = {"p256": (26, 24, 22, 20), "p384": (24, 20, 18, 16), "ed25519": (24, 22, 20, 18, 16), "p521": (20, 18, 16)}
 # (bits + 1, entry bytes): P-256 entries are packed to 64 B (ecdsa.hpp JG_EC_PACK64)
 _TAB = {"p256": (257, 64), "p384": (385, 128), "p521": (522, 160), "ed25519": (254, 128)}
 
@@ -147,16 +147,16 @@ def p384_point_mads_per_token(wq=None, nkeys=1):
     return ec_point_mads_per_token(15, 4, 5, 20, wq or p384_key_w(nkeys, P384_BUDGET), 384, 15 * 12, merged=False)
 
 
-def ed25519_point_mads_per_token(wa=20):
-    """k_ed_point: 13 comb windows of the base point (W = 20) + ceil(254 / wa)
-    of the key (ed25519.hpp ed_key_w: W = 20 / 18 / 16 by the table budget, 20
-    for config 3's single key), each a Niels addition of 7 field products
-    (ed25519.hip add_niels); p = 2^255 - 19 is reduced with 2 MADs per row
-    (mp.hpp mont_reduce_25519): a product is L^2 + 2L = 120 MADs.  Plus
-    k = H mod L (one reduction + one product mod L)."""
+def ed25519_point_mads_per_token(wa=24):
+    """k_ed_point: 11 comb windows of the base point (W = 24) + ceil(254 / wa)
+    of the key (ed25519.hpp ED_WA: W = 24 / 22 / 20 / 18 / 16 by the table
+    budget), each a Niels addition of 7 field products (ed25519.hip
+    add_niels); p = 2^255 - 19 is reduced with 2 MADs per row (mp.hpp
+    mont_reduce_25519): a product is L^2 + 2L = 120 MADs.  Plus k = H mod L
+    (one reduction + one product mod L)."""
     L = 10
     mul = L * L + 2 * L
-    adds = 13 * (1 - 2.0 ** -20) + -(-254 // wa) * (1 - 2.0 ** -wa)
+    adds = 11 * (1 - 2.0 ** -24) + -(-254 // wa) * (1 - 2.0 ** -wa)
     return adds * 7 * mul + 220
 
 
@@ -712,7 +712,7 @@ def run_configs(ctx, args, threads, rank, world, dist):
     # configs[4]: all 10 algs, 32 kids, ~5 % tampered; the 10M stream in 256k-token chunks (one chunk per step)
     meta = bench_keys()
     # one table budget over every curve (jg_set_table_budget): enough for the
-    # 32 kids' widest tiers (P-256 W = 26, P-384 24, P-521 20, Ed25519 20: 171 GB)
+    # 32 kids' widest tiers (P-256 W = 26, P-384 24, Ed25519 24, P-521 20: 171.0 GB of 171.8)
     ctx.set_table_budget(int(args.c5_table_budget_gb * (1 << 30)))
     ctx.load_keys([m[3] for m in meta])
     c5w = ctx.table_widths()

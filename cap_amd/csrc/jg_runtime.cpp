@@ -1246,10 +1246,10 @@ uint64_t blob_alloc(std::vector<uint32_t>& blob, size_t words) {
 // width tiers of a table class, widest first (ecdsa.hpp EC_*_WQ, ed25519.hpp ED_WA)
 std::vector<int> width_tiers(int c) {
   switch (c) {
-    case CLS_P256: return {EC_P256_WQ, EC_P256_WQ + 4};
-    case CLS_P384: return {EC_P384_WQ, EC_P384_WQ + 4};
-    case CLS_P521: return {EC_P521_WQ, EC_P521_WQ + 3};
-    case CLS_ED25519: return {ED_WA, ED_WA + 3};
+    case CLS_P256: return {std::begin(EC_P256_WQ), std::end(EC_P256_WQ)};
+    case CLS_P384: return {std::begin(EC_P384_WQ), std::end(EC_P384_WQ)};
+    case CLS_P521: return {std::begin(EC_P521_WQ), std::end(EC_P521_WQ)};
+    case CLS_ED25519: return {std::begin(ED_WA), std::end(ED_WA)};
     default: return {};
   }
 }

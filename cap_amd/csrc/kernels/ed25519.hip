@@ -394,9 +394,13 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   if (waves <= 0) return;
   dim3 g((unsigned)waves), b(WAVE);
-  if (a.wa == 20) hipLaunchKernelGGL(k_ed_point<20>, g, b, 0, s, a);
-  else if (a.wa == 18) hipLaunchKernelGGL(k_ed_point<18>, g, b, 0, s, a);
-  else hipLaunchKernelGGL(k_ed_point<16>, g, b, 0, s, a);
+  switch (a.wa) {
+    case 24: hipLaunchKernelGGL(k_ed_point<24>, g, b, 0, s, a); break;
+    case 22: hipLaunchKernelGGL(k_ed_point<22>, g, b, 0, s, a); break;
+    case 20: hipLaunchKernelGGL(k_ed_point<20>, g, b, 0, s, a); break;
+    case 18: hipLaunchKernelGGL(k_ed_point<18>, g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL(k_ed_point<16>, g, b, 0, s, a); break;
+  }
   mk("point");
   // tokens per thread for the batched inversion: keep >= ~8 waves per CU
   const int64_t n = a.end - a.begin;
@@ -422,9 +426,13 @@ void launch_ed_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, 
 
 void launch_ed_keytables(int wa, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
   if (tn <= 0) return;
-  if (wa == 20) ed_tables<20>(keys, blob, tidx, tn, s);
-  else if (wa == 18) ed_tables<18>(keys, blob, tidx, tn, s);
-  else ed_tables<16>(keys, blob, tidx, tn, s);
+  switch (wa) {
+    case 24: ed_tables<24>(keys, blob, tidx, tn, s); break;
+    case 22: ed_tables<22>(keys, blob, tidx, tn, s); break;
+    case 20: ed_tables<20>(keys, blob, tidx, tn, s); break;
+    case 18: ed_tables<18>(keys, blob, tidx, tn, s); break;
+    default: ed_tables<16>(keys, blob, tidx, tn, s); break;
+  }
 }
 
 void launch_ed_btable(uint32_t* tab, hipStream_t s) {

@@ -19,25 +19,25 @@ struct EdArgs {
                               // k_ed_finish's prefix products
   const uint32_t* btab;       // comb table of the base point B (Niels form)
   int64_t npad, begin, end;
-  int32_t wa;                 // comb width of the launch's key tables (ED_WA: 20 / 18 / 16)
+  int32_t wa;                 // comb width of the launch's key tables (ED_WA)
 };
 
 constexpr int ED_L = 10;
 constexpr int ED_STRIDE = 32;                   // 3 x 10 limbs, padded to 16 B
 // Signed-digit comb geometry (as ecdsa.hpp): scalars S, k < L < 2^253, so
 // ceil(254 / W) windows.  The base point's table is shared by all keys and gets
-// the wider window: B W=20 (13 windows, 872 MB), keys W=16 (16 windows, 67 MB
-// each) -> 29 additions per token (66 at W=8).
-// Key tables take a wider window when few keys share the context's table
-// budget (ED_WA, picked with the EC tiers of ecdsa.hpp): W = 20 (13 windows, 872 MB per
-// key: 26 additions per token), 18 (15 windows, 252 MB), 16 (16, 67 MB).
-constexpr int ed_comb_w(bool base) { return base ? 20 : 16; }
+// the widest window: B W = 24 (11 windows, 11.8 GB).  Key tables take the
+// widest tier the context's table budget allows (ED_WA, picked with the EC
+// tiers of ecdsa.hpp, jg_runtime.cpp key_widths): W = 24 (11 windows, 11.8 GB
+// per key: 22 additions per token), 22 (12, 3.2 GB), 20 (13, 872 MB), 18 (15,
+// 252 MB), 16 (16, 67 MB).  Round 2 stopped at W = 20 for both (26 additions).
+constexpr int ed_comb_w(bool base) { return base ? 24 : 16; }
 constexpr int ed_windows_w(int w) { return (253 + 1 + w - 1) / w; }
 constexpr int ed_entries(bool base) { return 1 << (ed_comb_w(base) - 1); }
 constexpr int ed_windows(bool base) { return ed_windows_w(ed_comb_w(base)); }
 constexpr int64_t ed_table_words_w(int w) { return (int64_t)ed_windows_w(w) * (1 << (w - 1)) * ED_STRIDE; }
 constexpr int64_t ed_table_words(bool base) { return ed_table_words_w(ed_comb_w(base)); }
-constexpr int ED_WA[3] = {20, 18, 16};   // key-table width tiers, widest first (budget: jg_runtime.cpp key_widths)
+constexpr int ED_WA[5] = {24, 22, 20, 18, 16};   // key-table width tiers, widest first
 constexpr int ED_MAX_KEYS = 256;
 
 void launch_ed(const EdArgs& a, hipStream_t s, const jgk::Marker& mk);

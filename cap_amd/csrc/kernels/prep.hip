@@ -9,7 +9,7 @@
 // each 128-byte window of the strings, the wave copies 33 dwords of every one
 // of its 64 tokens (two tokens per load instruction, each half-wave reading
 // 128 contiguous bytes) into a per-token LDS slot, then each lane reads its own
-// slot.  A lane-per-token walk over the arena instead makes every load
+// slot.  The loads of window c + 1 are issued before window c is hashed.  A lane-per-token walk over the arena instead makes every load
 // instruction touch 64 different cache lines (prep ran at ~0.4 TB/s that way:
 // L1 thrash, one L2 request per lane per dword).
 #include <hip/hip_runtime.h>
@@ -51,10 +51,22 @@ __device__ __forceinline__ int es_size(int alg) { return alg == 7 ? 32 : alg == 
 // layout of the decoded signature in the scratch rows
 enum Layout { LAY_BE = 0, LAY_SPLIT_BE = 1, LAY_LE = 2 };
 
-// Every lane names the arena dword index `w` where its window starts; the wave
-// copies dwords [w, w+33) of all 64 windows into slot[lane][0..33).  Called in
-// wave-uniform control flow only (one block == one wave; every lane copies
-// words of other lanes' windows).
+// Window c of token t's stream = arena dwords [base[t] + woff, + 33) with
+// woff = WIN c - skip (skip > 0 only past window 0 of Ed25519's hash stream,
+// whose first window carries the 16-word register prefix), or woff = 0 once
+// the token needs no more windows (nw[t] <= c: it re-reads its first window
+// instead of running past the arena).  fetch() loads this lane's share of the
+// wave's 64 windows into registers -- dword k = lane % 32 of tokens 2i + lane
+// / 32, plus dword 32 of its own -- so that the next window's loads are in
+// flight while the current one is hashed (issued one window ahead: prep was
+// ~40 % parked on memory with load -> barrier -> compute; prep_body's PF);  put() moves them
+// into the LDS slots.  Both in wave-uniform control flow only (one block ==
+// one wave; every lane carries words of other lanes' windows).
+struct WinRegs { uint32_t v[33]; };
+
+// Without prefetch: every lane names its window start `w`, the wave copies
+// dwords [w, w+33) of all 64 windows into the slots (loads and LDS stores
+// interleaved, few live registers).
 __device__ __forceinline__ void stage(uint32_t* slots, uint64_t* wsh, const uint32_t* arena_w, uint64_t w) {
   const int lane = threadIdx.x;
   wsh[lane] = w;
@@ -66,6 +78,29 @@ __device__ __forceinline__ void stage(uint32_t* slots, uint64_t* wsh, const uint
     slots[tt * SLOT + k] = arena_w[wsh[tt] + k];
   }
   slots[lane * SLOT + 32] = arena_w[w + 32];
+  __syncthreads();
+}
+
+__device__ __forceinline__ void fetch(WinRegs& r, const int64_t* base, const int32_t* nw, const uint32_t* arena_w,
+                                      uint32_t c, uint32_t skip) {
+  const int lane = threadIdx.x;
+  const int half = lane >> 5, k = lane & 31;
+  const int32_t woff = (int32_t)(WIN * c - (c ? skip : 0u));
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int tt = 2 * i + half;
+    r.v[i] = arena_w[base[tt] + ((int32_t)c < nw[tt] ? woff : 0) + k];
+  }
+  r.v[32] = arena_w[base[lane] + ((int32_t)c < nw[lane] ? woff : 0) + 32];
+}
+
+__device__ __forceinline__ void put(uint32_t* slots, const WinRegs& r) {
+  const int lane = threadIdx.x;
+  const int half = lane >> 5, k = lane & 31;
+  __syncthreads();                         // the previous window's reads are done
+#pragma unroll
+  for (int i = 0; i < 32; ++i) slots[(2 * i + half) * SLOT + k] = r.v[i];
+  slots[lane * SLOT + 32] = r.v[32];
   __syncthreads();
 }
 
@@ -139,7 +174,9 @@ __global__ void __launch_bounds__(64) k_prep_mid(PrepArgs a) {
 template <int CLS, int HM>
 __device__ __forceinline__ void prep_body(const PrepArgs& a) {
   __shared__ uint32_t slots[WAVE * SLOT];
-  __shared__ uint64_t wsh[WAVE];
+  __shared__ int64_t sbase[WAVE], hbase[WAVE];    // window streams: signature, signing input
+  __shared__ int32_t snw[WAVE], hnw[WAVE];
+  __shared__ uint64_t wsh[WAVE];                  // stage(): this window's start per lane
   __shared__ int8_t b64tab[256];
   const int lane = threadIdx.x;
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + lane;
@@ -204,13 +241,42 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a) {
   b64tab[lane] = (int8_t)b64val((uint32_t)lane);        // table for the fast path (all 256 bytes)
   b64tab[64 + lane] = (int8_t)b64val(64u + lane);
   b64tab[128 + lane] = (int8_t)b64val(128u + lane);
-  b64tab[192 + lane] = (int8_t)b64val(192u + lane);    // made visible by stage()'s first barrier
+  b64tab[192 + lane] = (int8_t)b64val(192u + lane);    // made visible by the barrier before the first fetch()
 
   const uint64_t sbyte = valid ? jb.sig_off : 0u;
   const uint64_t sw0 = sbyte >> 2;                     // arena dword of the segment's first char
   const uint32_t first = (uint32_t)(sbyte & 3ull);
   const uint32_t nchars = (valid && D) ? n : 0u;
   const uint32_t span = nchars ? first + nchars : 0u;  // window bytes the chars occupy
+  const uint32_t mshift = valid ? jb.off & 3u : 0u;
+  const uint32_t len = valid ? jb.sig_in_len : 0u;
+  const int hb_alg = alg_hash_bits(alg);
+  const int hb = CLS == CLS_ED25519 ? 512
+                 : HM == 1          ? 256
+                 : HM == 2          ? (hb_alg == 384 ? 384 : 512)
+                                    : hb_alg;
+  const uint32_t pw = (CLS == CLS_ED25519 && valid) ? 16u : 0u;
+  const uint32_t tot = 4 * pw + len;                   // bytes hashed
+  uint32_t nblk = 0, nwin = 0;
+  if (valid) {
+    nblk = hb == 256 ? (len + 9 + 63) / 64 : (tot + 17 + 127) / 128;
+    nwin = hb == 256 ? (nblk + 1) / 2 : nblk;
+  }
+  // both window streams, for fetch(): every lane's base and window count
+  sbase[lane] = span ? (int64_t)sw0 : 0;
+  snw[lane] = (int32_t)((span + 4 * WIN - 1) / (4 * WIN));
+  hbase[lane] = valid ? (int64_t)(jb.off >> 2) : 0;
+  hnw[lane] = (int32_t)nwin;
+  constexpr uint32_t HSKIP = CLS == CLS_ED25519 ? 16u : 0u;    // window c >= 1 starts at message word 32c - 16
+  // Prefetch one window ahead where it measured faster (RSA: 3+ signature
+  // windows, -10 %; Ed25519 -3 %); the ECDSA variants lose a wave per SIMD to
+  // the 33 extra live registers (96 -> 142 VGPRs) and ran 4-5 % slower
+  // (profiles/r03_s7_prep_prefetch_ab.json), so they load each window just
+  // before use, as round 2 did.
+  constexpr bool PF = CLS == CLS_ED25519 || CLS == CLS_RSA2K;
+  __syncthreads();
+  WinRegs wr;
+  if constexpr (PF) fetch(wr, sbase, snw, arena_w, 0, 0);
   uint32_t acc = 0, bitsn = 0, outi = 0;
   uint32_t cur_row = 0xffffffffu, cur_word = 0;
   uint32_t R_le[8] = {0, 0, 0, 0, 0, 0, 0, 0};          // Ed25519: first 32 bytes (R)
@@ -218,7 +284,9 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a) {
   for (uint32_t c = 0;; ++c) {
     const bool need = !bad && span > 4u * WIN * c;
     if (__ballot(need) == 0ull) break;
-    stage(slots, wsh, arena_w, need ? sw0 + (uint64_t)WIN * c : (valid ? sw0 : 0ull));
+    if constexpr (!PF) stage(slots, wsh, arena_w, need ? sw0 + (uint64_t)WIN * c : (uint64_t)sbase[lane]);
+    else put(slots, wr);
+    if (PF && __ballot(span > 4u * WIN * (c + 1)) != 0ull) fetch(wr, sbase, snw, arena_w, c + 1, 0);
     if (!need) continue;
     if (fast) {
       // window c holds characters [128c, 128c + 128) at byte offset `first`
@@ -313,16 +381,7 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a) {
   //   SHA-512/384: one 128-byte block per window.  Ed25519 hashes R || A || M:
   //   block 0 = the 64-byte register prefix + message words 0..15, block
   //   c >= 1 = message words 32c-16 ..
-  const uint64_t mw0 = valid ? jb.off >> 2 : 0u;
-  const uint32_t mshift = valid ? jb.off & 3u : 0u;
-  const uint32_t len = valid ? jb.sig_in_len : 0u;
-  const int hb_alg = alg_hash_bits(alg);
-  const int hb = CLS == CLS_ED25519 ? 512
-                 : HM == 1          ? 256
-                 : HM == 2          ? (hb_alg == 384 ? 384 : 512)
-                                    : hb_alg;
   uint32_t pre[16];
-  uint32_t pw = 0;
   if (CLS == CLS_ED25519 && valid) {
     const uint32_t* A = a.keyblob + a.keys[__builtin_amdgcn_readfirstlane(job_key(jb))].aux_off;
 #pragma unroll
@@ -330,23 +389,19 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a) {
       pre[k] = sha2::bswap32(R_le[k]);
       pre[8 + k] = sha2::bswap32(A[k]);
     }
-    pw = 16;
-  }
-  const uint32_t tot = 4 * pw + len;                   // bytes hashed
-  uint32_t nblk = 0, nwin = 0;
-  if (valid) {
-    nblk = hb == 256 ? (len + 9 + 63) / 64 : (tot + 17 + 127) / 128;
-    nwin = hb == 256 ? (nblk + 1) / 2 : nblk;
   }
   uint32_t h32[8];
   uint64_t h64[8];
   sha2::sha256_init(h32);
   sha2::sha512_init(h64, hb == 384);
+  if constexpr (PF) fetch(wr, hbase, hnw, arena_w, 0, HSKIP);
   for (uint32_t c = 0;; ++c) {
     const bool need = c < nwin;
     if (__ballot(need) == 0ull) break;
     const uint32_t i0 = hb == 256 ? 32u * c : (c == 0 ? 0u : 32u * c - pw);   // message word at window dword 0
-    stage(slots, wsh, arena_w, need ? mw0 + i0 : (valid ? mw0 : 0ull));
+    if constexpr (!PF) stage(slots, wsh, arena_w, (uint64_t)hbase[lane] + (need ? i0 : 0u));
+    else put(slots, wr);
+    if (PF && __ballot(c + 1 < nwin) != 0ull) fetch(wr, hbase, hnw, arena_w, c + 1, HSKIP);
     if (!need) continue;
     if (hb == 256) {
 #pragma unroll 1
