@@ -210,28 +210,86 @@ struct HostKey {
 // Device memory with shared ownership.  Comb tables are shared by key content
 // between key loads (a JWKS refresh that keeps a key keeps its table: no copy,
 // no rebuild), and a load's key blob is shared by its later width upgrades.
-// Stream-ordered (hipMallocAsync / hipFreeAsync on the key streams): a
-// generation is released only once no queued work can reference it (pipeline
-// slots hold their key state until their chunk has completed, resident
-// batches until the next run or jg_batch_free), and the release must not wait
-// for the device -- hipFree synchronises every stream, so dropping an old key
-// table would stall behind a background comb-table build (~1 s) or the
-// verification pipeline.
+// A generation is released only once no queued work can reference it
+// (pipeline slots hold their key state until their chunk has completed,
+// resident batches until the next run or jg_batch_free).  The release must not
+// make its caller wait for the device -- hipFree synchronises every stream, so
+// dropping an old key table inline would stall a key load behind a background
+// comb-table build (~1 s) or the verification pipeline -- so the last holder
+// hands the pointer to a reaper thread that calls hipFree.  (Round 3 tried
+// stream-ordered hipMallocAsync / hipFreeAsync instead: after a reload that
+// re-used freed memory for a new table, a small-order Ed25519 key's table
+// gave a wrong verdict and the parity suite hit an illegal address; with
+// plain hipMalloc and the reaper the same sequence is exact --
+// tools/diag_reload.py, tests/test_gpu_parity.py test_key_reload_reuses_tables.)
+class Reaper {
+ public:
+  void push(int dev, void* p, size_t bytes) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+    q_.push_back(Item{dev, p, bytes});
+    pending_[dev] += bytes;
+    cv_.notify_one();
+  }
+  // bytes handed over on device `dev` and not yet freed
+  size_t pending(int dev) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = pending_.find(dev);
+    return it == pending_.end() ? 0 : it->second;
+  }
+  // wait until every pointer handed over so far has been freed
+  void drain() {
+    std::unique_lock<std::mutex> lk(mu_);
+    idle_.wait(lk, [&] { return q_.empty() && !busy_; });
+  }
+  ~Reaper() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+      cv_.notify_one();
+    }
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (true) {
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) break;                       // stop requested, nothing left
+      const auto it = q_.front();
+      q_.pop_front();
+      busy_ = true;
+      lk.unlock();
+      if (hipSetDevice(it.dev) == hipSuccess) (void)hipFree(it.p);
+      lk.lock();
+      pending_[it.dev] -= it.bytes;
+      busy_ = false;
+      if (q_.empty()) idle_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, idle_;
+  struct Item { int dev; void* p; size_t bytes; };
+  std::deque<Item> q_;
+  std::map<int, size_t> pending_;
+  bool stop_ = false, busy_ = false;
+  std::thread th_;
+};
+Reaper& reaper() {
+  static Reaper r;
+  return r;
+}
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
   int dev = 0;
-  hipStream_t s = nullptr;        // the stream it was allocated on (and is freed on)
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() {
-    if (!p) return;
-    int cur = 0;
-    const bool had = hipGetDevice(&cur) == hipSuccess;
-    (void)hipSetDevice(dev);
-    (void)hipFreeAsync(p, s);
-    if (had) (void)hipSetDevice(cur);
+    if (p) reaper().push(dev, p, bytes);
   }
   template <class T>
   T* as() const { return (T*)p; }
@@ -240,7 +298,7 @@ using DevBufP = std::shared_ptr<DevBuf>;
 
 // hipMalloc into a DevBuf.  `fail` (jg_debug_fail_alloc): a countdown of
 // allocations after which one fails as if the device were out of memory.
-DevBufP dev_alloc(int dev, hipStream_t s, size_t bytes, std::atomic<int>* fail = nullptr) {
+DevBufP dev_alloc(int dev, size_t bytes, std::atomic<int>* fail = nullptr) {
   if (fail) {
     int f = fail->load();
     while (f > 0 && !fail->compare_exchange_weak(f, f - 1)) {}
@@ -248,10 +306,9 @@ DevBufP dev_alloc(int dev, hipStream_t s, size_t bytes, std::atomic<int>* fail =
   }
   auto b = std::make_shared<DevBuf>();
   b->dev = dev;
-  b->s = s;
   b->bytes = std::max<size_t>(bytes, 16);
   HIPCHK(hipSetDevice(dev));
-  HIPCHK(hipMallocAsync(&b->p, b->bytes, s));
+  HIPCHK(hipMalloc(&b->p, b->bytes));
   return b;
 }
 
@@ -856,6 +913,13 @@ void width_runs(const KeyState& K, const DevGen& G, const Plan& P, int c, Fn&& f
   int w = -1;
   for (int32_t k : K.cls_keys[c]) {
     const int kw = G.kw[(size_t)k];
+    // the launch width must be the width of the table the key's record points
+    // at: a wider launch would index past the end of a narrower table
+    const DevKey& rec = G.mirror[(size_t)k];
+    if (kw == 0 || rec.tab == 0 || rec.tab_w != kw)
+      throw std::runtime_error("key " + std::to_string(k) + ": comb table record (width " + std::to_string(rec.tab_w) +
+                               ", " + (rec.tab ? "set" : "null") + ") does not match its launch width " +
+                               std::to_string(kw));
     if (w >= 0 && kw != w) {
       const int64_t kb = P.kstart[(size_t)k];
       if (kb > beg) fn(beg, kb, w);
@@ -866,8 +930,30 @@ void width_runs(const KeyState& K, const DevGen& G, const Plan& P, int c, Fn&& f
   if (w >= 0 && r.end > beg) fn(beg, r.end, w);
 }
 
+// CAPJWT_CHECK_KEYS=1 (debugging): before each run, read the generation's
+// device key records back and compare their comb-table fields with the host mirror
+bool check_keys_env() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_CHECK_KEYS");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+void check_device_records(const DevGen& G) {
+  const size_t nk = G.mirror.size();
+  if (!nk) return;
+  std::vector<DevKey> dev(nk);
+  HIPCHK(hipMemcpy(dev.data(), G.keys(), sizeof(DevKey) * nk, hipMemcpyDeviceToHost));
+  for (size_t k = 0; k < nk; ++k)
+    if (dev[k].tab != G.mirror[k].tab || dev[k].tab_w != G.mirror[k].tab_w || dev[k].valid != G.mirror[k].valid)
+      throw std::runtime_error("key " + std::to_string(k) + ": device record (tab_w " + std::to_string(dev[k].tab_w) +
+                               ") differs from the host mirror (tab_w " + std::to_string(G.mirror[k].tab_w) + ")");
+}
+
 void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, const Plan& P, jg_batch* marks,
               bool fanout = true) {
+  if (check_keys_env()) check_device_records(G);
   const bool timed = marks && marks->timing;
   int nact = 0;
   for (int c = 1; c < NCLS; ++c) nact += P.ranges[c].end > P.ranges[c].begin;
@@ -1450,10 +1536,19 @@ constexpr uint64_t HBM_RESERVE = uint64_t(2) << 30;
 uint64_t free_hbm(int dev) {
   size_t fr = 0, tot = 0;
   HIPCHK(hipSetDevice(dev));
-  hipMemPool_t pool = nullptr;
-  if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) (void)hipMemPoolTrimTo(pool, 0);   // released tables
   HIPCHK(hipMemGetInfo(&fr, &tot));
-  return fr;
+  return fr + reaper().pending(dev);      // released tables the reaper is about to free
+}
+
+// CAPJWT_POISON_TABLES=1 (debugging): fill every new key comb table with a
+// byte pattern before its build, so an entry the build leaves unwritten cannot
+// pass for a stale one
+void poison_table(const DevBuf& t, hipStream_t s) {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_POISON_TABLES");
+    return e && std::atoi(e) != 0;
+  }();
+  if (on) HIPCHK(hipMemsetAsync(t.p, 0xA5, t.bytes, s));
 }
 
 // Launch the comb-table builds of keys (index list on the device at `didx`,
@@ -1499,8 +1594,8 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   g->mirror = S.dk;
   g->kw.assign(nk, 0);
   ensure_tables(d, S);
-  g->dkeys = dev_alloc(d->id, s, sizeof(DevKey) * std::max<size_t>(nk, 1), &ctx->fail_alloc);
-  g->blob = dev_alloc(d->id, s, sizeof(uint32_t) * std::max<size_t>(S.blob.size(), 4), &ctx->fail_alloc);
+  g->dkeys = dev_alloc(d->id, sizeof(DevKey) * std::max<size_t>(nk, 1), &ctx->fail_alloc);
+  g->blob = dev_alloc(d->id, sizeof(uint32_t) * std::max<size_t>(S.blob.size(), 4), &ctx->fail_alloc);
   // key prep index lists: p256 | p384 | p521 | ed
   std::vector<int32_t> idx;
   size_t at[4];
@@ -1510,7 +1605,7 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   }
   at[3] = idx.size();
   idx.insert(idx.end(), S.ed_idx.begin(), S.ed_idx.end());
-  DevBufP didx = dev_alloc(d->id, s, sizeof(int32_t) * std::max<size_t>(idx.size() + nk, 1), &ctx->fail_alloc);
+  DevBufP didx = dev_alloc(d->id, sizeof(int32_t) * std::max<size_t>(idx.size() + nk, 1), &ctx->fail_alloc);
   int32_t* di = didx->as<int32_t>();
   DevKey* dk = g->keys();
   uint32_t* blob = g->keyblob();
@@ -1580,7 +1675,10 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   }
   std::map<std::pair<int, int>, std::vector<int32_t>> groups;
   std::map<std::string, int32_t> first;          // one build per distinct (id, width)
-  for (auto& f : fresh) f.second.buf = dev_alloc(d->id, s, table_bytes(f.second.cls, f.second.w), &ctx->fail_alloc);
+  for (auto& f : fresh) {
+    f.second.buf = dev_alloc(d->id, table_bytes(f.second.cls, f.second.w), &ctx->fail_alloc);
+    poison_table(*f.second.buf, s);
+  }
   for (const auto& u : use) {
     const Req& r = fresh.at(u.second);
     const size_t i = u.first;
@@ -1602,7 +1700,7 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
 }
 
 void upload_cls(jg_ctx* ctx, Device* d, DevGen& g, const std::vector<uint8_t>& cls_tab) {
-  g.dcls = dev_alloc(d->id, d->kstream, std::max<size_t>(cls_tab.size(), 16), &ctx->fail_alloc);
+  g.dcls = dev_alloc(d->id, std::max<size_t>(cls_tab.size(), 16), &ctx->fail_alloc);
   if (!cls_tab.empty())
     HIPCHK(hipMemcpyAsync(g.dcls->p, cls_tab.data(), cls_tab.size(), hipMemcpyHostToDevice, d->kstream));
   HIPCHK(hipStreamSynchronize(d->kstream));
@@ -1659,12 +1757,13 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
     }
     HIPCHK(hipSetDevice(d->id));
     const DevGen& G = *cur->dev[i];
-    DevBufP t = dev_alloc(d->id, d->ustream, table_bytes(cls, w));
+    DevBufP t = dev_alloc(d->id, table_bytes(cls, w));
+    poison_table(*t, d->ustream);
     // a one-record key array pointing at the new table (the blob is the generation's)
     DevKey rec = G.mirror[k];
     rec.tab = (uint64_t)(uintptr_t)t->p;
     rec.tab_w = w;
-    DevBufP tmp = dev_alloc(d->id, d->ustream, sizeof(DevKey) + 16);
+    DevBufP tmp = dev_alloc(d->id, sizeof(DevKey) + 16);
     const int32_t zero = 0;
     HIPCHK(hipMemcpyAsync(tmp->p, &rec, sizeof(DevKey), hipMemcpyHostToDevice, d->ustream));
     HIPCHK(hipMemcpyAsync((char*)tmp->p + sizeof(DevKey), &zero, sizeof zero, hipMemcpyHostToDevice, d->ustream));
@@ -1697,7 +1796,7 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
     if (!hit) continue;
     any = true;
     g->tabs.push_back(built[i]);
-    g->dkeys = dev_alloc(d->id, d->ustream, sizeof(DevKey) * std::max<size_t>(g->mirror.size(), 1));
+    g->dkeys = dev_alloc(d->id, sizeof(DevKey) * std::max<size_t>(g->mirror.size(), 1));
     if (!g->mirror.empty())
       HIPCHK(hipMemcpyAsync(g->dkeys->p, g->mirror.data(), sizeof(DevKey) * g->mirror.size(), hipMemcpyHostToDevice,
                             d->ustream));
@@ -1870,7 +1969,8 @@ void jg_destroy(jg_ctx* ctx) {
     d->qcv.notify_all();
     if (d->worker.joinable()) d->worker.join();
   }
-  ctx->publish(nullptr);                           // key generations: freed on the key streams
+  ctx->publish(nullptr);                           // key generations: handed to the reaper
+  reaper().drain();                                // ... and freed before jg_destroy returns
   for (auto& d : ctx->devs) {
     (void)hipSetDevice(d->id);
     for (auto& l : d->lanes) l.destroy();

@@ -241,3 +241,37 @@ def test_p256_key_table_widths(tier):
         if (0 if s is None else out[s]) != want:
             bad.append((t["name"], t["key"]))
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("tier", [24, 22, 20, 18, 16])
+def test_ed25519_key_table_widths(tier):
+    """Every Ed25519 key comb width (ed25519.hpp ED_WA, picked by the table
+    budget) against the oracle: the golden Ed25519 keys alone in a context
+    whose budget buys `tier`, every EdDSA golden token against every one of
+    them (small-order and non-canonical keys included)."""
+    import bench
+    from cap_amd import _lib
+    from oracle import jws
+    keys, toks = H.golden()
+    ed = [k for k in keys if k.get("kty") == "OKP"]
+    n = len(ed)
+    budget = n * bench.table_bytes("ed25519", tier)
+    assert bench.key_widths({"ed25519": n}, budget)["ed25519"] == tier
+    ctx = _lib.Context()
+    ctx.set_table_budget(budget)
+    ctx.load_keys([H.abi_key(k) for k in ed])
+    widths = ctx.table_widths()
+    assert {w for w in widths if w} == {tier}, widths
+    kid_index = {k["kid"]: i for i, k in enumerate(ed)}
+    okeys = {k["kid"]: jws.Key.from_fixture(k) for k in ed}
+    cross = [dict(t, key=k["kid"]) for t in toks if t["alg"] == "EdDSA" for k in ed]
+    arena, slots = H.jobs_from_tokens(cross, kid_index)
+    out = ctx.verify(arena)
+    ctx.close()
+    bad = []
+    for t, s in zip(cross, slots):
+        p = jws.parse_jws(t["token"])
+        want = int(jws.verify_sig(p, okeys[t["key"]])) if p is not None else 0
+        if (0 if s is None else out[s]) != want:
+            bad.append((t["name"], t["key"]))
+    assert not bad, bad[:10]
