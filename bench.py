@@ -249,20 +249,38 @@ def bench_keys():
 
 
 # ---------------------------------------------------------------- measurement
-def measure(ctx, arena, toks, steps, warmup, dist):
+def measure(ctx, arena, toks, steps, warmup, dist, second=None):
+    """Stage the batch (and a second one: `second` = (arena, toks), default a
+    copy of the first) and time `steps` steps enqueued back to back,
+    alternating between the two staged batches.  The runtime puts consecutive
+    resident batches on two lanes on different hardware queues, so one step's
+    front kernels overlap the previous step's point kernel (jg_runtime.cpp
+    batch_lanes); each step is a complete pass over its own 1 x `len(toks)`
+    jobs (its own device arena copy and scratch, verdicts copied back every
+    step).  BENCH_ONE_BATCH=1 times one staged batch alone (round-2 layout)."""
     from cap_amd import _lib
     from cap_amd.shard import max_over_ranks
     global LAST_WINDOW, LAST_SYNC_MS
-    h = ctypes.c_void_p()
     L = _lib.lib()
-    rc = L.jg_batch_stage(ctx.h, 0, arena, len(arena), toks.ctypes.data_as(ctypes.POINTER(_lib.JgTok)), len(toks),
-                          ctypes.byref(h))
-    if rc != 0:
-        raise RuntimeError(ctx.error())
-    b = _lib.Batch(ctx, h, len(toks))
+
+    def stage(ar, tk):
+        h = ctypes.c_void_p()
+        if L.jg_batch_stage(ctx.h, 0, ar, len(ar), tk.ctypes.data_as(ctypes.POINTER(_lib.JgTok)), len(tk),
+                            ctypes.byref(h)) != 0:
+            raise RuntimeError(ctx.error())
+        return _lib.Batch(ctx, h, len(tk))
+    b = stage(arena, toks)
     v = np.frombuffer(b.run(want_verdicts=True), dtype=np.uint8)
     accepted = int(v.sum())
     pinned = _lib.PinnedBuffer(len(toks))
+    batches = [(b, pinned, accepted)]
+    if os.environ.get("BENCH_ONE_BATCH") != "1":
+        a2, t2 = second if second is not None else (arena, toks)
+        if len(t2) != len(toks):
+            raise ValueError("the second batch must have as many jobs as the first")
+        b2 = stage(a2, t2)
+        acc2 = int(np.frombuffer(b2.run(want_verdicts=True), dtype=np.uint8).sum())
+        batches.append((b2, _lib.PinnedBuffer(len(t2)), acc2))
     # per-kernel device times: average over synchronous runs (the warmup)
     times = {}
     w0 = time.clock_gettime_ns(time.CLOCK_BOOTTIME)
@@ -278,33 +296,40 @@ def measure(ctx, arena, toks, steps, warmup, dist):
         torch.cuda.synchronize()
         td.barrier()
     # timed region: K steps streamed back to back (kernels + verdict D2H into
-    # pinned memory each step), one synchronisation at the end
+    # pinned memory each step), alternating batches, one synchronisation per batch at the end
     t0 = time.perf_counter()
-    for _ in range(steps):
-        b.enqueue(pinned)
-    b.sync()
+    for i in range(steps):
+        bb, pb, _ = batches[i % len(batches)]
+        bb.enqueue(pb)
+    for bb, _, _ in batches:
+        bb.sync()
     elapsed = time.perf_counter() - t0
-    for name, ms in b.kernel_times():          # last timed step
-        times.setdefault(name, []).append(ms)
-    last = np.frombuffer(pinned.bytes(), dtype=np.uint8)
-    if int(last.sum()) != accepted:
-        raise RuntimeError("verdicts changed between runs")
-    pinned.free()
+    for bb, pb, acc in batches[:min(steps, len(batches))]:
+        if int(np.frombuffer(pb.bytes(), dtype=np.uint8).sum()) != acc:
+            raise RuntimeError("verdicts changed between runs")
+    if len(batches) > 1 and batches[1][2] != accepted and second is None:
+        raise RuntimeError("the two copies of the batch disagree")
+    for bb, pb, _ in batches:
+        pb.free()
     if dist:
         import torch
         torch.cuda.synchronize()
         elapsed = max_over_ranks(elapsed, device=COLL_DEVICE)
-    b.free()
+    for bb, _, _ in batches:
+        bb.free()
     kms = {k: float(np.mean(x)) for k, x in times.items()}
     # the synchronous runs' launches, for tools/cfg_roofline_check.py: every
     # kernel of this batch ran `runs` times inside [start, end] (CLOCK_BOOTTIME,
     # the clock of rocprofv3's timestamps)
     LAST_WINDOW = {"boottime_ns": [w0, w1], "runs": max(1, warmup)}
+    global LAST_ACCEPTED2
+    LAST_ACCEPTED2 = batches[1][2] if len(batches) > 1 else None
     return elapsed, accepted, kms, v
 
 
 LAST_WINDOW = None
 LAST_SYNC_MS = None
+LAST_ACCEPTED2 = None       # accepted count of measure()'s second staged batch
 
 
 def h2d_bandwidth(nbytes, iters=5):
@@ -624,13 +649,18 @@ def roofline_line(kernel_ms, per_gpu, kernels):
 
 
 def config_line(ctx, name, workload, pool, algs, keyidx, expected_good, per_gpu, steps, warmup, dist, world,
-                kernels=None, class_of_key=None):
+                kernels=None, class_of_key=None, second=None):
     """One BASELINE config measured like the headline.  `kernels`: roofline
     work per token of the class kernels to report; a kernel sees only its
     class's tokens -- by alg family, or by `class_of_key[key index]` (kernel
-    class name per key) where keys of one family fall into several classes."""
+    class name per key) where keys of one family fall into several classes.
+    `second` = (pool, algs, keyidx, expected_good) of measure()'s second
+    staged batch (default: a copy of the first)."""
     arena, toks = pack(pool, algs, keyidx, per_gpu)
-    el, acc, _, v = measure(ctx, arena, toks, steps, warmup, dist)
+    sec = pack(*second[:3], per_gpu) if second is not None else None
+    el, acc, _, v = measure(ctx, arena, toks, steps, warmup, dist, second=sec)
+    acc2 = LAST_ACCEPTED2
+    del sec
     # per-class kernel times from the synchronous runs of the batch: in the
     # timed region steps are pipelined, so a class kernel there shares the
     # chip with the previous step's kernels and its duration is no roofline
@@ -643,8 +673,12 @@ def config_line(ctx, name, workload, pool, algs, keyidx, expected_good, per_gpu,
             "ms_per_step": el * 1000.0 / steps, "tokens_per_gpu": per_gpu, "unique_pool": len(pool),
             "accepted": acc, "expected_accepted": want, "kernel_ms": kms,
             "kernel_ms_from": "synchronous runs of the batch (bench warmup), one at a time", "trace_window": LAST_WINDOW}
-    if acc != want:
-        line["error"] = f"accepted {acc} != expected {want}"
+    want2 = want
+    if second is not None:
+        reps2 = (per_gpu + len(second[0]) - 1) // len(second[0])
+        want2 = int(np.tile(second[3], reps2)[:per_gpu].sum())
+    if acc != want or acc2 not in (None, want2):
+        line["error"] = f"accepted {acc} (second batch {acc2}) != expected {want} ({want2})"
     if kernels:
         # per-class token counts: a mixed batch's class kernels see only their share
         share = {}
@@ -736,9 +770,11 @@ def run_configs(ctx, args, threads, rank, world, dist):
     chunk = 262144
     line = config_line(
         ctx, "mixed_10alg_32kid", "all 10 algs, 32 kids, 5% tampered, 10M stream on 8 GPUs in 262144-token chunks "
-        "(configs[4]); one chunk per step per GPU", pool[:chunk], algs[:chunk], keyidx[:chunk], good[:chunk], chunk,
+        "(configs[4]); one chunk per step per GPU, steps alternating between the share's first two chunks",
+        pool[:chunk], algs[:chunk], keyidx[:chunk], good[:chunk], chunk,
         max(1, args.steps // 2), 1, dist, world, kernels={k: v for k, v in work.items() if k.split("_")[0] in present},
-        class_of_key=kcls)
+        class_of_key=kcls,
+        second=(pool[chunk:2 * chunk], algs[chunk:2 * chunk], keyidx[chunk:2 * chunk], good[chunk:2 * chunk]))
     line["pool"] = c5_pool_note(args.c5_unique)
     line["table_budget_GiB"] = args.c5_table_budget_gb
     line["key_comb_w"] = {m[0]: w for m, w in zip(meta, c5w) if w}
@@ -927,7 +963,13 @@ def main():
     npool = min(args.pool or args.tokens, args.tokens)
     pool = gen_tokens("ES256", npool, golden_keypaths(kids), host_threads, f"r{rank}")
     arena, toks = pack(pool, [ALG_IDS["ES256"]] * npool, np.arange(npool) % len(kids), args.tokens)
-    el, acc, kms, _ = measure(ctx, arena, toks, args.steps, args.warmup, dist)
+    # the second staged batch of measure(): another npool unique tokens
+    pool2 = gen_tokens("ES256", npool, golden_keypaths(kids), host_threads, f"r{rank}b")
+    second = pack(pool2, [ALG_IDS["ES256"]] * npool, np.arange(npool) % len(kids), args.tokens)
+    del pool2
+    el, acc, kms, _ = measure(ctx, arena, toks, args.steps, args.warmup, dist, second=second)
+    acc2 = LAST_ACCEPTED2
+    del second
     ntok = len(toks)
     value = world * ntok * args.steps / el
     ms_step = el * 1000.0 / args.steps
@@ -947,7 +989,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u32 (28-bit limbs, 64-bit v_mad_u64_u32 accumulators)",
         "data": f"synthetic: OpenSSL-signed ES256 JWTs (testJWTClaims shape), {npool} unique tokens"
-                + (f" replicated to {ntok}" if npool < ntok else "") + " per GPU, no verdict caching",
+                + (f" replicated to {ntok}" if npool < ntok else "") + " per GPU, no verdict caching; "
+                "steps alternate between two staged batches of different tokens (bench.measure)",
         "config": {"workload": "ES256 P-256 JWKS with 4 kids, 1M tokens batch-verified per MI355X (BASELINE configs[1])",
                    "tokens_per_gpu": ntok, "unique_tokens": npool, "kids": 4,
                    "table_budget_GiB": budget / (1 << 30), "p256_key_comb_w": P256_WQ,
@@ -967,8 +1010,8 @@ def main():
         "kernel_ms": kms,
         "cpu": cpu,
     }
-    if acc != ntok:
-        result["error"] = f"only {acc}/{ntok} valid tokens accepted"
+    if acc != ntok or acc2 not in (None, ntok):
+        result["error"] = f"only {acc}/{ntok} (second batch {acc2}) valid tokens accepted"
     if rank == 0 and world == 1:
         result["pcie"] = measure_pcie(ctx, arena, toks)
     # the same batch at the library's default table budget (what a caller gets

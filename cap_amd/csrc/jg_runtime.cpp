@@ -479,6 +479,7 @@ struct Item {                     // one device's share of a submission
 struct Device {
   int id = 0;
   Lane lane0;                     // resident batches, hashing
+  Lane lane1;                     // resident batches staged second, fourth, ... (CAPJWT_BATCH_LANES)
   hipStream_t kstream = nullptr;  // key loads (staging, narrow tables): beside the verify streams
   hipStream_t ustream = nullptr;  // background width upgrades of key comb tables
   uint32_t* gtab[NCLS] = {};
@@ -497,6 +498,7 @@ struct Device {
   Lane lanes[NLANE];
   Slot slots[NSLOT];
   int next_slot = 0, next_lane = 0;
+  int next_res = 0;                // resident batches staged (CAPJWT_BATCH_LANES)
   std::thread worker;
   std::mutex qmu;
   std::condition_variable qcv, idle_cv;
@@ -892,6 +894,20 @@ bool prep_midstate() {
     return !(e && std::atoi(e) == 0);
   }();
   return on;
+}
+
+// Resident batches alternate between two lanes whose main streams sit on
+// different hardware queues (lane0, lane1), so runs of two staged batches
+// enqueued back to back overlap: one batch's latency-bound front kernels
+// (prep, scalar stage) and tails share the CUs with the other's point kernel
+// (ES256 +6 %, profiles/r03_s9_altlanes_ab.json).  CAPJWT_BATCH_LANES=1 puts
+// every resident batch on lane0 (A/B).
+int batch_lanes() {
+  static const int n = [] {
+    const char* e = std::getenv("CAPJWT_BATCH_LANES");
+    return e ? std::atoi(e) : 2;
+  }();
+  return n;
 }
 
 bool pipeline_fanout() {
@@ -1927,8 +1943,10 @@ jg_ctx* jg_create(const int* devices, int ndev) {
       HIPCHK(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
       for (auto& l : d->lanes) l.create_main();
       d->lane0.create_main();
+      d->lane1.create_main();
       for (auto& l : d->lanes) l.create_fanout();
       d->lane0.create_fanout();
+      d->lane1.create_fanout();
       for (auto& s : d->slots) {
         HIPCHK(hipEventCreateWithFlags(&s.done, pipe_trace() ? hipEventDefault : hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
@@ -1980,6 +1998,7 @@ void jg_destroy(jg_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     }
     d->lane0.sync();
+    d->lane1.sync();
     if (d->copy) {
       (void)hipStreamSynchronize(d->copy);
       (void)hipStreamDestroy(d->copy);
@@ -2005,6 +2024,7 @@ void jg_destroy(jg_ctx* ctx) {
       }
     }
     d->lane0.destroy();
+    d->lane1.destroy();
   }
   delete ctx;
 }
@@ -2138,10 +2158,10 @@ int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t ar
     b->ctx = ctx;
     b->dslot = (size_t)device_slot;
     b->dev = ctx->devs[device_slot].get();
-    b->lane = &b->dev->lane0;
     b->own = std::make_unique<Bufs>();
     b->b = b->own.get();
     std::lock_guard<std::mutex> g(b->dev->mu);
+    b->lane = batch_lanes() > 1 && (b->dev->next_res++ & 1) ? &b->dev->lane1 : &b->dev->lane0;
     HIPCHK(hipSetDevice(b->dev->id));
     PlanScratch X;
     if (arena_len >= (uint64_t(1) << 32) - ARENA_SLACK) {
