@@ -116,9 +116,9 @@ uint64_t default_table_budget() {
 // chunks ramp up from 4096 jobs (the copy engine starts after a short host
 // plan) and the tail ends in a quarter-size chunk (little kernel time left
 // exposed after the last copy).
-std::vector<size_t> chunk_cuts(size_t lo, size_t hi, size_t C) {
+std::vector<size_t> chunk_cuts(size_t lo, size_t hi, size_t C, size_t first = 4096) {
   std::vector<size_t> cut{lo};
-  for (size_t ramp = std::min<size_t>(C, 4096); cut.back() < hi; ramp = std::min(C, 2 * ramp))
+  for (size_t ramp = std::min<size_t>(C, first); cut.back() < hi; ramp = std::min(C, 2 * ramp))
     cut.push_back(std::min(hi, cut.back() + ramp));
   const size_t tail = C / 4;
   if (cut.size() > 2 && tail >= 1024 && cut.back() - cut[cut.size() - 2] > tail)
@@ -452,6 +452,7 @@ struct Slot {
   hipEvent_t done = nullptr;       // slot stream: verdicts copied back
   hipEvent_t copied = nullptr;     // copy stream: the chunk's inputs are on the device
   hipEvent_t tr_a = nullptr, tr_b = nullptr, tr_c = nullptr;   // CAPJWT_PIPE_TRACE: H2D start / end, kernels end
+  hipEvent_t ev_planned = nullptr, ev_cls[NCLS] = {};            // class-grouped chunks (GroupFan)
   double host_ms[4] = {};                                       // wait, plan, enqueue, of which H2D calls
   int chunk_no = 0;
   size_t reserved = 0;             // chunk capacity (jobs) the buffers were sized for
@@ -474,6 +475,7 @@ struct Item {                     // one device's share of a submission
   const uint8_t* dev_arena = nullptr;   // device view of a page-locked arena (kernels read it over PCIe)
   size_t chunk = 0, nchunks = 0;
   std::vector<size_t> cuts;       // chunk boundaries (chunk_cuts)
+  bool grouped = false;           // mixed classes: chunks run class-grouped (enqueue_chunk)
 };
 
 struct Device {
@@ -630,6 +632,38 @@ void rebuild_class_tables(KeyState& K) {
     for (int a = 0; a < NALG; ++a)
       if (hk.valid && alg_family(a) == hk.kind) K.cls_tab[k * NALG + a] = (uint8_t)hk.cls;
   }
+}
+
+// Pipeline chunks whose jobs fall into two or more kernel classes run
+// class-grouped: the chunk's plan fill on the copy stream, then each class
+// chain on the lane of its group -- RSA-2K/3K, RSA-4K+, the EC and Ed25519
+// classes -- and the verdict scatter on the lane of the chunk's costliest
+// group once every class is done.  A group's launches from consecutive chunks
+// queue on one lane (one hardware queue each) while the three groups run side
+// by side; lane-per-chunk instead ran each chunk's classes one after another
+// (~6 ms of serial latency per 262 k mixed chunk).  CAPJWT_CLASS_GROUPS=0:
+// lane per chunk for every submission (A/B).
+bool class_grouping() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_CLASS_GROUPS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+int cls_group(int c) { return c == CLS_RSA4K ? 1 : c <= CLS_RSA3K ? 0 : 2; }
+
+// two or more kernel classes among (a sample of) the jobs
+bool mixed_classes(const KeyState& K, const jg_tok* toks, size_t n) {
+  const size_t step = std::max<size_t>(1, n / 2048), nk = K.keys.size();
+  int first = -1;
+  for (size_t i = 0; i < n; i += step) {
+    if (toks[i].key_idx >= nk) continue;
+    const int c = classify(K, toks[i]);
+    if (c == CLS_REJECT) continue;
+    if (first < 0) first = c;
+    else if (c != first) return true;
+  }
+  return false;
 }
 
 // Reject a job list that names a key outside the table or a byte span outside
@@ -967,17 +1001,28 @@ void check_device_records(const DevGen& G) {
                                ") differs from the host mirror (tab_w " + std::to_string(G.mirror[k].tab_w) + ")");
 }
 
+// Explicit streams of a class-grouped pipeline chunk (enqueue_chunk): the
+// chunk's control work on `ctrl`, each class chain on cls[c], the verdict
+// scatter on `join` once every class's `done` event has fired.
+struct GroupFan {
+  hipStream_t ctrl = nullptr, join = nullptr;
+  hipStream_t cls[NCLS] = {};
+  hipEvent_t start = nullptr;
+  hipEvent_t done[NCLS] = {};
+};
+
 void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, const Plan& P, jg_batch* marks,
-              bool fanout = true) {
+              bool fanout = true, const GroupFan* gf = nullptr) {
   if (check_keys_env()) check_device_records(G);
   const bool timed = marks && marks->timing;
   int nact = 0;
   for (int c = 1; c < NCLS; ++c) nact += P.ranges[c].end > P.ranges[c].begin;
-  const bool conc = !timed && fanout && nact > 1;
+  const bool conc = !timed && !gf && fanout && nact > 1;
   const int64_t np = P.npad;
-  const hipStream_t s0 = L->stream;
+  const hipStream_t s0 = gf ? gf->join : L->stream;
   mark(marks, "begin");
-  HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, s0));
+  HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, gf ? gf->ctrl : s0));
+  if (gf) HIPCHK(hipEventRecord(gf->start, gf->ctrl));
   PrepArgs pa{};
   pa.arena = (const uint8_t*)B->arena.p;
   pa.jobs = (const JobDev*)B->jobs.p;
@@ -1001,6 +1046,9 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
     if (conc) {
       s = L->cstream[c];
       HIPCHK(hipStreamWaitEvent(s, L->ev_start, 0));
+    } else if (gf) {
+      s = gf->cls[c];
+      HIPCHK(hipStreamWaitEvent(s, gf->start, 0));
     }
     pa.begin = r.begin;
     pa.end = r.end;
@@ -1057,6 +1105,9 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
     if (conc) {
       HIPCHK(hipEventRecord(L->ev_done[c], s));
       HIPCHK(hipStreamWaitEvent(s0, L->ev_done[c], 0));
+    } else if (gf) {
+      HIPCHK(hipEventRecord(gf->done[c], s));
+      if (s != s0) HIPCHK(hipStreamWaitEvent(s0, gf->done[c], 0));
     }
   }
   launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s0);
@@ -1209,7 +1260,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   }
   Lane& LN = d->lanes[d->next_lane];
   d->next_lane = (d->next_lane + 1) % NLANE;
-  const hipStream_t s = LN.stream;
+  hipStream_t s = LN.stream;
   const bool tr = pipe_trace();
   S.host_ms[1] = tr ? ms_since(t_start) : 0.0;
   const auto t_enq = std::chrono::steady_clock::now();
@@ -1221,7 +1272,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   size_scratch(&S.bufs, P, bytes);
   S.bufs.jobs.get(sizeof(JobDev) * P.npad);
   S.bufs.perm.get(sizeof(int32_t) * P.npad);
-  uint8_t* dm = (uint8_t*)S.bufs.meta.get(L.toks_off);
+  uint8_t* dm = (uint8_t*)S.bufs.meta.get(L.bytes);
   const uint8_t* hbd = (const uint8_t*)S.h_meta.dp;
   const hipStream_t cs = d->copy;
   if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
@@ -1229,11 +1280,38 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   HIPCHK(hipEventRecord(S.copied, cs));
   if (tr) HIPCHK(hipEventRecord(S.tr_b, cs));
   if (tr) S.host_ms[3] = ms_since(t_enq);
-  HIPCHK(hipStreamWaitEvent(s, S.copied, 0));
-  launch_copy(hbd, dm, L.toks_off, s);
+  int nact = 0, jgrp = 0;
+  double gcost[3] = {0, 0, 0};
+  for (int c = 1; c < NCLS; ++c) {
+    const int64_t m = P.ranges[c].end - P.ranges[c].begin;
+    if (m <= 0) continue;
+    ++nact;
+    gcost[cls_group(c)] += CLS_COST[c] * (double)m;
+  }
+  for (int g = 1; g < 3; ++g)
+    if (gcost[g] > gcost[jgrp]) jgrp = g;
+  const bool grouped = it.grouped && nact >= 2;
+  GroupFan gf;
+  hipStream_t fs = s;                              // the plan fill's stream
+  if (grouped) {
+    gf.ctrl = cs;                                  // in order after the chunk's H2D copy
+    gf.join = d->lanes[jgrp].stream;
+    for (int c = 1; c < NCLS; ++c) gf.cls[c] = d->lanes[cls_group(c)].stream;
+    gf.start = S.ev_planned;
+    for (int c = 0; c < NCLS; ++c) gf.done[c] = S.ev_cls[c];
+    fs = cs;
+  } else {
+    HIPCHK(hipStreamWaitEvent(s, S.copied, 0));
+  }
+  // grouped chunks fill the plan on the copy stream: the whole plan block goes
+  // over by DMA (a zero-copy read of the jobs there would hold the next
+  // chunk's H2D copy behind a PCIe-bound kernel); else the header by a copy
+  // kernel and the jobs read in place from pinned memory
+  if (grouped) HIPCHK(hipMemcpyAsync(dm, hb, L.bytes, hipMemcpyHostToDevice, cs));
+  else launch_copy(hbd, dm, L.toks_off, fs);
   {
     PlanFillArgs fa{};
-    fa.toks = (const jg_tok*)(hbd + L.toks_off);
+    fa.toks = (const jg_tok*)((grouped ? (const uint8_t*)dm : hbd) + L.toks_off);
     fa.n = (int64_t)n;
     fa.base = dbase;
     fa.cls_tab = G.cls();
@@ -1242,9 +1320,14 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
     fa.pad = (const int64_t*)(dm + L.pad_off);
     fa.jobs = (JobDev*)S.bufs.jobs.p;
     fa.perm = (int32_t*)S.bufs.perm.p;
-    launch_plan_fill(fa, s);
+    launch_plan_fill(fa, fs);
   }
-  run_plan(d, K, G, &LN, &S.bufs, P, nullptr, pipeline_fanout());
+  if (grouped) {
+    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, &gf);
+    s = gf.join;                                   // verdicts leave once every class is done
+  } else {
+    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, pipeline_fanout());
+  }
   if (tr) HIPCHK(hipEventRecord(S.tr_c, s));
   S.h_verdict.get(std::max<size_t>(n, 1));
   launch_copy(S.bufs.verdict.p, S.h_verdict.dp, n, s);
@@ -1897,7 +1980,11 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
     it.ks = ks;
     it.dev_arena = dview;
     it.chunk = C;
-    it.cuts = chunk_cuts(it.lo, it.hi, C);
+    it.grouped = class_grouping() && mixed_classes(*ks, toks + it.lo, it.hi - it.lo);
+    // grouped chunks serialise each class group's launches on one lane, so a
+    // long ramp of small chunks would queue latency-bound launches (an
+    // RSA-4096 modexp takes ~1.5 ms at any size): start at C / 4
+    it.cuts = chunk_cuts(it.lo, it.hi, C, it.grouped ? std::max<size_t>(4096, C / 4) : 4096);
     it.nchunks = it.cuts.size() - 1;
     t->pending += it.nchunks;
     items.push_back(std::move(it));
@@ -1953,6 +2040,8 @@ jg_ctx* jg_create(const int* devices, int ndev) {
         HIPCHK(hipEventCreate(&s.tr_a));
         HIPCHK(hipEventCreate(&s.tr_b));
         HIPCHK(hipEventCreate(&s.tr_c));
+        HIPCHK(hipEventCreateWithFlags(&s.ev_planned, hipEventDisableTiming));
+        for (auto& e : s.ev_cls) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       }
       HIPCHK(hipStreamCreateWithFlags(&d->kstream, hipStreamNonBlocking));
       HIPCHK(hipStreamCreateWithFlags(&d->ustream, hipStreamNonBlocking));
@@ -1994,7 +2083,9 @@ void jg_destroy(jg_ctx* ctx) {
     for (auto& l : d->lanes) l.destroy();
     for (auto& s : d->slots) {
       if (s.done) (void)hipEventDestroy(s.done);
-      for (hipEvent_t e : {s.tr_a, s.tr_b, s.tr_c, s.copied})
+      for (hipEvent_t e : s.ev_cls)
+        if (e) (void)hipEventDestroy(e);
+      for (hipEvent_t e : {s.tr_a, s.tr_b, s.tr_c, s.copied, s.ev_planned})
         if (e) (void)hipEventDestroy(e);
     }
     d->lane0.sync();
