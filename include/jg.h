@@ -181,7 +181,10 @@ void jg_host_free(void* p);
  * its dispatch plan (bucketing by algorithm family and key); jg_batch_run runs
  * the verify kernels on the resident inputs (no H2D) and, if verdict_out is
  * non-NULL, copies verdicts back.  jg_batch_run is asynchronous when
- * verdict_out is NULL; jg_batch_sync waits. */
+ * verdict_out is NULL; jg_batch_sync waits.  Consecutively staged batches of a
+ * device alternate between two compute lanes on different hardware queues
+ * (CAPJWT_BATCH_LANES=1: one lane): runs of one batch are in order, runs of
+ * two batches enqueued back to back overlap on the device. */
 int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t arena_len,
                    const jg_tok* toks, size_t ntok, jg_batch** out);
 int jg_batch_run(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out);

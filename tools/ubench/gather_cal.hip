@@ -34,6 +34,23 @@ __global__ void __launch_bounds__(64) k_gather(const uint32_t* __restrict__ tab,
   if (acc == 0x9e3779b9u) out[0] = acc;
 }
 
+// the packed P-256 layout (ecdsa.hpp JG_EC_PACK64): 64-byte entries, 64-B
+// aligned, 4 x dwordx4 -- each entry half of one 128-B line
+__global__ void __launch_bounds__(64) k_gather64(const uint32_t* __restrict__ tab, uint32_t* out) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  uint32_t acc = 0;
+  for (int g = 0; g < GATHERS; ++g) {
+    const uint64_t e = (uint64_t)mix(i * 64u + (uint32_t)g + 0x5bd1e995u) % (NENT * ENT_WORDS / 16);
+    const uint4* p = reinterpret_cast<const uint4*>(tab + e * 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = p[k];
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  }
+  if (acc == 0x9e3779b9u) out[0] = acc;
+}
+
 __global__ void k_stream(const uint4* __restrict__ src, size_t n, uint32_t* out) {
   uint32_t acc = 0;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -51,11 +68,13 @@ int main() {
   if (hipMemset(tab, 1, bytes) != hipSuccess) return 1;
   const unsigned lanes = 1u << 20;
   hipLaunchKernelGGL(k_gather, dim3(lanes / 64), dim3(64), 0, 0, tab, out);
+  hipLaunchKernelGGL(k_gather64, dim3(lanes / 64), dim3(64), 0, 0, tab, out);
   const size_t sbytes = (size_t)1 << 30;
   hipLaunchKernelGGL(k_stream, dim3(8192), dim3(256), 0, 0, (const uint4*)tab, sbytes / 16, out);
   if (hipDeviceSynchronize() != hipSuccess) return 2;
-  std::printf("{\"gather_requested_bytes\": %zu, \"stream_requested_bytes\": %zu, \"entry_bytes\": 80, "
-              "\"gathers\": %zu}\n", (size_t)lanes * GATHERS * 80, sbytes, (size_t)lanes * GATHERS);
+  std::printf("{\"gather_requested_bytes\": %zu, \"gather64_requested_bytes\": %zu, \"stream_requested_bytes\": %zu, "
+              "\"entry_bytes\": 80, \"gathers\": %zu}\n", (size_t)lanes * GATHERS * 80, (size_t)lanes * GATHERS * 64,
+              sbytes, (size_t)lanes * GATHERS);
   (void)hipFree(tab);
   (void)hipFree(out);
   return 0;
