@@ -641,12 +641,22 @@ void rebuild_class_tables(KeyState& K) {
 // group once every class is done.  A group's launches from consecutive chunks
 // queue on one lane (one hardware queue each) while the three groups run side
 // by side; lane-per-chunk instead ran each chunk's classes one after another
-// (~6 ms of serial latency per 262 k mixed chunk).  CAPJWT_CLASS_GROUPS=0:
-// lane per chunk for every submission (A/B).
+// (~6 ms of serial latency per 262 k mixed chunk).  OFF by default
+// (CAPJWT_CLASS_GROUPS=1 turns it on): the JWKS end-to-end leg of configs[4]
+// once returned one wrong verdict per pass in this mode while the background
+// upgrader was widening tables (tools/c5_e2e_probe.py); not reproduced since,
+// root cause not found, so lane-per-chunk stays the default.
 bool class_grouping() {
   static const bool on = [] {
     const char* e = std::getenv("CAPJWT_CLASS_GROUPS");
-    return !(e && std::atoi(e) == 0);
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+bool group_ctrl_copy() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_GROUP_CTRL");
+    return e && std::string(e) == "copy";
   }();
   return on;
 }
@@ -1277,9 +1287,6 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   const hipStream_t cs = d->copy;
   if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
   if (bytes) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, cs));
-  HIPCHK(hipEventRecord(S.copied, cs));
-  if (tr) HIPCHK(hipEventRecord(S.tr_b, cs));
-  if (tr) S.host_ms[3] = ms_since(t_enq);
   int nact = 0, jgrp = 0;
   double gcost[3] = {0, 0, 0};
   for (int c = 1; c < NCLS; ++c) {
@@ -1291,24 +1298,27 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   for (int g = 1; g < 3; ++g)
     if (gcost[g] > gcost[jgrp]) jgrp = g;
   const bool grouped = it.grouped && nact >= 2;
+  // grouped chunks: the whole plan block goes over by DMA behind the arena
+  // (the plan fill then reads device memory); else the header by a copy
+  // kernel and the jobs read in place from pinned memory
+  if (grouped) HIPCHK(hipMemcpyAsync(dm, hb, L.bytes, hipMemcpyHostToDevice, cs));
+  HIPCHK(hipEventRecord(S.copied, cs));
+  if (tr) HIPCHK(hipEventRecord(S.tr_b, cs));
+  if (tr) S.host_ms[3] = ms_since(t_enq);
   GroupFan gf;
   hipStream_t fs = s;                              // the plan fill's stream
   if (grouped) {
-    gf.ctrl = cs;                                  // in order after the chunk's H2D copy
     gf.join = d->lanes[jgrp].stream;
+    // CAPJWT_GROUP_CTRL=copy: plan fill on the copy stream (A/B); default:
+    // on the join lane once the copies have landed
+    gf.ctrl = group_ctrl_copy() ? cs : gf.join;
     for (int c = 1; c < NCLS; ++c) gf.cls[c] = d->lanes[cls_group(c)].stream;
     gf.start = S.ev_planned;
     for (int c = 0; c < NCLS; ++c) gf.done[c] = S.ev_cls[c];
-    fs = cs;
-  } else {
-    HIPCHK(hipStreamWaitEvent(s, S.copied, 0));
+    fs = gf.ctrl;
   }
-  // grouped chunks fill the plan on the copy stream: the whole plan block goes
-  // over by DMA (a zero-copy read of the jobs there would hold the next
-  // chunk's H2D copy behind a PCIe-bound kernel); else the header by a copy
-  // kernel and the jobs read in place from pinned memory
-  if (grouped) HIPCHK(hipMemcpyAsync(dm, hb, L.bytes, hipMemcpyHostToDevice, cs));
-  else launch_copy(hbd, dm, L.toks_off, fs);
+  if (fs != cs) HIPCHK(hipStreamWaitEvent(fs, S.copied, 0));
+  if (!grouped) launch_copy(hbd, dm, L.toks_off, fs);
   {
     PlanFillArgs fa{};
     fa.toks = (const jg_tok*)((grouped ? (const uint8_t*)dm : hbd) + L.toks_off);
@@ -1917,7 +1927,16 @@ void upgrade_loop(jg_ctx* ctx) {
     skip.clear();
     lk.unlock();
     try {
-      while (upgrade_one(ctx, skip)) {
+      // CAPJWT_DEBUG_MAX_UPGRADES=n (testing): stop after n table upgrades per
+      // process, leaving the rest of the keys on their narrow tables -- a
+      // deterministic stand-in for the window in which a class runs mixed widths
+      static const int max_up = [] {
+        const char* e = std::getenv("CAPJWT_DEBUG_MAX_UPGRADES");
+        return e ? std::atoi(e) : -1;
+      }();
+      static std::atomic<int> ups{0};
+      while ((max_up < 0 || ups.load() < max_up) && upgrade_one(ctx, skip)) {
+        ++ups;
         std::lock_guard<std::mutex> g(ctx->up_mu);
         if (ctx->up_stop) break;
       }
