@@ -22,7 +22,7 @@ EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_las
            "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_enqueue", "jg_batch_sync",
            "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
            "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_table_budget", "jg_keys_wait_tables",
-           "jg_keys_table_widths", "jg_debug_fail_alloc"]
+           "jg_keys_table_widths", "jg_debug_fail_alloc", "jg_debug_table_digest"]
 
 
 class JgKey(ctypes.Structure):
@@ -80,6 +80,7 @@ def lib():
         L.jg_keys_wait_tables.argtypes = [vp]
         L.jg_keys_table_widths.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.jg_debug_fail_alloc.argtypes = [vp, ctypes.c_int]
+        L.jg_debug_table_digest.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         L.jg_version.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -190,6 +191,13 @@ class Context:
         arr = (ctypes.c_int * max(1, n))()
         lib().jg_keys_table_widths(self.h, arr, n)
         return list(arr[:n])
+
+    def table_digest(self, key):
+        """jg_debug_table_digest: 64-bit digest of key `key`'s comb table (0 = none)."""
+        v = ctypes.c_uint64()
+        if lib().jg_debug_table_digest(self.h, int(key), ctypes.byref(v)) != 0:
+            raise JgError(f"jg_debug_table_digest: {self.error()}")
+        return v.value
 
     def debug_fail_alloc(self, n):
         """jg_debug_fail_alloc: the n-th device allocation of later key loads fails (0 = off)."""

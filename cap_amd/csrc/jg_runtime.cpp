@@ -1660,6 +1660,19 @@ void poison_table(const DevBuf& t, hipStream_t s) {
   if (on) HIPCHK(hipMemsetAsync(t.p, 0xA5, t.bytes, s));
 }
 
+// jg_debug_table_digest: an order-sensitive 64-bit digest of n words
+__global__ void k_digest(const uint32_t* __restrict__ t, uint64_t n, unsigned long long* out) {
+  unsigned long long acc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    acc += (unsigned long long)t[i] * (2ull * i + 1ull) + (i ^ t[i]);
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+void launch_digest(const uint32_t* t, uint64_t n, unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_digest, dim3(4096), dim3(256), 0, s, t, n, out);
+  HIPCHK(hipGetLastError());
+}
+
 // Launch the comb-table builds of keys (index list on the device at `didx`,
 // grouped by class and width) on stream s.
 void build_tables(const std::map<std::pair<int, int>, std::vector<int32_t>>& groups, DevKey* keys, uint32_t* blob,
@@ -2199,6 +2212,30 @@ int jg_keys_table_widths(jg_ctx* ctx, int* widths, int cap) {
   const int n = (int)ks->keys.size();
   for (int i = 0; i < n && i < cap; ++i) widths[i] = ks->dev.empty() || ks->dev[0]->kw.empty() ? 0 : ks->dev[0]->kw[(size_t)i];
   return n;
+}
+
+int jg_debug_table_digest(jg_ctx* ctx, int key, uint64_t* digest) {
+  if (!ctx || !digest || key < 0) return -1;
+  try {
+    KeyStateP ks = ctx->state();
+    if (!ks || key >= (int)ks->keys.size() || ks->dev.empty()) return -1;
+    const DevGen& G = *ks->dev[0];
+    const int w = G.kw[(size_t)key];
+    if (w == 0 || G.mirror[(size_t)key].tab == 0) { *digest = 0; return 0; }
+    Device* d = ctx->devs[0].get();
+    HIPCHK(hipSetDevice(d->id));
+    const uint64_t bytes = table_bytes(ks->keys[(size_t)key].cls, w);
+    DevBufP out = dev_alloc(d->id, sizeof(unsigned long long));
+    HIPCHK(hipMemsetAsync(out->p, 0, sizeof(unsigned long long), d->kstream));
+    launch_digest((const uint32_t*)(uintptr_t)G.mirror[(size_t)key].tab, bytes / 4, out->as<unsigned long long>(),
+                  d->kstream);
+    HIPCHK(hipMemcpyAsync(digest, out->p, sizeof(uint64_t), hipMemcpyDeviceToHost, d->kstream));
+    HIPCHK(hipStreamSynchronize(d->kstream));
+    return 0;
+  } catch (const std::exception& e) {
+    ctx->set_err(e.what());
+    return -2;
+  }
 }
 
 int jg_debug_fail_alloc(jg_ctx* ctx, int n) {

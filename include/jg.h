@@ -120,6 +120,11 @@ int jg_keys_table_widths(jg_ctx* ctx, int* widths, int cap);
  * fails as if hipMalloc ran out of memory; 0 disables.  Returns 0 or -1. */
 int jg_debug_fail_alloc(jg_ctx* ctx, int n);
 
+/* Test hook: a 64-bit digest of key `key`'s current comb table on the first
+ * device (0 when it has none) -- tables built at different times or on
+ * different paths must agree.  Returns 0, -1 or -2. */
+int jg_debug_table_digest(jg_ctx* ctx, int key, uint64_t* digest);
+
 /* Verify ntok jobs, blocking (= jg_submit + jg_wait).  Host buffers; copied to
  * the device(s) in chunks whose H2D copies overlap the kernels of the previous
  * chunk (direct DMA when `arena` is pinned -- jg_host_alloc -- else through
