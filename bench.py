@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 KEYDIR = os.path.join(ROOT, "tests", "golden", "keys")
 BENCHKEYS = os.path.join(ROOT, "tools", "benchkeys")
 TOKGEN = os.path.join(ROOT, "tools", "tokgen", "tokgen")
-TRAFFIC = os.path.join(ROOT, "profiles", "r02_s13_pmc_traffic.json")
+TRAFFIC = os.path.join(ROOT, "profiles", "r03_s14_pmc_traffic.json")
 COLL_DEVICE = "cuda"            # device of the timing all-reduce (RCCL); "cpu" under gloo
 
 # measured v_mad_u64_u32 issue rate, chip-wide: the integer multiply-add
@@ -973,6 +973,7 @@ def main():
     del pool2
     el, acc, kms, _ = measure(ctx, arena, toks, args.steps, args.warmup, dist, second=second)
     acc2 = LAST_ACCEPTED2
+    es_window = LAST_WINDOW
     del second
     ntok = len(toks)
     value = world * ntok * args.steps / el
@@ -1003,13 +1004,15 @@ def main():
         "roofline": {"bound": "valu", "kernel": "k_ec_point<P256>",
                      "achieved": achieved, "peak": MAD_PEAK_T, "unit": "TMAD/s",
                      "frac": achieved / MAD_PEAK_T, "traffic": load_traffic("p256_point"),
+                     "trace_window": es_window,
                      "note": "integer multiply-add roofline (SURVEY §8d): algorithmic 32x32->64 MADs "
-                             f"per token {p256_point_mads_per_token():.0f} x tokens / HIP-event kernel time; "
-                             "peak = measured v_mad_u64_u32 rate; traffic = HBM bytes per launch, "
-                             "2 x FETCH_SIZE + WRITE_SIZE of the rocprofv3 --pmc passes in "
-                             f"{os.path.relpath(TRAFFIC, ROOT)} (the x2 calibrated for this kernel's random "
-                             "80-byte comb-entry gathers by tools/ubench/gather_cal: 192 B of 128-B lines per "
-                             "entry, 23 entries per token)"},
+                             f"per token {p256_point_mads_per_token():.0f} x tokens / HIP-event kernel time of the "
+                             "synchronous runs (trace_window: their CLOCK_BOOTTIME span; the timed steps overlap two "
+                             "batches, so their launches share the CUs); peak = measured v_mad_u64_u32 rate; "
+                             "traffic = HBM bytes per launch, 2 x FETCH_SIZE + WRITE_SIZE of the rocprofv3 --pmc "
+                             f"passes in {os.path.relpath(TRAFFIC, ROOT)} (x2 calibrated for the packed 64-byte "
+                             "comb entries by tools/ubench/gather_cal: FETCH counts 64 B per 64-B-aligned entry, "
+                             "x2 = the 128-B line holding it; 20 entries per token)"},
         "roofline_other": roofline_line(kms, ntok, {"p256_prep": ("hbm", prep_bytes_per_token(342, 49))}),
         "kernel_ms": kms,
         "cpu": cpu,

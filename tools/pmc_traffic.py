@@ -52,11 +52,14 @@ def calibration(cal_csv, cal_json):
     agg = load(cal_csv)
     out = {}
     for (name, _), v in agg.items():
-        for tag, key in (("gather", "gather_requested_bytes"), ("stream", "stream_requested_bytes")):
-            if name.startswith("k_" + tag):
+        for tag, key in (("gather", "gather_requested_bytes"), ("gather64", "gather64_requested_bytes"),
+                         ("stream", "stream_requested_bytes")):
+            if name.startswith("k_" + tag + "(") and key in req:
                 out[tag] = {"fetch_bytes": sum(v) * 1024, "requested_bytes": req[key],
                             "fetch_per_requested_byte": sum(v) * 1024 / req[key]}
     out["gather"]["fetch_bytes_per_80B_entry"] = out["gather"]["fetch_per_requested_byte"] * 80
+    if "gather64" in out:
+        out["gather64"]["fetch_bytes_per_64B_entry"] = out["gather64"]["fetch_per_requested_byte"] * 64
     return out
 
 
@@ -71,10 +74,13 @@ def main(fetch_csv, write_csv, cal_csv, cal_json, out):
         fetch, write = fv[0], wv[0]
         res[alias] = {"symbol": sym, "grid": grid, "launches": fv[1], "fetch_bytes_raw": fetch, "write_bytes": write,
                       "hbm_bytes_per_launch": 2 * fetch + write, "hbm_bytes_per_launch_undoubled": fetch + write}
-    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes over "
-                         "`bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-configs` (tools/gpu_profile_r02.sh)",
-               "correction": "FETCH_SIZE x2: the guide's streaming-read calibration, confirmed for this repo's "
-                             "streaming and 80-byte gather patterns by `calibration` below",
+    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes over a short bench.py run "
+                         "(tools/gpu_profile_r03.sh; round 2: tools/gpu_profile_r02.sh)",
+               "correction": "FETCH_SIZE x2: the guide's streaming-read calibration; `calibration` below measures "
+                             "this repo's patterns with known byte counts (tools/ubench/gather_cal): streaming 0.5 "
+                             "FETCH per requested byte, 80-B entries 1.2 (x2 = the 1.5 128-B lines an entry "
+                             "touches), 64-B-aligned entries (P-256's packed tables since round 3) 1.0 (x2 = the "
+                             "128-B line holding the entry)",
                "calibration": calibration(cal_csv, cal_json),
                "kernels": res}, open(out, "w"), indent=1)
     for k, v in res.items():
