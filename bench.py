@@ -771,9 +771,9 @@ def run_configs(ctx, args, threads, rank, world, dist):
             "rsa4096_modexp": rsa_modexp_mads_per_token(148, 4), "p256_point": p256_point_mads_per_token(wof.get("p256")),
             "p384_point": p384_point_mads_per_token(wof.get("p384")),
             "ed25519_point": ed25519_point_mads_per_token(wof.get("ed25519", 20))}
-    chunk = 262144
+    chunk = args.c5_chunk
     line = config_line(
-        ctx, "mixed_10alg_32kid", "all 10 algs, 32 kids, 5% tampered, 10M stream on 8 GPUs in 262144-token chunks "
+        ctx, "mixed_10alg_32kid", f"all 10 algs, 32 kids, 5% tampered, 10M stream on 8 GPUs in {chunk}-token chunks "
         "(configs[4]); one chunk per step per GPU, steps alternating between the share's first two chunks",
         pool[:chunk], algs[:chunk], keyidx[:chunk], good[:chunk], chunk,
         max(1, args.steps // 2), 1, dist, world, kernels={k: v for k, v in work.items() if k.split("_")[0] in present},
@@ -896,6 +896,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--tokens", type=int, default=1 << 20, help="tokens per GPU per step")
+    ap.add_argument("--c5-chunk", type=int, default=262144, help="configs[4] resident chunk (tokens per step)")
     ap.add_argument("--pool", type=int, default=0, help="unique signed ES256 tokens (default: all unique)")
     ap.add_argument("--rs-pool", type=int, default=100000, help="unique RS256 tokens (BASELINE configs[0]: 100k)")
     ap.add_argument("--no-ab", action="store_true", help="skip the replicated-pool A/B line")

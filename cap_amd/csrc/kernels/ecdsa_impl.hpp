@@ -438,8 +438,12 @@ __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z
   }
 }
 
+// JG_EC_POINT_ATTR: per translation unit, as JG_EC_SCALAR_ATTR (occupancy A/Bs)
+#ifndef JG_EC_POINT_ATTR
+#define JG_EC_POINT_ATTR
+#endif
 template <class CV>
-__global__ void __launch_bounds__(64) k_ec_point(EcArgs a) {
+__global__ void __launch_bounds__(64) JG_EC_POINT_ATTR k_ec_point(EcArgs a) {
   using Fp = typename CV::Fp;
   using Fn = typename CV::Fn;
   constexpr int L = Fp::L;
