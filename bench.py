@@ -628,8 +628,8 @@ def c5_pool(meta, total, threads, rank, ec_unique=True):
 
 def c5_pool_note(ec_unique):
     if ec_unique:
-        return ("every EC / Ed25519 token unique over the 1,250,000-token share (the resident chunk is its first "
-                "262144); RSA tokens cycle 1024 (512 for 4096-bit kids) per kid: the modexp has no data-dependent "
+        return ("every EC / Ed25519 token unique over the 1,250,000-token share (the resident steps alternate "
+                "between its first two --c5-chunk chunks); RSA tokens cycle 1024 (512 for 4096-bit kids) per kid: the modexp has no data-dependent "
                 "gathers, so repeats cost the same")
     return "1024 (512) unique tokens per kid replicated (round-2 layout)"
 
@@ -896,7 +896,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--tokens", type=int, default=1 << 20, help="tokens per GPU per step")
-    ap.add_argument("--c5-chunk", type=int, default=262144, help="configs[4] resident chunk (tokens per step)")
+    ap.add_argument("--c5-chunk", type=int, default=625000,
+                    help="configs[4] resident chunk (tokens per step; default: half of the GPU's 1.25M share, so the "
+                         "two alternating staged chunks cover the whole share)")
     ap.add_argument("--pool", type=int, default=0, help="unique signed ES256 tokens (default: all unique)")
     ap.add_argument("--rs-pool", type=int, default=100000, help="unique RS256 tokens (BASELINE configs[0]: 100k)")
     ap.add_argument("--no-ab", action="store_true", help="skip the replicated-pool A/B line")
