@@ -74,12 +74,14 @@ def p256_point_mads_per_token(wq=None):
 
 # key comb-table width tiers, widest first (kernels/ecdsa.hpp EC_*_WQ, ed25519.hpp ED_WA)
 WIDTH_TIERS = {"p256": (26, 24, 22, 20), "p384": (24, 20, 18, 16), "ed25519": (24, 22, 20, 18, 16), "p521": (20, 18, 16)}
-# (bits + 1, entry bytes): P-256 entries are packed to 64 B (ecdsa.hpp JG_EC_PACK64)
-_TAB = {"p256": (257, 64), "p384": (385, 128), "p521": (522, 160), "ed25519": (254, 128)}
+# (bits + 2 for EC / 254 for Ed25519, entry bytes): ceil(that / W) windows
+# (ecdsa.hpp ec_windows_w, ed25519.hpp ed_windows_w); P-256 entries are packed
+# to 64 B (ecdsa.hpp JG_EC_PACK64)
+_TAB = {"p256": (258, 64), "p384": (386, 128), "p521": (523, 160), "ed25519": (254, 128)}
 
 
 def table_bytes(cls, w):
-    """Bytes of one key comb table: ceil((bits + 1) / W) windows x 2^(W-1) entries."""
+    """Bytes of one key comb table: ceil((bits + 2) / W) windows x 2^(W-1) entries."""
     bits, entry = _TAB[cls]
     return -(-bits // w) * (1 << (w - 1)) * entry
 
@@ -123,7 +125,7 @@ def ec_point_mads_per_token(L, red_row, fold, wg, wq, bits, red_generic, merged)
     nred, nfold = (10, 1) if merged else (11, 2)
     madd = 8 * L * L + 3 * L * (L + 1) // 2 + nred * red + nfold * fold
     madd_z1 = 4 * L * L + 2 * L * (L + 1) // 2 + (nred - 5) * red + nfold * fold
-    ng, nq = (bits + 1 + wg - 1) // wg, (bits + 1 + wq - 1) // wq
+    ng, nq = (bits + 2 + wg - 1) // wg, (bits + 2 + wq - 1) // wq
     adds = ng * (1 - 2.0 ** -wg) + nq * (1 - 2.0 ** -wq) - 1
     gmul, gsqr = L * L + red_generic, L * (L + 1) // 2 + red_generic
     return (adds - 1) * madd + madd_z1 + gsqr + 2 * gmul

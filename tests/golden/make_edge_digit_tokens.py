@@ -71,6 +71,26 @@ def scan_ed(kid, n, wb, wa, meta, threads):
     return hits
 
 
+def scan_p521_top_carry(kid, n, meta, threads):
+    """ES512 tokens whose u2, recoded at W = 18 over 29 windows (round 3's
+    window count), carries out of the top window (tests/test_gpu_tables.py)."""
+    toks = bench.gen_tokens("ES512", n, [meta[kid][2]], threads, "topcarry")
+    nn = ORDER["ES512"]
+    hits = []
+    for t in toks:
+        d = t.rfind(b".")
+        sig = base64.urlsafe_b64decode(t[d + 1:] + b"=" * (-len(t[d + 1:]) % 4))
+        r, s = int.from_bytes(sig[:66], "big"), int.from_bytes(sig[66:], "big")
+        u2 = r * pow(s, -1, nn) % nn
+        c = 0
+        for w in range(29):
+            v = ((u2 >> (18 * w)) & ((1 << 18) - 1)) + c
+            c = 1 if v >= (1 << 17) else 0
+        if c:
+            hits.append(t.decode())
+    return hits
+
+
 def main():
     meta = {m[0]: m for m in bench.bench_keys()}
     threads = os.cpu_count() or 1
@@ -82,6 +102,9 @@ def main():
     h = scan_ed("kid-30", 1000000, 24, 24, meta, threads)
     sets.append({"alg": "EdDSA", "kid": "kid-30", "wg": 24, "wq": 24, "tokens": [x[0] for x in h],
                  "hits": [[i, x[1], x[2]] for i, x in enumerate(h)]})
+    sets.append({"name": "p521_w18_top_carry", "alg": "ES512", "kid": "kid-27", "wg": 20, "wq": 18,
+                 "tokens": scan_p521_top_carry("kid-27", 200000, meta, threads),
+                 "hits": "u2's top W = 18 window all ones with a carry in (lost over 29 windows; 30 hold it)"})
     json.dump({"note": "valid tokens whose comb digits hit the last table entry; made by make_edge_digit_tokens.py",
                "sets": sets}, open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "edge_digit_tokens.json"), "w"),
               indent=1)
