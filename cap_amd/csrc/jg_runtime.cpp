@@ -641,15 +641,14 @@ void rebuild_class_tables(KeyState& K) {
 // group once every class is done.  A group's launches from consecutive chunks
 // queue on one lane (one hardware queue each) while the three groups run side
 // by side; lane-per-chunk instead ran each chunk's classes one after another
-// (~6 ms of serial latency per 262 k mixed chunk).  OFF by default
-// (CAPJWT_CLASS_GROUPS=1 turns it on): the JWKS end-to-end leg of configs[4]
-// once returned one wrong verdict per pass in this mode while the background
-// upgrader was widening tables (tools/c5_e2e_probe.py); not reproduced since,
-// root cause not found, so lane-per-chunk stays the default.
+// (~6 ms of serial latency per 262 k mixed chunk).  CAPJWT_CLASS_GROUPS=0:
+// lane per chunk for every submission (A/B).  (The wrong ES512 verdicts once
+// seen in this mode were the P-521 W = 18 lost top-window carry, ecdsa.hpp
+// ec_windows_w, which hit lane-per-chunk runs the same way.)
 bool class_grouping() {
   static const bool on = [] {
     const char* e = std::getenv("CAPJWT_CLASS_GROUPS");
-    return e && std::atoi(e) != 0;
+    return !(e && std::atoi(e) == 0);
   }();
   return on;
 }
