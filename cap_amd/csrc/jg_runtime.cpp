@@ -1675,7 +1675,7 @@ void launch_digest(const uint32_t* t, uint64_t n, unsigned long long* out, hipSt
 // Launch the comb-table builds of keys (index list on the device at `didx`,
 // grouped by class and width) on stream s.
 void build_tables(const std::map<std::pair<int, int>, std::vector<int32_t>>& groups, DevKey* keys, uint32_t* blob,
-                  int32_t* didx, hipStream_t s) {
+                  int32_t* didx, hipStream_t s, bool sliced = false) {
   std::vector<int32_t> all;
   std::vector<std::pair<size_t, size_t>> span;
   for (const auto& g : groups) {
@@ -1689,8 +1689,8 @@ void build_tables(const std::map<std::pair<int, int>, std::vector<int32_t>>& gro
     const int c = g.first.first, w = g.first.second;
     int32_t* ix = didx + span[i].first;
     const int n = (int)span[i].second;
-    if (c == CLS_ED25519) launch_ed_keytables(w, keys, blob, ix, n, s);
-    else launch_ec_keytables(c, w, keys, blob, ix, n, s);
+    if (c == CLS_ED25519) launch_ed_keytables(w, keys, blob, ix, n, s, sliced);
+    else launch_ec_keytables(c, w, keys, blob, ix, n, s, sliced);
     ++i;
   }
   HIPCHK(hipGetLastError());
@@ -1890,7 +1890,9 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
     HIPCHK(hipMemcpyAsync((char*)tmp->p + sizeof(DevKey), &zero, sizeof zero, hipMemcpyHostToDevice, d->ustream));
     std::map<std::pair<int, int>, std::vector<int32_t>> groups;
     groups[{cls, w}].push_back(0);
-    build_tables(groups, tmp->as<DevKey>(), G.keyblob(), (int32_t*)((char*)tmp->p + sizeof(DevKey)), d->ustream);
+    // sliced: the upgrade stream may share a hardware queue with a verify
+    // lane, which then waits at most one slice behind it (tables.hpp)
+    build_tables(groups, tmp->as<DevKey>(), G.keyblob(), (int32_t*)((char*)tmp->p + sizeof(DevKey)), d->ustream, true);
     built[i] = t;
   }
   // publish against whatever state is current now (a load may have replaced

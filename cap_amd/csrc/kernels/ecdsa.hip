@@ -11,11 +11,14 @@ void launch_ec_p256(const EcArgs& a, hipStream_t s, const Marker& mk);
 void launch_ec_p384(const EcArgs& a, hipStream_t s, const Marker& mk);
 void launch_ec_p521(const EcArgs& a, hipStream_t s, const Marker& mk);
 void launch_ec_keyprep_p256(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);
-void launch_ec_keytables_p256(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s);
+void launch_ec_keytables_p256(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s,
+                              bool sliced);
 void launch_ec_keyprep_p384(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);
-void launch_ec_keytables_p384(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s);
+void launch_ec_keytables_p384(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s,
+                              bool sliced);
 void launch_ec_keyprep_p521(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);
-void launch_ec_keytables_p521(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s);
+void launch_ec_keytables_p521(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s,
+                              bool sliced);
 void launch_ec_gtable_p256(uint32_t* tab, hipStream_t s);
 void launch_ec_gtable_p384(uint32_t* tab, hipStream_t s);
 void launch_ec_gtable_p521(uint32_t* tab, hipStream_t s);
@@ -40,12 +43,13 @@ void launch_ec_keyprep(int cls, DevKey* keys, uint32_t* blob, const int32_t* idx
   }
 }
 
-void launch_ec_keytables(int cls, int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
+void launch_ec_keytables(int cls, int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s,
+                         bool sliced) {
   if (tn <= 0) return;
   switch (cls) {
-    case CLS_P256: launch_ec_keytables_p256(wq, keys, blob, tidx, tn, s); break;
-    case CLS_P384: launch_ec_keytables_p384(wq, keys, blob, tidx, tn, s); break;
-    case CLS_P521: launch_ec_keytables_p521(wq, keys, blob, tidx, tn, s); break;
+    case CLS_P256: launch_ec_keytables_p256(wq, keys, blob, tidx, tn, s, sliced); break;
+    case CLS_P384: launch_ec_keytables_p384(wq, keys, blob, tidx, tn, s, sliced); break;
+    case CLS_P521: launch_ec_keytables_p521(wq, keys, blob, tidx, tn, s, sliced); break;
     default: break;
   }
 }

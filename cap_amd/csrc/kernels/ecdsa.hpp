@@ -117,6 +117,6 @@ void launch_ec_keyprep(int cls, jgk::DevKey* keys, uint32_t* blob, const int32_t
 // comb tables (width wq) of the valid keys tidx[0..tn), written at each key's
 // `tab` (ec_table_words_w(cls, wq) words); after launch_ec_keyprep
 void launch_ec_keytables(int cls, int wq, jgk::DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn,
-                         hipStream_t s);
+                         hipStream_t s, bool sliced = false);
 // generator table for a curve into `tab` (ec_table_words(cls) words)
 void launch_ec_gtable(int cls, uint32_t* tab, hipStream_t s);

@@ -26,6 +26,7 @@
 #include "common.hpp"
 #include "ecdsa.hpp"
 #include "mp.hpp"
+#include "tables.hpp"
 
 using namespace jgk;
 
@@ -740,12 +741,12 @@ __global__ void k_ec_table_base_keys(const DevKey* keys, uint32_t* blob, const i
 }
 
 template <class CV>
-__global__ void k_ec_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+__global__ void k_ec_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n, int e0, int e1) {
   constexpr int W = CV::WQ, NWIN = ec_windows_w(CV::CLS, CV::WQ);
   constexpr int NE = 1 << (CV::WQ - 1), STRIDE = ec_stride(CV::CLS);
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
-  if (k >= n || e >= NWIN * NE || e % NE == 0) return;
+  if (k >= n || e >= e1 || e >= NWIN * NE || e % NE == 0) return;
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
   uint32_t* tab = (uint32_t*)K.tab;
@@ -802,14 +803,18 @@ void keyprep_chain(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipS
   if (n > 0) hipLaunchKernelGGL(k_ec_keyprep<CV>, dim3((n + 63) / 64), dim3(64), 0, s, keys, blob, idx, n);
 }
 
-// comb tables of keys tidx[0..tn) at CV::WQ, written to each key's `tab`
+// comb tables of keys tidx[0..tn) at CV::WQ, written to each key's `tab`;
+// `sliced`: the entries in launches of TABLE_SLICE threads, the stream
+// synchronised after each (table_slices)
 template <class CV>
-void keytables_chain(DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
+void keytables_chain(DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s, bool sliced) {
   constexpr int NWIN = ec_windows_w(CV::CLS, CV::WQ), NE = 1 << (CV::WQ - 1);
   if (tn <= 0) return;
   dim3 b(64);
   hipLaunchKernelGGL(k_ec_table_base_keys<CV>, dim3((NWIN + 63) / 64, tn), b, 0, s, keys, blob, tidx, tn);
-  hipLaunchKernelGGL(k_ec_table_keys<CV>, dim3((NWIN * NE + 63) / 64, tn), b, 0, s, keys, blob, tidx, tn);
+  table_slices(NWIN * NE, tn, sliced, s, [&](int e0, int e1, dim3 g) {
+    hipLaunchKernelGGL(k_ec_table_keys<CV>, g, b, 0, s, keys, blob, tidx, tn, e0, e1);
+  });
 }
 
 template <class CV>

@@ -13,11 +13,12 @@ void launch_ec_keyprep_p384(DevKey* keys, uint32_t* blob, const int32_t* idx, in
   keyprep_chain<CurveP384W<16>>(keys, blob, idx, n, s);
 }
 
-void launch_ec_keytables_p384(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
-  if (wq == 24) keytables_chain<CurveP384W<24>>(keys, blob, tidx, tn, s);
-  else if (wq == 20) keytables_chain<CurveP384W<20>>(keys, blob, tidx, tn, s);
-  else if (wq == 18) keytables_chain<CurveP384W<18>>(keys, blob, tidx, tn, s);
-  else keytables_chain<CurveP384W<16>>(keys, blob, tidx, tn, s);
+void launch_ec_keytables_p384(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s,
+                              bool sliced) {
+  if (wq == 24) keytables_chain<CurveP384W<24>>(keys, blob, tidx, tn, s, sliced);
+  else if (wq == 20) keytables_chain<CurveP384W<20>>(keys, blob, tidx, tn, s, sliced);
+  else if (wq == 18) keytables_chain<CurveP384W<18>>(keys, blob, tidx, tn, s, sliced);
+  else keytables_chain<CurveP384W<16>>(keys, blob, tidx, tn, s, sliced);
 }
 
 void launch_ec_gtable_p384(uint32_t* tab, hipStream_t s) { gtable_chain<CurveP384W<16>>(tab, s); }

@@ -13,10 +13,11 @@ void launch_ec_keyprep_p521(DevKey* keys, uint32_t* blob, const int32_t* idx, in
   keyprep_chain<CurveP521W<16>>(keys, blob, idx, n, s);
 }
 
-void launch_ec_keytables_p521(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
-  if (wq == 20) keytables_chain<CurveP521W<20>>(keys, blob, tidx, tn, s);
-  else if (wq == 18) keytables_chain<CurveP521W<18>>(keys, blob, tidx, tn, s);
-  else keytables_chain<CurveP521W<16>>(keys, blob, tidx, tn, s);
+void launch_ec_keytables_p521(int wq, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s,
+                              bool sliced) {
+  if (wq == 20) keytables_chain<CurveP521W<20>>(keys, blob, tidx, tn, s, sliced);
+  else if (wq == 18) keytables_chain<CurveP521W<18>>(keys, blob, tidx, tn, s, sliced);
+  else keytables_chain<CurveP521W<16>>(keys, blob, tidx, tn, s, sliced);
 }
 
 void launch_ec_gtable_p521(uint32_t* tab, hipStream_t s) { gtable_chain<CurveP521W<16>>(tab, s); }

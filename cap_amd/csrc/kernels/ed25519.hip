@@ -18,6 +18,7 @@
 #include "common.hpp"
 #include "ed25519.hpp"
 #include "mp.hpp"
+#include "tables.hpp"
 
 using namespace jgk;
 
@@ -381,11 +382,11 @@ __global__ void k_ed_table_base_keys(const DevKey* keys, uint32_t* blob, const i
 }
 
 template <int W>
-__global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n) {
+__global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_t* idx, int n, int e0, int e1) {
   constexpr int NWIN = ed_windows_w(W), NE = 1 << (W - 1);
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = e0 + blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
-  if (k >= n || e >= NWIN * NE || e % NE == 0) return;
+  if (k >= n || e >= e1 || e >= NWIN * NE || e % NE == 0) return;
   const DevKey& K = keys[idx[k]];
   if (!K.valid) return;
   uint32_t* tab = (uint32_t*)K.tab;
@@ -416,10 +417,12 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
 
 namespace {
 template <int W>
-void ed_tables(DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
+void ed_tables(DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s, bool sliced) {
   constexpr int NWIN = ed_windows_w(W), NE = 1 << (W - 1);
   hipLaunchKernelGGL(k_ed_table_base_keys<W>, dim3((NWIN + 63) / 64, tn), dim3(64), 0, s, keys, blob, tidx, tn);
-  hipLaunchKernelGGL(k_ed_table_keys<W>, dim3((NWIN * NE + 63) / 64, tn), dim3(64), 0, s, keys, blob, tidx, tn);
+  table_slices(NWIN * NE, tn, sliced, s, [&](int e0, int e1, dim3 g) {
+    hipLaunchKernelGGL(k_ed_table_keys<W>, g, dim3(64), 0, s, keys, blob, tidx, tn, e0, e1);
+  });
 }
 }  // namespace
 
@@ -428,14 +431,14 @@ void launch_ed_keyprep(DevKey* keys, uint32_t* blob, const int32_t* idx, int n, 
   hipLaunchKernelGGL(k_ed_decode, dim3((n + 63) / 64), dim3(64), 0, s, keys, blob, idx, n);
 }
 
-void launch_ed_keytables(int wa, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s) {
+void launch_ed_keytables(int wa, DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s, bool sliced) {
   if (tn <= 0) return;
   switch (wa) {
-    case 24: ed_tables<24>(keys, blob, tidx, tn, s); break;
-    case 22: ed_tables<22>(keys, blob, tidx, tn, s); break;
-    case 20: ed_tables<20>(keys, blob, tidx, tn, s); break;
-    case 18: ed_tables<18>(keys, blob, tidx, tn, s); break;
-    default: ed_tables<16>(keys, blob, tidx, tn, s); break;
+    case 24: ed_tables<24>(keys, blob, tidx, tn, s, sliced); break;
+    case 22: ed_tables<22>(keys, blob, tidx, tn, s, sliced); break;
+    case 20: ed_tables<20>(keys, blob, tidx, tn, s, sliced); break;
+    case 18: ed_tables<18>(keys, blob, tidx, tn, s, sliced); break;
+    default: ed_tables<16>(keys, blob, tidx, tn, s, sliced); break;
   }
 }
 

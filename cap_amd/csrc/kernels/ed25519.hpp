@@ -45,5 +45,6 @@ void launch_ed(const EdArgs& a, hipStream_t s, const jgk::Marker& mk);
 // aux_off) and mark validity
 void launch_ed_keyprep(jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, int n, hipStream_t s);
 // comb tables of -A (width wa) of the valid keys tidx[0..tn), at each key's `tab`
-void launch_ed_keytables(int wa, jgk::DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s);
+void launch_ed_keytables(int wa, jgk::DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s,
+                         bool sliced = false);
 void launch_ed_btable(uint32_t* tab, hipStream_t s);
