@@ -164,6 +164,8 @@ inline size_t grow_size(size_t n, size_t cap) {
   return (want + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
 }
 
+std::atomic<int> g_grows{0};      // CAPJWT_PIPE_TRACE: Grow / HGrow reallocations so far
+
 struct Grow {                     // grow-only device allocation
   void* p = nullptr;
   size_t cap = 0;
@@ -174,6 +176,7 @@ struct Grow {                     // grow-only device allocation
       p = nullptr;
       const size_t c = grow_size(n, cap);
       cap = 0;
+      g_grows.fetch_add(1, std::memory_order_relaxed);
       HIPCHK(hipMalloc(&p, c));
       cap = c;
     }
@@ -193,6 +196,7 @@ struct HGrow {                    // grow-only pinned host allocation
       p = dp = nullptr;
       const size_t want = grow_size(n, cap);
       cap = 0;
+      g_grows.fetch_add(1, std::memory_order_relaxed);
       HIPCHK(hipHostMalloc(&p, want, hipHostMallocPortable | hipHostMallocMapped));
       HIPCHK(hipHostGetDevicePointer(&dp, p, 0));
       cap = want;
@@ -453,7 +457,8 @@ struct Slot {
   hipEvent_t copied = nullptr;     // copy stream: the chunk's inputs are on the device
   hipEvent_t tr_a = nullptr, tr_b = nullptr, tr_c = nullptr;   // CAPJWT_PIPE_TRACE: H2D start / end, kernels end
   hipEvent_t ev_planned = nullptr, ev_cls[NCLS] = {};            // class-grouped chunks (GroupFan)
-  double host_ms[4] = {};                                       // wait, plan, enqueue, of which H2D calls
+  double host_ms[5] = {};                                       // wait, plan, enqueue, of which H2D calls, of which sizing
+  int grows = 0;                                                // buffer reallocations while enqueuing (trace)
   int chunk_no = 0;
   size_t reserved = 0;             // chunk capacity (jobs) the buffers were sized for
   uint64_t reserved_epoch = ~0ull; // key table they were sized against
@@ -1150,8 +1155,8 @@ void finish_slot(Slot& S) {
     (void)hipEventElapsedTime(&b, g_trace_ref, S.tr_b);
     (void)hipEventElapsedTime(&c, g_trace_ref, S.tr_c);
     (void)hipEventElapsedTime(&dn, g_trace_ref, S.done);
-    std::fprintf(stderr, "[pipe] chunk %3d n=%7zu host wait %.3f plan %.3f enq %.3f (h2d calls %.3f) | gpu h2d %.3f-%.3f kern-end %.3f done %.3f ms\n",
-                 S.chunk_no, S.n, S.host_ms[0], S.host_ms[1], S.host_ms[2], S.host_ms[3], a, b, c, dn);
+    std::fprintf(stderr, "[pipe] chunk %3d n=%7zu host wait %.3f plan %.3f enq %.3f (h2d calls %.3f, sizing %.3f, grows %d) | gpu h2d %.3f-%.3f kern-end %.3f done %.3f ms\n",
+                 S.chunk_no, S.n, S.host_ms[0], S.host_ms[1], S.host_ms[2], S.host_ms[3], S.host_ms[4], S.grows, a, b, c, dn);
   }
   S.inflight = false;
   auto t = std::move(S.ticket);
@@ -1170,6 +1175,10 @@ void finish_slot(Slot& S) {
 void reserve_slot(const KeyState& K, Slot& S, size_t C, size_t nbuckets, double bytes_per_job) {
   const PlanBlock L(nbuckets, C);
   S.h_meta.get(L.bytes);
+  // the plan block's device copy too: grown per chunk size, its hipFree
+  // stalled the host 2.5-4.5 ms behind the whole device on each slot's first
+  // larger chunk (CAPJWT_PIPE_TRACE "grows")
+  S.bufs.meta.get(L.bytes);
   S.h_verdict.get(C);
   int sig_rows = 1, scratch_rows = 1;
   bool rsa = false;
@@ -1200,6 +1209,7 @@ void reserve_slot(const KeyState& K, Slot& S, size_t C, size_t nbuckets, double 
 
 void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_tok* toks, size_t n, uint8_t* out) {
   const auto t_start = std::chrono::steady_clock::now();
+  const int grows0 = g_grows.load(std::memory_order_relaxed);
   const KeyState& K = *it.ks;
   const DevGen& G = *K.dev[dslot];
   if (S.reserved != it.chunk || S.reserved_epoch != K.epoch) {
@@ -1282,6 +1292,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   S.bufs.jobs.get(sizeof(JobDev) * P.npad);
   S.bufs.perm.get(sizeof(int32_t) * P.npad);
   uint8_t* dm = (uint8_t*)S.bufs.meta.get(L.bytes);
+  if (tr) S.host_ms[4] = ms_since(t_enq);
   const uint8_t* hbd = (const uint8_t*)S.h_meta.dp;
   const hipStream_t cs = d->copy;
   if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
@@ -1343,6 +1354,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(S.done, s));
   if (tr) S.host_ms[2] = ms_since(t_enq);
+  if (tr) S.grows = g_grows.load(std::memory_order_relaxed) - grows0;
   S.ticket = it.t;
   S.ks = it.ks;
   S.out = out;
