@@ -116,12 +116,20 @@ uint64_t default_table_budget() {
 // chunks ramp up from 4096 jobs (the copy engine starts after a short host
 // plan) and the tail ends in a quarter-size chunk (little kernel time left
 // exposed after the last copy).
-std::vector<size_t> chunk_cuts(size_t lo, size_t hi, size_t C, size_t first = 4096) {
+// The last chunk is split off at C/4 (`tail`) so an H2D-bound stream exposes
+// less compute after its last copy; class-grouped (mixed) streams are
+// compute-bound and skip it (tail = false): 524 k chunks of configs[4]
+// 25.5-25.9 -> 24.5-25.1 ms per 1.25 M tokens (profiles/r03_s23_c5_tail_ab.txt).
+std::vector<size_t> chunk_cuts(size_t lo, size_t hi, size_t C, size_t first = 4096, bool tail_chunk = true) {
   std::vector<size_t> cut{lo};
   for (size_t ramp = std::min<size_t>(C, first); cut.back() < hi; ramp = std::min(C, 2 * ramp))
     cut.push_back(std::min(hi, cut.back() + ramp));
+  static const bool split_tail = [] {           // CAPJWT_TAIL_SPLIT=0: never a short last chunk (A/B)
+    const char* e = std::getenv("CAPJWT_TAIL_SPLIT");
+    return !(e && std::atoi(e) == 0);
+  }();
   const size_t tail = C / 4;
-  if (cut.size() > 2 && tail >= 1024 && cut.back() - cut[cut.size() - 2] > tail)
+  if (split_tail && tail_chunk && cut.size() > 2 && tail >= 1024 && cut.back() - cut[cut.size() - 2] > tail)
     cut.insert(cut.end() - 1, cut.back() - tail);
   return cut;
 }
@@ -2029,7 +2037,7 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
     // grouped chunks serialise each class group's launches on one lane, so a
     // long ramp of small chunks would queue latency-bound launches (an
     // RSA-4096 modexp takes ~1.5 ms at any size): start at C / 4
-    it.cuts = chunk_cuts(it.lo, it.hi, C, it.grouped ? std::max<size_t>(4096, C / 4) : 4096);
+    it.cuts = chunk_cuts(it.lo, it.hi, C, it.grouped ? std::max<size_t>(4096, C / 4) : 4096, !it.grouped);
     it.nchunks = it.cuts.size() - 1;
     t->pending += it.nchunks;
     items.push_back(std::move(it));
