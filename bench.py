@@ -149,6 +149,24 @@ def p384_point_mads_per_token(wq=None, nkeys=1):
     return ec_point_mads_per_token(15, 4, 5, 20, wq or p384_key_w(nkeys, P384_BUDGET), 384, 15 * 12, merged=False)
 
 
+def p521_key_w(nkeys, budget):
+    """The P-521 key comb width of a load holding `nkeys` P-521 keys and
+    nothing else (W = 20 / 18 / 16)."""
+    return key_widths({"p521": nkeys}, budget)["p521"]
+
+
+def p521_point_mads_per_token(wq=None, nkeys=1):
+    """P-521 (ecdsa.hpp: L = 20 28-bit limbs, G W = 20, key W = 20 / 18 / 16
+    by the table budget): p = 2^521 - 1, so m + 1 = 2^521 has ONE non-zero
+    28-bit limb (M1[18] = 2^17, field_consts.hpp P521P) and a Montgomery
+    reduction row is one constant MAD (the unmasked rows' hi32 * 16 carry MADs
+    are carries, not counted); Y3's two products share one reduction
+    (ecdsa_impl.hpp y3_from, sum_ok), X3 = r^2 - hhh - 2v is one value fold
+    through freduce (2^521 = 1 mod p: FOLDC = 1, one MAD); the final check's
+    generic reduction is the same one-constant row."""
+    return ec_point_mads_per_token(20, 1, 1, 20, wq or p521_key_w(nkeys, P384_BUDGET), 521, 20 * 1, merged=True)
+
+
 def ed25519_point_mads_per_token(wa=24):
     """k_ed_point: 11 comb windows of the base point (W = 24) + ceil(254 / wa)
     of the key (ed25519.hpp ED_WA: W = 24 / 22 / 20 / 18 / 16 by the table
@@ -717,7 +735,8 @@ def run_configs(ctx, args, threads, rank, world, dist):
     ctx.load_keys(abi_keys(["rsa4096-a"]))
     pool = gen_tokens("PS512", 4096, golden_keypaths(["rsa4096-a"]), threads, f"c2r{rank}")
     out["ps512_rsa4096"] = config_line(
-        ctx, "ps512_rsa4096", "PS512 RSA-4096 (PSS/MGF1-SHA512), 1M tokens / 8 GPUs = 131072 per GPU (configs[2])",
+        ctx, "ps512_rsa4096", "PS512 RSA-4096 (PSS/MGF1-SHA512), 1M tokens / 8 GPUs = 131072 per GPU (configs[2]); "
+        "a 4096-token signed pool replicated 32x (the modexp has no data-dependent gathers)",
         pool, [ALG_IDS["PS512"]] * len(pool), [0] * len(pool), np.ones(len(pool), bool), 131072,
         max(1, args.steps // 2), 1, dist, world,
         kernels={"rsa4096_modexp": rsa_modexp_mads_per_token(148, 4),
@@ -768,10 +787,11 @@ def run_configs(ctx, args, threads, rank, world, dist):
         return "ed25519"
     kcls = [key_class(m[4]) for m in meta]
     present = set(kcls)
-    wof = {c: next(w for w, k in zip(c5w, kcls) if k == c) for c in ("p256", "p384", "ed25519") if c in kcls}
+    wof = {c: next(w for w, k in zip(c5w, kcls) if k == c) for c in ("p256", "p384", "p521", "ed25519") if c in kcls}
     work = {"rsa2048_modexp": rsa_modexp_mads_per_token(74, 2), "rsa3072_modexp": rsa_modexp_mads_per_token(112, 4),
             "rsa4096_modexp": rsa_modexp_mads_per_token(148, 4), "p256_point": p256_point_mads_per_token(wof.get("p256")),
             "p384_point": p384_point_mads_per_token(wof.get("p384")),
+            "p521_point": p521_point_mads_per_token(wof.get("p521")),
             "ed25519_point": ed25519_point_mads_per_token(wof.get("ed25519", 20))}
     chunk = args.c5_chunk
     line = config_line(
@@ -1103,7 +1123,7 @@ def main():
         except (OSError, subprocess.CalledProcessError, ValueError) as e:
             result["cpu_baseline_openssl_error"] = str(e)
         if "es256" in ossl:
-            result["cpu_baseline"] = dict(ossl["es256"], kind="port", cpu=cpu,
+            result["cpu_baseline"] = dict(ossl["es256"], kind="openssl", cpu=cpu,
                                           label="OpenSSL, not Go: OpenSSL 3 libcrypto EVP_DigestVerify (tools/cpuverify) "
                                                 "on the same tokens and keys; Go is absent on the GPU box")
         else:

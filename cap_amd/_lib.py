@@ -22,7 +22,8 @@ EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_las
            "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_enqueue", "jg_batch_sync",
            "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
            "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_table_budget", "jg_keys_wait_tables",
-           "jg_keys_table_widths", "jg_debug_fail_alloc", "jg_debug_table_digest"]
+           "jg_keys_table_widths", "jg_debug_fail_alloc", "jg_debug_table_digest",
+           "jg_debug_max_upgrades"]
 
 
 class JgKey(ctypes.Structure):
@@ -80,6 +81,7 @@ def lib():
         L.jg_keys_wait_tables.argtypes = [vp]
         L.jg_keys_table_widths.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.jg_debug_fail_alloc.argtypes = [vp, ctypes.c_int]
+        L.jg_debug_max_upgrades.argtypes = [vp, ctypes.c_int]
         L.jg_debug_table_digest.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         L.jg_version.restype = ctypes.c_char_p
         _lib = L
@@ -198,6 +200,11 @@ class Context:
         if lib().jg_debug_table_digest(self.h, int(key), ctypes.byref(v)) != 0:
             raise JgError(f"jg_debug_table_digest: {self.error()}")
         return v.value
+
+    def debug_max_upgrades(self, n):
+        """jg_debug_max_upgrades: the background upgrader widens at most n more tables (-1 = no limit)."""
+        if lib().jg_debug_max_upgrades(self.h, int(n)) != 0:
+            raise JgError("jg_debug_max_upgrades failed")
 
     def debug_fail_alloc(self, n):
         """jg_debug_fail_alloc: the n-th device allocation of later key loads fails (0 = off)."""

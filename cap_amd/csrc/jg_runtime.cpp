@@ -72,7 +72,7 @@ bool pipe_trace() {
   static const bool on = std::getenv("CAPJWT_PIPE_TRACE") != nullptr;
   return on;
 }
-hipEvent_t g_trace_ref = nullptr;
+hipEvent_t g_trace_ref = nullptr;     // first chunk's H2D start (trace only)
 
 // CAPJWT_RELEASE_GTABLES=1: free a device's fixed-base tables when the last
 // context using them is destroyed (default: kept for the process, ~31 GB per device)
@@ -82,7 +82,7 @@ bool release_gtables() {
     return e && std::atoi(e) != 0;
   }();
   return on;
-}     // first chunk's H2D start (trace only)
+}
 
 double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -320,7 +320,21 @@ DevBufP dev_alloc(int dev, size_t bytes, std::atomic<int>* fail = nullptr) {
   b->dev = dev;
   b->bytes = std::max<size_t>(bytes, 16);
   HIPCHK(hipSetDevice(dev));
-  HIPCHK(hipMalloc(&b->p, b->bytes));
+  hipError_t e = hipMalloc(&b->p, b->bytes);
+  if (e == hipErrorOutOfMemory && reaper().pending(dev) > 0) {
+    // free_hbm() counts memory the reaper has been handed but not yet freed
+    // (its hipFree waits for the whole device): wait for it and try once more
+    (void)hipGetLastError();
+    b->p = nullptr;
+    reaper().drain();
+    e = hipMalloc(&b->p, b->bytes);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    b->p = nullptr;
+    throw std::runtime_error(std::string("hipMalloc(") + std::to_string(b->bytes >> 20) + " MiB): " +
+                             hipGetErrorString(e));
+  }
   return b;
 }
 
@@ -557,6 +571,12 @@ struct jg_ctx {
   std::atomic<size_t> chunk{chunk_jobs()};   // jobs per pipeline chunk
   std::atomic<uint64_t> table_budget{default_table_budget()};   // HBM for key comb tables, all curves
   std::atomic<int> fail_alloc{0};            // jg_debug_fail_alloc countdown
+  // jg_debug_max_upgrades: background table upgrades left before the upgrader
+  // stops (-1 = no limit); CAPJWT_DEBUG_MAX_UPGRADES sets the initial value
+  std::atomic<int> upgrades_left{[] {
+    const char* e = std::getenv("CAPJWT_DEBUG_MAX_UPGRADES");
+    return e ? std::atoi(e) : -1;
+  }()};
   // the published key table (KeyState): swapped whole under ks_mu
   std::mutex ks_mu;
   KeyStateP ks;
@@ -1961,16 +1981,12 @@ void upgrade_loop(jg_ctx* ctx) {
     skip.clear();
     lk.unlock();
     try {
-      // CAPJWT_DEBUG_MAX_UPGRADES=n (testing): stop after n table upgrades per
-      // process, leaving the rest of the keys on their narrow tables -- a
-      // deterministic stand-in for the window in which a class runs mixed widths
-      static const int max_up = [] {
-        const char* e = std::getenv("CAPJWT_DEBUG_MAX_UPGRADES");
-        return e ? std::atoi(e) : -1;
-      }();
-      static std::atomic<int> ups{0};
-      while ((max_up < 0 || ups.load() < max_up) && upgrade_one(ctx, skip)) {
-        ++ups;
+      // jg_debug_max_upgrades (testing): stop after n table upgrades, leaving
+      // the rest of the keys on their narrow tables -- a deterministic
+      // stand-in for the window in which a class runs mixed widths
+      while (ctx->upgrades_left.load() != 0 && upgrade_one(ctx, skip)) {
+        int left = ctx->upgrades_left.load();
+        while (left > 0 && !ctx->upgrades_left.compare_exchange_weak(left, left - 1)) {}
         std::lock_guard<std::mutex> g(ctx->up_mu);
         if (ctx->up_stop) break;
       }
@@ -2262,6 +2278,18 @@ int jg_debug_table_digest(jg_ctx* ctx, int key, uint64_t* digest) {
 int jg_debug_fail_alloc(jg_ctx* ctx, int n) {
   if (!ctx || n < 0) return -1;
   ctx->fail_alloc.store(n);
+  return 0;
+}
+
+int jg_debug_max_upgrades(jg_ctx* ctx, int n) {
+  if (!ctx || n < -1) return -1;
+  ctx->upgrades_left.store(n);
+  KeyStateP cur = ctx->state();
+  if (n != 0 && cur && !cur->dev.empty() && needs_upgrade(*cur)) {   // resume widening
+    std::lock_guard<std::mutex> g(ctx->up_mu);
+    ctx->up_pending = true;
+    ctx->up_cv.notify_all();
+  }
   return 0;
 }
 

@@ -92,7 +92,7 @@ constexpr int64_t ec_table_words(int cls, bool gen) { return ec_table_words_w(cl
 // additions per token with the W = 26 generator), 24 (11 windows, 7.4 GB), 22
 // (12, 2.0 GB), 20 (13, 545 MB); P-384: 24 (17 windows, 18.3 GB), 20 (20
 // windows, 1.34 GB), 18 (22, 369 MB), 16 (25, 105 MB); P-521: 20 (27, 2.26 GB),
-// 18 (29, 608 MB), 16 (33, 173 MB).  The runtime picks one width per curve
+// 18 (30, 629 MB), 16 (33, 173 MB).  The runtime picks one width per curve
 // from the context's table budget, a single total over every curve's key
 // tables (jg_runtime.cpp key_widths); the narrowest width is always allowed.
 constexpr int EC_P256_WQ[4] = {26, 24, 22, 20};

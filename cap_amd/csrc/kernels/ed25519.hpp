@@ -38,6 +38,13 @@ constexpr int ed_windows(bool base) { return ed_windows_w(ed_comb_w(base)); }
 constexpr int64_t ed_table_words_w(int w) { return (int64_t)ed_windows_w(w) * (1 << (w - 1)) * ED_STRIDE; }
 constexpr int64_t ed_table_words(bool base) { return ed_table_words_w(ed_comb_w(base)); }
 constexpr int ED_WA[5] = {24, 22, 20, 18, 16};   // key-table width tiers, widest first
+// recode (ed25519.hip) carries out of a window when its value exceeds 2^(W-1):
+// the top window must hold at most W - 1 bits of a scalar < 2^253 (its value
+// + the incoming carry then stays <= 2^(W-1) and no carry leaves the last digit)
+constexpr bool ed_top_window_ok(int w) { return 253 - w * (ed_windows_w(w) - 1) <= w - 1; }
+static_assert(ed_top_window_ok(ed_comb_w(true)) && ed_top_window_ok(24) && ed_top_window_ok(22) &&
+              ed_top_window_ok(20) && ed_top_window_ok(18) && ed_top_window_ok(16),
+              "Ed25519 comb window count leaves no room for the top carry");
 constexpr int ED_MAX_KEYS = 256;
 
 void launch_ed(const EdArgs& a, hipStream_t s, const jgk::Marker& mk);

@@ -120,6 +120,12 @@ int jg_keys_table_widths(jg_ctx* ctx, int* widths, int cap);
  * fails as if hipMalloc ran out of memory; 0 disables.  Returns 0 or -1. */
 int jg_debug_fail_alloc(jg_ctx* ctx, int n);
 
+/* Test hook: the background upgrader widens at most n more comb tables of
+ * this context (-1 = no limit, the default; CAPJWT_DEBUG_MAX_UPGRADES sets
+ * the initial value), so a class can be held at mixed widths; raising it
+ * resumes widening.  Returns 0 or -1. */
+int jg_debug_max_upgrades(jg_ctx* ctx, int n);
+
 /* Test hook: a 64-bit digest of key `key`'s current comb table on the first
  * device (0 when it has none) -- tables built at different times or on
  * different paths must agree.  Returns 0, -1 or -2. */

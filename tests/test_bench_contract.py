@@ -48,3 +48,17 @@ def test_point_mads_follow_the_window_count():
     assert abs((m[22] - m[24]) - per_add) < 1 and abs((m[20] - m[22]) - per_add) < 1
     # a mixed addition: 8 mul + 3 sqr (L = 10) under 10 reductions of 4 L MADs
     assert abs(per_add - (8 * 100 + 3 * 55 + 10 * 40)) < 1
+
+
+def test_p521_point_mads():
+    src = open(os.path.join(ROOT, "cap_amd", "csrc", "kernels", "ecdsa.hpp")).read()
+    m = re.search(r"EC_P521_WQ\[\d+\]\s*=\s*\{([^}]*)\}", src)
+    assert [int(x) for x in m.group(1).split(",")] == [20, 18, 16]
+    assert bench.p521_key_w(3, 32 * GiB) == 20
+    assert bench.p521_key_w(1, 0) == 16
+    m = {w: bench.p521_point_mads_per_token(w) for w in (16, 18, 20)}
+    # windows ceil(523 / W): 27 at 20, 30 at 18, 33 at 16 -- three mixed additions per step
+    per_add = (m[18] - m[20]) / 3
+    assert abs((m[16] - m[18]) / 3 - per_add) < 1
+    # a mixed addition: 8 mul + 3 sqr (L = 20) under 10 one-constant reductions + one fold MAD
+    assert abs(per_add - (8 * 400 + 3 * 210 + 10 * 20 + 1)) < 1
