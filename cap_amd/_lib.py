@@ -23,7 +23,7 @@ EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_las
            "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
            "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_table_budget", "jg_keys_wait_tables",
            "jg_keys_table_widths", "jg_debug_fail_alloc", "jg_debug_table_digest",
-           "jg_debug_max_upgrades"]
+           "jg_debug_max_upgrades", "jg_debug_lifetime_check"]
 
 
 class JgKey(ctypes.Structure):
@@ -82,10 +82,20 @@ def lib():
         L.jg_keys_table_widths.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.jg_debug_fail_alloc.argtypes = [vp, ctypes.c_int]
         L.jg_debug_max_upgrades.argtypes = [vp, ctypes.c_int]
+        L.jg_debug_lifetime_check.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                              ctypes.POINTER(ctypes.c_uint64)]
         L.jg_debug_table_digest.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         L.jg_version.restype = ctypes.c_char_p
         _lib = L
     return _lib
+
+
+def lifetime_check(enable=-1):
+    """jg_debug_lifetime_check: 1 / 0 turns the key-memory lifetime check on /
+    off (-1 leaves it); returns (violations, events checked) so far."""
+    bad, chk = ctypes.c_uint64(), ctypes.c_uint64()
+    lib().jg_debug_lifetime_check(int(enable), ctypes.byref(bad), ctypes.byref(chk))
+    return bad.value, chk.value
 
 
 class Key:

@@ -338,6 +338,55 @@ DevBufP dev_alloc(int dev, size_t bytes, std::atomic<int>* fail = nullptr) {
   return b;
 }
 
+// Lifetime check (debugging; CAPJWT_CHECK_LIFETIME=1 or jg_debug_lifetime_check).
+// The rule the runtime relies on: a key generation's device memory (records,
+// blob, comb tables) is released only once every launch that reads it has
+// completed -- pipeline slots drop their key state in finish_slot after the
+// chunk's `done` event, resident batches after a lane synchronize, loads and
+// upgrades synchronise their own streams.  hipFree's implicit device-wide
+// synchronisation would hide a violation, so the check does not rely on it:
+// every stream that launches against a generation records an event into the
+// generation's UseLog, and the generation's destructor (before any of its
+// buffers go to the reaper) queries them all; an event still pending is a
+// violation, logged with the stream's role and counted.
+std::atomic<int> g_lifetime_on{[] {
+  const char* e = std::getenv("CAPJWT_CHECK_LIFETIME");
+  return e && std::atoi(e) != 0 ? 1 : 0;
+}()};
+std::atomic<uint64_t> g_lifetime_bad{0}, g_lifetime_checked{0};
+
+struct UseLog {
+  std::mutex mu;
+  std::vector<std::pair<hipEvent_t, std::string>> ev;
+  UseLog() = default;
+  UseLog(const UseLog&) {}                         // a copied generation starts with no uses
+  UseLog& operator=(const UseLog&) { return *this; }
+  void record(hipStream_t s, const char* role, int c = -1) {
+    if (!g_lifetime_on.load(std::memory_order_relaxed)) return;
+    hipEvent_t e = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(e, s));
+    char buf[128];
+    if (c >= 0) std::snprintf(buf, sizeof buf, "%s of class %d (stream %p)", role, c, (void*)s);
+    else std::snprintf(buf, sizeof buf, "%s (stream %p)", role, (void*)s);
+    std::lock_guard<std::mutex> g(mu);
+    ev.emplace_back(e, buf);
+  }
+  ~UseLog() {
+    for (auto& x : ev) {
+      const hipError_t q = hipEventQuery(x.first);
+      g_lifetime_checked.fetch_add(1, std::memory_order_relaxed);
+      if (q == hipErrorNotReady) {
+        g_lifetime_bad.fetch_add(1, std::memory_order_relaxed);
+        std::fprintf(stderr, "[capjwt] lifetime check: a key generation is released while work on %s has not "
+                             "completed\n", x.second.c_str());
+      }
+      (void)hipGetLastError();
+      (void)hipEventDestroy(x.first);
+    }
+  }
+};
+
 // One device's copy of a key table generation: the DevKey records, the key
 // blob (moduli, R^2, Montgomery coordinates), the class table of k_plan_fill,
 // and the comb tables the records point at.  Immutable once published; a
@@ -347,6 +396,7 @@ struct DevGen {
   std::vector<DevBufP> tabs;      // comb tables the keys' `tab` addresses point into
   std::vector<DevKey> mirror;     // host copy of dkeys (after key prep: validity, tables)
   std::vector<uint8_t> kw;        // per key: comb width of its table (0 = none)
+  mutable UseLog uses;            // lifetime check; last member, so it is checked before the buffers go
   DevKey* keys() const { return dkeys ? dkeys->as<DevKey>() : nullptr; }
   uint32_t* keyblob() const { return blob ? blob->as<uint32_t>() : nullptr; }
   const uint8_t* cls() const { return dcls ? dcls->as<uint8_t>() : nullptr; }
@@ -1155,6 +1205,15 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
   launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s0);
   mark(marks, "scatter");
   HIPCHK(hipGetLastError());
+  if (g_lifetime_on.load(std::memory_order_relaxed)) {
+    for (int c = 1; c < NCLS; ++c) {
+      if (P.ranges[c].end <= P.ranges[c].begin) continue;
+      if (conc) G.uses.record(L->cstream[c], "class stream", c);
+      else if (gf) G.uses.record(gf->cls[c], "group lane", c);
+    }
+    if (gf) G.uses.record(gf->ctrl, "chunk control");
+    G.uses.record(s0, gf ? "join lane" : "lane");
+  }
 }
 
 void collect_times(jg_batch* b) {
@@ -1369,6 +1428,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
     fa.jobs = (JobDev*)S.bufs.jobs.p;
     fa.perm = (int32_t*)S.bufs.perm.p;
     launch_plan_fill(fa, fs);
+    G.uses.record(fs, "plan fill");                // reads the generation's class table
   }
   if (grouped) {
     run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, &gf);
@@ -2278,6 +2338,14 @@ int jg_debug_table_digest(jg_ctx* ctx, int key, uint64_t* digest) {
 int jg_debug_fail_alloc(jg_ctx* ctx, int n) {
   if (!ctx || n < 0) return -1;
   ctx->fail_alloc.store(n);
+  return 0;
+}
+
+int jg_debug_lifetime_check(int enable, uint64_t* violations, uint64_t* checked) {
+  if (enable > 0) g_lifetime_on.store(1);
+  else if (enable == 0) g_lifetime_on.store(0);
+  if (violations) *violations = g_lifetime_bad.load();
+  if (checked) *checked = g_lifetime_checked.load();
   return 0;
 }
 

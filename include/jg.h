@@ -126,6 +126,14 @@ int jg_debug_fail_alloc(jg_ctx* ctx, int n);
  * resumes widening.  Returns 0 or -1. */
 int jg_debug_max_upgrades(jg_ctx* ctx, int n);
 
+/* Debug check of the key-memory lifetime rule (process-wide; also
+ * CAPJWT_CHECK_LIFETIME=1): every stream that launches against a key
+ * generation records an event, and releasing the generation queries them --
+ * one still pending is a violation (logged to stderr).  enable: 1 on, 0 off,
+ * -1 unchanged; *violations / *checked (either may be NULL) receive the
+ * counts so far.  Returns 0. */
+int jg_debug_lifetime_check(int enable, uint64_t* violations, uint64_t* checked);
+
 /* Test hook: a 64-bit digest of key `key`'s current comb table on the first
  * device (0 when it has none) -- tables built at different times or on
  * different paths must agree.  Returns 0, -1 or -2. */

@@ -25,3 +25,13 @@ def golden():
     toks = json.load(open(os.path.join(d, "tokens.json")))
     keys = {k["kid"]: jws.Key.from_fixture(k) for k in keys_raw}
     return {"keys": keys, "keys_raw": keys_raw, "tokens": toks}
+
+
+def pytest_sessionstart(session):
+    """A GPU session (-m gpu) runs with the key-memory lifetime check on
+    (include/jg.h jg_debug_lifetime_check): every key generation released
+    during the suite must find the work of every stream that used it done;
+    tests/test_gpu_zz_lifetime.py (the last GPU module) asserts the count."""
+    if (session.config.getoption("markexpr", "") or "").strip() == "gpu":
+        from cap_amd import _lib
+        _lib.lifetime_check(1)
