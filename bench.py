@@ -171,11 +171,12 @@ def ed25519_point_mads_per_token(wa=24):
     """k_ed_point: 11 comb windows of the base point (W = 24) + ceil(254 / wa)
     of the key (ed25519.hpp ED_WA: W = 24 / 22 / 20 / 18 / 16 by the table
     budget), each a Niels addition of 7 field products (ed25519.hip
-    add_niels); p = 2^255 - 19 is reduced with 2 MADs per row (mp.hpp
-    mont_reduce_25519): a product is L^2 + 2L = 120 MADs.  Plus k = H mod L
-    (one reduction + one product mod L)."""
+    add_niels) in radix 2^25.5 (kernels/fe25519.hpp): 100 partial products
+    and the one MAD that folds the carry out of the top limb (x 19) -- no
+    reduction rows.  Plus k = H mod L (one Montgomery reduction + one product
+    mod L, 28-bit limbs: 220)."""
     L = 10
-    mul = L * L + 2 * L
+    mul = L * L + 1
     adds = 11 * (1 - 2.0 ** -24) + -(-254 // wa) * (1 - 2.0 ** -wa)
     return adds * 7 * mul + 220
 

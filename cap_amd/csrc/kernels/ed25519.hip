@@ -17,6 +17,7 @@
 
 #include "common.hpp"
 #include "ed25519.hpp"
+#include "fe25519.hpp"
 #include "mp.hpp"
 #include "tables.hpp"
 
@@ -41,15 +42,41 @@ __device__ __forceinline__ bool lt_limbs(const uint32_t* a, const uint32_t* b) {
 
 struct EPt { uint32_t X[L], Y[L], Z[L], T[L]; };
 
-// extended + Niels (y+x, y-x, 2dxy) affine -> extended (complete, a = -1)
-__device__ __forceinline__ void add_niels(EPt& P, const uint32_t* ypx, const uint32_t* ymx, const uint32_t* t2d) {
-  uint32_t t[L], A[L], B[L], C[L], D[L], E[L], F[L], G[L], H[L];
-  mp::sub<Fp>(t, P.Y, P.X); mp::mul<Fp>(A, t, ymx);
-  mp::add<Fp>(t, P.Y, P.X); mp::mul<Fp>(B, t, ypx);
-  mp::mul<Fp>(C, P.T, t2d);
-  mp::add<Fp>(D, P.Z, P.Z); mp::norm<Fp>(D);
-  mp::sub<Fp>(E, B, A); mp::sub<Fp>(F, D, C); mp::add<Fp>(G, D, C); mp::add<Fp>(H, B, A);
-  mp::mul<Fp>(P.X, E, F); mp::mul<Fp>(P.Y, G, H); mp::mul<Fp>(P.T, E, H); mp::mul<Fp>(P.Z, F, G);
+// Hot loop (k_ed_point): points and table entries in the radix-2^25.5 form of
+// fe25519.hpp (plain values, no Montgomery factor).  Table building, key
+// decoding and the finish stay in ED25519P's Montgomery form (mp.hpp) and
+// convert at the boundary (entries are stored canonical in radix 2^25.5).
+struct FPt { uint32_t X[fe::L], Y[fe::L], Z[fe::L], T[fe::L]; };
+
+// extended + Niels (y+x, y-x, 2dxy) affine -> extended (complete, a = -1):
+// 7 products.  fe::mul's second operand carries the factor 19 and must be the
+// smaller one: the point side for A, B, C, then E and G (tools/fe25519_bounds.py)
+__device__ __forceinline__ void add_niels(FPt& P, const uint32_t* ypx, const uint32_t* ymx, const uint32_t* t2d) {
+  uint32_t t[fe::L], A[fe::L], B[fe::L], C[fe::L], D[fe::L], E[fe::L], F[fe::L], G[fe::L], H[fe::L];
+  fe::sub(t, P.Y, P.X); fe::mul(A, ymx, t);
+  fe::add(t, P.Y, P.X); fe::mul(B, ypx, t);
+  fe::mul(C, t2d, P.T);
+  fe::add(D, P.Z, P.Z);
+  fe::sub(E, B, A); fe::sub(F, D, C); fe::add(G, D, C); fe::add(H, B, A);
+  fe::mul(P.X, F, E); fe::mul(P.Y, H, G); fe::mul(P.T, H, E); fe::mul(P.Z, F, G);
+}
+
+// radix-2^25.5 limbs (limbs < 2^31) -> ED25519P Montgomery form
+__device__ void fe_to_mont(uint32_t* m, const uint32_t* f) {
+  uint32_t c[fe::L], w[8], pl[L];
+  fe::copy(c, f);
+  fe::canon(c);
+  fe::to_words(w, c);
+  mp::words_to_limbs<L, 8>(pl, w);
+  mp::to_mont<Fp>(m, pl);
+}
+
+// ED25519P Montgomery form (normalized) -> canonical radix-2^25.5 limbs
+__device__ void mont_to_fe(uint32_t* f, const uint32_t* m) {
+  uint32_t pl[L], w[8];
+  mp::from_mont<Fp>(pl, m);
+  mp::limbs_to_words<L, 8>(w, pl);
+  fe::from_words(f, w);
 }
 
 // extended + extended (complete)
@@ -65,7 +92,7 @@ __device__ void add_full(EPt& R, const EPt& P, const EPt& Q) {
 }
 
 template <int NE>
-__device__ __forceinline__ void add_window(EPt& P, const uint32_t* __restrict__ tab, int w, int d) {
+__device__ __forceinline__ void add_window(FPt& P, const uint32_t* __restrict__ tab, int w, int d) {
   if (d == 0) return;
 #ifdef JG_AB_TINY_TABLE
   const int ad = (((d < 0 ? -d : d) - 1) & 255) + 1;     // A/B only: every gather within 256 entries (wrong verdicts)
@@ -73,17 +100,17 @@ __device__ __forceinline__ void add_window(EPt& P, const uint32_t* __restrict__ 
   const int ad = d < 0 ? -d : d;
 #endif
   const uint32_t* ent = tab + ((int64_t)w * NE + (ad - 1)) * ED_STRIDE;
-  uint32_t ypx[L], ymx[L], t2d[L];
+  uint32_t ypx[fe::L], ymx[fe::L], t2d[fe::L];
 #pragma unroll
-  for (int j = 0; j < L; ++j) { ypx[j] = ent[j]; ymx[j] = ent[L + j]; t2d[j] = ent[2 * L + j]; }
+  for (int j = 0; j < fe::L; ++j) { ypx[j] = ent[j]; ymx[j] = ent[fe::L + j]; t2d[j] = ent[2 * fe::L + j]; }
   // -(x, y) = (-x, y): swap y+x / y-x and negate 2dxy -- selected per lane, so
   // the wave runs ONE addition (a branch on the digit's sign made lanes of
   // both signs execute both inlined copies of add_niels)
   const bool neg = d < 0;
-  uint32_t a1[L], a2[L], nt[L];
-  mp::neg<Fp>(nt, t2d);
+  uint32_t a1[fe::L], a2[fe::L], nt[fe::L];
+  fe::neg(nt, t2d);
 #pragma unroll
-  for (int j = 0; j < L; ++j) {
+  for (int j = 0; j < fe::L; ++j) {
     a1[j] = neg ? ymx[j] : ypx[j];
     a2[j] = neg ? ypx[j] : ymx[j];
     t2d[j] = neg ? nt[j] : t2d[j];
@@ -148,9 +175,8 @@ __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
   int d1[NB], d2[NA];
   recode<ed_comb_w(true), NB>(d1, s);
   recode<WA, NA>(d2, k);
-  EPt P;
-#pragma unroll
-  for (int j = 0; j < L; ++j) { P.X[j] = 0; P.T[j] = 0; P.Y[j] = Fp::ONE[j]; P.Z[j] = Fp::ONE[j]; }
+  FPt P;                                      // the neutral element (0, 1, 1, 0)
+  fe::set_small(P.X, 0u); fe::set_small(P.Y, 1u); fe::set_small(P.Z, 1u); fe::set_small(P.T, 0u);
   const uint32_t* __restrict__ atab = key_table(K);
 #pragma unroll 1
   for (int w = 0; w < NW; ++w) {
@@ -163,7 +189,7 @@ __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
     add_window<(1 << (WA - 1))>(P, atab, w, e2);
   }
 #pragma unroll
-  for (int j = 0; j < L; ++j) {
+  for (int j = 0; j < fe::L; ++j) {                // radix-2^25.5 limbs (k_ed_finish converts)
     a.xyz[(int64_t)j * np + p] = P.X[j];
     a.xyz[(int64_t)(L + j) * np + p] = P.Y[j];
     a.xyz[(int64_t)(2 * L + j) * np + p] = P.Z[j];
@@ -188,8 +214,10 @@ __global__ void __launch_bounds__(64) k_ed_finish(EdArgs a, int B) {
   auto live = [&](int64_t p) { return job_live(a.jobs[p]) && a.status[p] == ST_OK; };
   auto load_z = [&](int64_t p, uint32_t* Z) {
     if (live(p)) {
+      uint32_t f[fe::L];
 #pragma unroll
-      for (int j = 0; j < L; ++j) Z[j] = a.xyz[(int64_t)(2 * L + j) * np + p];
+      for (int j = 0; j < fe::L; ++j) f[j] = a.xyz[(int64_t)(2 * L + j) * np + p];
+      fe_to_mont(Z, f);
     } else {
       mp::set_const<Fp>(Z, Fp::ONE);
     }
@@ -223,12 +251,14 @@ __global__ void __launch_bounds__(64) k_ed_finish(EdArgs a, int B) {
     mp::mul<Fp>(inv, inv, Z);
     if (!job_live(a.jobs[p])) continue;
     if (a.status[p] != ST_OK) { a.verdict_pad[p] = 0; continue; }
-    uint32_t X[L], Y[L], x[L], y[L], tt[L];
+    uint32_t X[L], Y[L], x[L], y[L], tt[L], fx[fe::L], fy[fe::L];
 #pragma unroll
-    for (int k = 0; k < L; ++k) {
-      X[k] = a.xyz[(int64_t)k * np + p];
-      Y[k] = a.xyz[(int64_t)(L + k) * np + p];
+    for (int k = 0; k < fe::L; ++k) {
+      fx[k] = a.xyz[(int64_t)k * np + p];
+      fy[k] = a.xyz[(int64_t)(L + k) * np + p];
     }
+    fe_to_mont(X, fx);
+    fe_to_mont(Y, fy);
     mp::mul<Fp>(tt, X, zi); mp::from_mont<Fp>(x, tt);
     mp::mul<Fp>(tt, Y, zi); mp::from_mont<Fp>(y, tt);
     uint32_t enc[8];
@@ -253,8 +283,10 @@ __device__ void niels_entry(uint32_t* out, const EPt& P) {
   mp::mul<Fp>(t, x, y);
   mp::set_const<Fp>(d2, ED25519C::D2_M);
   mp::mul<Fp>(t2d, t, d2); mp::canon<Fp>(t2d);
-#pragma unroll
-  for (int j = 0; j < L; ++j) { out[j] = ypx[j]; out[L + j] = ymx[j]; out[2 * L + j] = t2d[j]; }
+  // stored canonical in k_ed_point's radix-2^25.5 form
+  mont_to_fe(out, ypx);
+  mont_to_fe(out + fe::L, ymx);
+  mont_to_fe(out + 2 * fe::L, t2d);
 }
 
 // canonical a -> a / 2 mod p (canonical)
@@ -268,11 +300,13 @@ __device__ void half_mod(uint32_t* r, const uint32_t* a) {
   for (int j = 0; j < L; ++j) r[j] = (v[j] >> 1) | (j + 1 < L ? (v[j + 1] & 1u) << (MP_W - 1) : 0u);
 }
 
-// affine (x, y) of a Niels entry (y+x, y-x, 2dxy)
+// affine (x, y) of a Niels entry (y+x, y-x, 2dxy; stored in radix 2^25.5)
 __device__ void niels_affine(uint32_t* x, uint32_t* y, const uint32_t* ent) {
-  uint32_t t[L];
-  mp::sub<Fp>(t, ent, ent + L); mp::canon<Fp>(t); half_mod(x, t);
-  mp::add<Fp>(t, ent, ent + L); mp::canon<Fp>(t); half_mod(y, t);
+  uint32_t t[L], ypx[L], ymx[L];
+  fe_to_mont(ypx, ent);
+  fe_to_mont(ymx, ent + fe::L);
+  mp::sub<Fp>(t, ypx, ymx); mp::canon<Fp>(t); half_mod(x, t);
+  mp::add<Fp>(t, ypx, ymx); mp::canon<Fp>(t); half_mod(y, t);
 }
 
 // window base 2^(W w) * P as the Niels entry d = 1 of window w

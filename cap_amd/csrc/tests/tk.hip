@@ -7,6 +7,7 @@
 #include <cstdint>
 
 #include "../kernels/mp.hpp"
+#include "../kernels/fe25519.hpp"
 #include "../kernels/ecdsa_impl.hpp"   // EC device functions (anonymous namespace) for point-level tests
 
 #include <type_traits>
@@ -149,4 +150,35 @@ extern "C" int tk_ec(int curve, int what, const void* in, size_t in_bytes, uint3
     case 3: return run_ec<CurveP521>(what, in, in_bytes, out, out_bytes, n);
     default: return -1;
   }
+}
+
+// ---------------------------------------------------------------- radix-2^25.5 GF(2^255 - 19)
+namespace {
+__global__ void k_fe(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t x[fe::L], y[fe::L], r[fe::L];
+  for (int j = 0; j < fe::L; ++j) { x[j] = a[i * fe::L + j]; y[j] = b[i * fe::L + j]; }
+  if (op == 0) {
+    fe::mul(r, x, y);
+  } else {
+    fe::copy(r, x);
+    fe::canon(r);
+  }
+  for (int j = 0; j < fe::L; ++j) out[i * fe::L + j] = r[j];
+}
+}  // namespace
+
+// op 0: fe::mul(a, b), 1: fe::canon(a); arrays of n x 10 limbs (lane-major)
+extern "C" int tk_fe25519(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, int n) {
+  const size_t bytes = sizeof(uint32_t) * fe::L * (size_t)n;
+  uint32_t *da, *db, *dout;
+  if (hipMalloc(&da, bytes) || hipMalloc(&db, bytes) || hipMalloc(&dout, bytes)) return -1;
+  (void)hipMemcpy(da, a, bytes, hipMemcpyHostToDevice);
+  (void)hipMemcpy(db, b, bytes, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_fe, dim3((n + 63) / 64), dim3(64), 0, 0, op, da, db, dout, n);
+  const hipError_t e = hipDeviceSynchronize();
+  (void)hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+  (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout);
+  return e == hipSuccess ? 0 : -2;
 }
