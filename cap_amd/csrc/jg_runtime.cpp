@@ -88,6 +88,20 @@ double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 
+// CAPJWT_LOAD_TRACE=1: per-phase wall times of jg_keys_load on stderr
+bool load_trace() {
+  static const bool on = std::getenv("CAPJWT_LOAD_TRACE") != nullptr;
+  return on;
+}
+struct PhaseClock {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(const char* what) {
+    if (!load_trace()) return;
+    std::fprintf(stderr, "[capjwt load] %-28s %8.2f ms\n", what, ms_since(t));
+    t = std::chrono::steady_clock::now();
+  }
+};
+
 size_t chunk_jobs() {
   static const size_t n = [] {
     if (const char* e = std::getenv("CAPJWT_CHUNK")) {
@@ -1809,12 +1823,14 @@ void build_tables(const std::map<std::pair<int, int>, std::vector<int32_t>>& gro
 // failure; the device state and the published key table are then untouched.
 std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S, bool narrow_first) {
   HIPCHK(hipSetDevice(d->id));
+  PhaseClock pc;
   const hipStream_t s = d->kstream;
   const size_t nk = S.dk.size();
   auto g = std::make_shared<DevGen>();
   g->mirror = S.dk;
   g->kw.assign(nk, 0);
   ensure_tables(d, S);
+  pc.lap("fixed-base tables");
   g->dkeys = dev_alloc(d->id, sizeof(DevKey) * std::max<size_t>(nk, 1), &ctx->fail_alloc);
   g->blob = dev_alloc(d->id, sizeof(uint32_t) * std::max<size_t>(S.blob.size(), 4), &ctx->fail_alloc);
   // key prep index lists: p256 | p384 | p521 | ed
@@ -1840,6 +1856,7 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   HIPCHK(hipGetLastError());
   if (nk) HIPCHK(hipMemcpyAsync(g->mirror.data(), dk, sizeof(DevKey) * nk, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  pc.lap("records + key prep");
 
   // comb tables of the keys that prepped valid
   struct Req { int cls, w; DevBufP buf; std::string id; };
@@ -1896,10 +1913,12 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   }
   std::map<std::pair<int, int>, std::vector<int32_t>> groups;
   std::map<std::string, int32_t> first;          // one build per distinct (id, width)
+  pc.lap("table lookup + free HBM");
   for (auto& f : fresh) {
     f.second.buf = dev_alloc(d->id, table_bytes(f.second.cls, f.second.w), &ctx->fail_alloc);
     poison_table(*f.second.buf, s);
   }
+  pc.lap("new table allocations");
   for (const auto& u : use) {
     const Req& r = fresh.at(u.second);
     const size_t i = u.first;
@@ -1911,6 +1930,7 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   }
   if (nk) HIPCHK(hipMemcpyAsync(dk, g->mirror.data(), sizeof(DevKey) * nk, hipMemcpyHostToDevice, s));
   build_tables(groups, dk, blob, di, s);          // synchronises s
+  pc.lap("new comb tables (kernels)");
   {
     std::lock_guard<std::mutex> tg(d->tmu);
     for (auto it = d->tcache.begin(); it != d->tcache.end();)
@@ -2254,6 +2274,7 @@ int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys) {
   if (nkeys > 65535) { ctx->set_err("at most 65535 keys"); return -1; }
   try {
     std::lock_guard<std::mutex> lg(ctx->load_mu);
+    PhaseClock pc;
     std::string content = key_content(keys, nkeys, ctx->table_budget.load());
     KeyStateP cur = ctx->state();
     if (cur && cur->epoch > 0 && cur->content == content) return 0;   // unchanged key set: no device work
@@ -2261,14 +2282,17 @@ int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys) {
     auto ns = std::make_shared<KeyState>();
     std::string warn;
     build_keys(keys, nkeys, ctx->table_budget.load(), S, ns->keys, &warn);   // throws before any device work
+    pc.lap("host key staging");
     // stage on every device beside running work; any failure throws and
     // leaves the published table (and what verifies against it) untouched
     std::vector<std::shared_ptr<DevGen>> gens;
     for (auto& d : ctx->devs) gens.push_back(stage_device(ctx, d.get(), S, !tables_sync()));
+    pc.lap("device staging (all devices)");
     // device-side validity (on-curve, Ed25519 decoding) back into the host view
     for (size_t i = 0; i < ns->keys.size(); ++i) ns->keys[i].valid = ns->keys[i].valid && gens[0]->mirror[i].valid;
     rebuild_class_tables(*ns);
     for (size_t i = 0; i < gens.size(); ++i) upload_cls(ctx, ctx->devs[i].get(), *gens[i], ns->cls_tab);
+    pc.lap("class tables");
     ns->tab_id = std::move(S.tab_id);
     ns->want_w = std::move(S.want_w);
     ns->epoch = (cur ? cur->epoch : 0) + 1;
@@ -2276,6 +2300,7 @@ int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys) {
     for (auto& g : gens) ns->dev.push_back(std::move(g));
     const bool up = needs_upgrade(*ns);
     ctx->publish(std::move(ns));
+    pc.lap("publish (old state released)");
     if (up) {
       std::lock_guard<std::mutex> g(ctx->up_mu);
       ctx->up_pending = true;
