@@ -27,7 +27,13 @@ namespace {
 #endif
 
 constexpr int WIN = 32;         // dwords per window step (128 bytes of string)
-constexpr int SLOT = 36;        // LDS words per token slot (33 used; stride 36 keeps lanes' reads on distinct banks)
+// LDS words per token slot (33 used).  JG_PREP_SLOT A/B: the slot stride sets
+// the ds_read bank pattern of the per-lane slot reads and the LDS per wave
+// (SLOT 36: 11.0 KB per wave, 14 waves per CU)
+#ifndef JG_PREP_SLOT
+#define JG_PREP_SLOT 36
+#endif
+constexpr int SLOT = JG_PREP_SLOT;
 
 __device__ __forceinline__ int b64val(uint32_t c) {
   if (c - 'A' < 26u) return (int)(c - 'A');

@@ -1,0 +1,9 @@
+# Round-4 A/Bs on one box (run via gpurun from the repo root):
+#   prep LDS slot stride (ES256 line), Ed25519 radix-2^25.5 vs round-3 Montgomery point loop (config lines)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+echo "[prep slot] $(date +%T)"
+timeout -k 10 400 python3 tools/ab_run.py gpurun_out/r04_prep_slot_ab.json 'slot36:' 'slot34:CAPJWT_LIB=cap_amd/ab_slot34.so' 'slot33:CAPJWT_LIB=cap_amd/ab_slot33.so' 'slot36b:' || exit 1
+echo "[ed radix] $(date +%T)"
+timeout -k 10 600 python3 tools/ab_run.py gpurun_out/r04_ed_radix_ab.json 'radix255:' 'mont_r03:CAPJWT_LIB=cap_amd/ab_edr03.so' -- --configs-only --steps 6 --warmup 2 --no-ab --no-refresh || exit 1
