@@ -182,6 +182,13 @@ __device__ __forceinline__ void store_digit_rows(const EcArgs& a, int64_t p, con
 //   inv = c_{B-1}^-1
 //   pass 2 (j descending): w_j = inv * c_{j-1}, inv *= s_j;
 //           u1 = e w_j, u2 = r w_j (mod n), signed W-bit digits
+// The inversion is shared by the EC_SCALAR_WPB waves of a block
+// (mp::block_inv); JG_EC_SCALAR_WPB = 1 is the round-3 kernel (one inversion
+// per wave).
+#ifndef JG_EC_SCALAR_WPB
+#define JG_EC_SCALAR_WPB 4
+#endif
+constexpr int EC_SCALAR_WPB = JG_EC_SCALAR_WPB;
 template <class CV>
 // JG_EC_SCALAR_ATTR: per translation unit.  ecdsa_p521.hip caps the kernel at
 // two waves per SIMD: left alone the compiler gives the P-521 instantiation
@@ -192,18 +199,18 @@ template <class CV>
 #ifndef JG_EC_SCALAR_ATTR
 #define JG_EC_SCALAR_ATTR
 #endif
-__global__ void __launch_bounds__(64) JG_EC_SCALAR_ATTR k_ec_scalar_batch(EcArgs a, int B) {
+__global__ void __launch_bounds__(64 * EC_SCALAR_WPB) JG_EC_SCALAR_ATTR k_ec_scalar_batch(EcArgs a, int B) {
   using Fn = typename CV::Fn;
   constexpr int L = Fn::L;
   const int64_t np = a.npad;
   const int64_t n = a.end - a.begin;
   const int64_t S = (n + B - 1) / B;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= S) return;
+  if (EC_SCALAR_WPB == 1 && i >= S) return;        // (blocks of several waves keep every thread for the barriers)
   uint32_t acc[L];
   mp::set_const<Fn>(acc, Fn::ONE);
   int nb = 0;
-  for (int j = 0; j < B; ++j) {
+  for (int j = 0; j < B && i < S; ++j) {
     const int64_t p = a.begin + i + (int64_t)j * S;
     if (p >= a.end) break;
     uint32_t r[L], s[L], e[L], sm[L];
@@ -219,7 +226,7 @@ __global__ void __launch_bounds__(64) JG_EC_SCALAR_ATTR k_ec_scalar_batch(EcArgs
     ++nb;
   }
   uint32_t inv[L];
-  mp::inv<Fn>(inv, acc);
+  mp::block_inv<Fn, EC_SCALAR_WPB>(inv, acc);
   for (int j = nb - 1; j >= 0; --j) {
     const int64_t p = a.begin + i + (int64_t)j * S;
     uint32_t cprev[L], sm[L], w[L];
@@ -789,7 +796,8 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   }();
   int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * wpc * WAVE)));
   const int64_t S = (n + B - 1) / B;
-  hipLaunchKernelGGL(k_ec_scalar_batch<CV>, dim3((unsigned)((S + WAVE - 1) / WAVE)), b, 0, s, a, B);
+  constexpr int TPB = WAVE * EC_SCALAR_WPB;
+  hipLaunchKernelGGL(k_ec_scalar_batch<CV>, dim3((unsigned)((S + TPB - 1) / TPB)), dim3(TPB), 0, s, a, B);
   mk("scalar");
   hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
   mk("point");

@@ -204,12 +204,17 @@ __global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
 //           canonical encoding, byte compare with R.
 // Z != 0 for every output of the complete addition law; padding and rejected
 // tokens contribute Z = 1.
-__global__ void __launch_bounds__(64) k_ed_finish(EdArgs a, int B) {
+// Waves per block sharing one inversion (mp::block_inv, as k_ec_scalar_batch)
+#ifndef JG_ED_FINISH_WPB
+#define JG_ED_FINISH_WPB 4
+#endif
+constexpr int ED_FINISH_WPB = JG_ED_FINISH_WPB;
+__global__ void __launch_bounds__(64 * ED_FINISH_WPB) k_ed_finish(EdArgs a, int B) {
   const int64_t np = a.npad;
   const int64_t n = a.end - a.begin;
   const int64_t S = (n + B - 1) / B;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= S) return;
+  if (ED_FINISH_WPB == 1 && i >= S) return;       // (blocks of several waves keep every thread for the barriers)
   uint32_t* pre = a.xyz + (int64_t)3 * L * np;
   auto live = [&](int64_t p) { return job_live(a.jobs[p]) && a.status[p] == ST_OK; };
   auto load_z = [&](int64_t p, uint32_t* Z) {
@@ -225,7 +230,7 @@ __global__ void __launch_bounds__(64) k_ed_finish(EdArgs a, int B) {
   uint32_t acc[L];
   mp::set_const<Fp>(acc, Fp::ONE);
   int nb = 0;
-  for (int j = 0; j < B; ++j) {
+  for (int j = 0; j < B && i < S; ++j) {
     const int64_t p = a.begin + i + (int64_t)j * S;
     if (p >= a.end) break;
     uint32_t Z[L];
@@ -236,7 +241,7 @@ __global__ void __launch_bounds__(64) k_ed_finish(EdArgs a, int B) {
     ++nb;
   }
   uint32_t inv[L];
-  mp::inv<Fp>(inv, acc);
+  mp::block_inv<Fp, ED_FINISH_WPB>(inv, acc);
   for (int j = nb - 1; j >= 0; --j) {
     const int64_t p = a.begin + i + (int64_t)j * S;
     uint32_t cprev[L], Z[L], zi[L];
@@ -445,7 +450,8 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t n = a.end - a.begin;
   const int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * 8 * WAVE)));
   const int64_t S = (n + B - 1) / B;
-  hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)((S + WAVE - 1) / WAVE)), b, 0, s, a, B);
+  constexpr int TPB = WAVE * ED_FINISH_WPB;
+  hipLaunchKernelGGL(k_ed_finish, dim3((unsigned)((S + TPB - 1) / TPB)), dim3(TPB), 0, s, a, B);
   mk("finish");
 }
 

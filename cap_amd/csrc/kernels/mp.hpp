@@ -677,6 +677,61 @@ MPD void inv(uint32_t* r, const uint32_t* x) {
   to_mont<F>(r, a);        // a^-1 R
 }
 
+// Batched inversion shared by the WPB waves of a block (Montgomery's trick
+// through LDS).  A wave computes one inversion however many lanes use it, so
+// per-thread batching (k_ec_scalar_batch, k_ed_finish: B tokens per thread)
+// pays one inversion per wave; here the block's waves hand their per-lane
+// products to wave 0, which inverts ONE product per lane for all WPB waves
+// (WPB - 1 products forward, 2 (WPB - 1) back) while the other waves wait at
+// the barrier.  In: x = aR (Montgomery, nonzero); out: a^-1 R.  Every thread
+// of the block must call it (two __syncthreads).
+template <class F, int WPB>
+MPD void block_inv(uint32_t* r, const uint32_t* x) {
+  constexpr int L = F::L;
+  __shared__ uint32_t sh_x[WPB * L * 64];           // per wave: its lanes' x, then their inverses
+  __shared__ uint32_t sh_p[(WPB > 1 ? WPB - 1 : 1) * L * 64];   // prefix products x_0 ... x_j
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if constexpr (WPB == 1) {
+    inv<F>(r, x);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < L; ++k) sh_x[(w * L + k) * 64 + lane] = x[k];
+  __syncthreads();
+  if (w == 0) {                                     // wave-uniform
+    uint32_t acc[L], t[L];
+    copy<F>(acc, x);
+#pragma unroll 1
+    for (int j = 1; j < WPB; ++j) {
+#pragma unroll
+      for (int k = 0; k < L; ++k) sh_p[((j - 1) * L + k) * 64 + lane] = acc[k];
+#pragma unroll
+      for (int k = 0; k < L; ++k) t[k] = sh_x[(j * L + k) * 64 + lane];
+      mul<F>(acc, acc, t);
+    }
+    uint32_t iv[L];
+    inv<F>(iv, acc);                                // (x_0 ... x_{WPB-1})^-1
+#pragma unroll 1
+    for (int j = WPB - 1; j >= 1; --j) {
+      uint32_t xj[L], pj[L], out[L];
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+        xj[k] = sh_x[(j * L + k) * 64 + lane];
+        pj[k] = sh_p[((j - 1) * L + k) * 64 + lane];
+      }
+      mul<F>(out, iv, pj);                          // x_j^-1
+      mul<F>(iv, iv, xj);                           // (x_0 ... x_{j-1})^-1
+#pragma unroll
+      for (int k = 0; k < L; ++k) sh_x[(j * L + k) * 64 + lane] = out[k];
+    }
+#pragma unroll
+    for (int k = 0; k < L; ++k) sh_x[k * 64 + lane] = iv[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < L; ++k) r[k] = sh_x[(w * L + k) * 64 + lane];
+}
+
 // canonical equality of two normalized values < 2m (reduces both)
 template <class F>
 MPD bool eq_mod(const uint32_t* a, const uint32_t* b) {

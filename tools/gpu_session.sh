@@ -1,22 +1,27 @@
 # One GPU call: named test files first, the whole -m gpu suite, the default
 # bench, then optional probes (run via gpurun from the repo root):
 #   bash tools/gpu_session.sh "<first test files>" [probe ...]
-# probes: e2e_ab (tools/e2e_ab.sh), keyload (tools/keyload_trace.py)
+# probes: e2e_ab (tools/e2e_ab.sh), keyload (tools/keyload_trace.py),
+#   ab (tools/ab_r04.sh), pmc_int (tools/gpu_pmc_int.sh); "-" as the first
+#   argument skips the tests and the bench
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 FIRST=$1; shift
+if [ "$FIRST" = "-" ]; then SKIP=1; FIRST=""; fi
 if [ -n "$FIRST" ]; then
   timeout -k 10 400 python -u -m pytest $FIRST -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_first.log 2>&1 || { echo PYTEST_FIRST_FAIL; tail -40 gpurun_out/pytest_first.log; exit 1; }
   tail -1 gpurun_out/pytest_first.log
 fi
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pytest.log; exit 1; }
+[ -z "$SKIP" ] && { timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pytest.log; exit 1; }
 grep -E "passed|failed" gpurun_out/pytest.log | tail -2
 timeout -k 10 500 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH_FAIL; tail -30 gpurun_out/bench.err; exit 1; }
-python3 tools/bench_summary.py gpurun_out/bench.json || true
+python3 tools/bench_summary.py gpurun_out/bench.json || true; }
 for p in "$@"; do
   case $p in
     e2e_ab) bash tools/e2e_ab.sh || exit 1 ;;
+    ab) bash tools/ab_r04.sh || exit 1 ;;
+    pmc_int) bash tools/gpu_pmc_int.sh int || exit 1 ;;
     keyload) timeout -k 10 300 python -u tools/keyload_trace.py > gpurun_out/keyload.log 2>&1 || { echo KEYLOAD_FAIL; tail -20 gpurun_out/keyload.log; exit 1; }; cat gpurun_out/keyload.log ;;
   esac
 done
