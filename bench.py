@@ -434,6 +434,11 @@ def measure_e2e(pool, kids_jwk, total, threads):
     reps = (total + len(pool) - 1) // len(pool)
     blob = b"\n".join((pool * reps)[:total])
     v.ValidateBlob(b"\n".join(pool[:4096]), e)          # warm: JWKS fetch + key staging
+    # steady state: the key set's comb tables widened in the background after
+    # the first fetch (narrow tables first, jg_runtime.cpp upgrade_one); timed
+    # passes that overlap those ~1 s of table builds measure the load, not the
+    # validation rate (round 3's e2e line did)
+    ks.WaitTables()
     best, acc = float("inf"), 0
     for _ in range(2):
         t0 = time.perf_counter()

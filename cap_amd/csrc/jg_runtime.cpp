@@ -438,7 +438,7 @@ using KeyStateP = std::shared_ptr<const KeyState>;
 // Fixed-base tables of the curve generators / Ed25519 base point depend only
 // on (device, curve): every jg_ctx of the process shares one copy per device,
 // built on first use and kept for the life of the process (they are constants
-// of the curves: ~31 GB per device with all four, the P-256 one 26.8 GB and
+// of the curves: ~31 GB per device with all four, the P-256 one 21.5 GB and
 // ~1.1 s to build -- a process that opens and closes contexts must not pay
 // that again).  Deliberately never freed: the cache outlives static
 // destruction, and the driver reclaims device memory at process exit.
@@ -1818,7 +1818,7 @@ void build_tables(const std::map<std::pair<int, int>, std::vector<int32_t>>& gro
 // same key content and width when this device already has one (a JWKS
 // refresh), else a new one.  With `narrow_first` a key that has no table at
 // its budgeted width gets the widest table it already has, or a new table at
-// the narrowest width (P-256: 545 MB, ~0.1 s), so it verifies at once; the
+// the narrowest width (P-256: 436 MB, ~0.1 s), so it verifies at once; the
 // upgrader builds the wide table later (jg_keys_wait_tables).  Throws on any
 // failure; the device state and the published key table are then untouched.
 std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S, bool narrow_first) {

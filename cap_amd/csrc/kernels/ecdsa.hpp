@@ -52,7 +52,7 @@ constexpr int ec_order_bits(int cls) { return cls == jgk::CLS_P256 ? 256 : cls =
 // generator's table is built once per engine and shared by every key, so it
 // gets the wider window (gen = true); per-key tables stay narrower so a JWKS of
 // hundreds of keys still fits:
-//   P-256: G W=26 (10 windows, 26.8 GB), keys W=20 (13 windows, 545 MB each):
+//   P-256: G W=26 (10 windows, 21.5 GB packed), keys W=20 (13 windows, 436 MB each):
 //          22 additions per token (23 with G W=24, 25 with W=20/20, ~32 with 16/16)
 //   P-384: G W=20 (20 windows, 1.3 GB), keys W=16 (25 windows, 105 MB): 44 (65 at 12/12)
 //   P-521: G W=20 (27 windows, 2.3 GB), keys W=16 (33 windows, 173 MB): 59 (87 at 12/12)
@@ -88,9 +88,9 @@ constexpr int64_t ec_table_words_w(int cls, int w) {
 }
 constexpr int64_t ec_table_words(int cls, bool gen) { return ec_table_words_w(cls, ec_comb_w(cls, gen)); }
 // Key-table width tiers (HBM for fewer additions, as the generators' wide
-// windows do), widest first.  P-256: W = 26 (10 windows, 26.8 GB per key: 20
-// additions per token with the W = 26 generator), 24 (11 windows, 7.4 GB), 22
-// (12, 2.0 GB), 20 (13, 545 MB); P-384: 24 (17 windows, 18.3 GB), 20 (20
+// windows do), widest first.  P-256 (64-B packed entries): W = 26 (10 windows,
+// 21.5 GB per key: 20 additions per token with the W = 26 generator), 24 (11
+// windows, 5.9 GB), 22 (12, 1.6 GB), 20 (13, 436 MB); P-384: 24 (17 windows, 18.3 GB), 20 (20
 // windows, 1.34 GB), 18 (22, 369 MB), 16 (25, 105 MB); P-521: 20 (27, 2.26 GB),
 // 18 (30, 629 MB), 16 (33, 173 MB).  The runtime picks one width per curve
 // from the context's table budget, a single total over every curve's key

@@ -96,7 +96,7 @@ void jg_destroy(jg_ctx* ctx);
  *    drain): work submitted before the call finishes against the old table,
  *    work submitted after it returns runs against the new one.  A key that was
  *    already loaded keeps its comb table (shared by content, no copy); a new
- *    EC / Ed25519 key gets a narrow table first (P-256 W = 20: 545 MB, about
+ *    EC / Ed25519 key gets a narrow table first (P-256 W = 20: 436 MB, about
  *    0.1 s) so it verifies as soon as this returns, and its budgeted wide table
  *    is built in the background and swapped in when complete
  *    (jg_keys_wait_tables).  CAPJWT_TABLES_SYNC=1 builds full width here.
@@ -176,13 +176,16 @@ int jg_set_chunk(jg_ctx* ctx, size_t jobs);
 /* HBM (bytes per device, one total over all curves) the context may spend on
  * the comb tables of its EC and Ed25519 keys (default 32 GiB, or
  * CAPJWT_TABLE_BUDGET_GB).  The next jg_keys_load first gives every key its
- * curve's narrowest table (always allowed: P-256 W = 20, 545 MB; P-384 16,
+ * curve's narrowest table (always allowed: P-256 W = 20, 436 MB; P-384 16,
  * 105 MB; P-521 16, 173 MB; Ed25519 16, 67 MB), then widens P-256, P-384,
  * Ed25519 and P-521 in that order, each curve to the widest width whose tables
- * for all of its keys still fit what is left: P-256 W = 26 (26.8 GB per key,
- * 20 point additions per token), 24 (7.4 GB, 21) or 22 (2.0 GB); P-384 W = 24
- * (18.3 GB), 20 (1.34 GB) or 18; Ed25519 20 (872 MB) or 18; P-521 20 (2.26 GB)
- * or 18 -- HBM traded for fewer additions, as the shared generator tables do.
+ * for all of its keys still fit what is left: P-256 W = 26 (21.5 GB per key,
+ * 20 point additions per token), 24 (5.9 GB, 21) or 22 (1.6 GB); P-384 W = 24
+ * (18.3 GB), 20 (1.34 GB) or 18 (369 MB); Ed25519 24 (11.8 GB), 22 (3.2 GB),
+ * 20 (872 MB) or 18 (252 MB); P-521 20 (2.26 GB) or 18 (629 MB: 30 windows)
+ * -- HBM traded for fewer additions, as the shared generator tables do.  At
+ * the default 32 GiB a lone P-256 key gets W = 26, 2-5 keys 24, 6-21 keys 22;
+ * bench.py key_widths mirrors the rule (tests/test_bench_contract.py).
  * New tables are also sized against free HBM: a load narrows them rather than
  * fail.  Besides the budget, each device holds the generator / base-point
  * tables (about 31 GB with all four curves) for the life of the process
