@@ -454,6 +454,50 @@ def measure_e2e(pool, kids_jwk, total, threads):
                     "on host_threads cores + one jg_verify_batch (H2D included); not the headline value"}
 
 
+E2E_KIDS = ["p256-a", "p256-b", "p256-c", "p256-d"]
+
+
+def e2e_child_main(tokfile, total):
+    """--e2e-child: measure_e2e over the tokens in `tokfile` (newline-separated)
+    in this fresh process, CAPJWT_TRACE phase times of the best pass included;
+    one JSON line on stdout."""
+    os.environ["CAPJWT_TRACE"] = "1"
+    pool = open(tokfile, "rb").read().split(b"\n")
+    jwk = [{"kty": "EC", "kid": f"kid-{i:02d}", "crv": "P-256", **xy} for i, xy in enumerate(p256_jwk_xy(E2E_KIDS))]
+    cpu = cpu_info()
+    print(json.dumps(measure_e2e(pool, jwk, total, cpu["cores_used"])))
+
+
+def measure_e2e_fresh(pool, total):
+    """measure_e2e in a child process (bench.py --e2e-child), so the line
+    measures Validator.ValidateBatch as a fresh service process runs it and
+    not this bench process's accumulated state; the child's CAPJWT_TRACE
+    phase times of its last pass ride along."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="capjwt_e2e_", suffix=".txt")
+    try:
+        with os.fdopen(fd, "wb") as f:
+            f.write(b"\n".join(pool))
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--e2e-child", path, "--tokens", str(total)],
+                           capture_output=True, text=True, timeout=600)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        raise RuntimeError(f"e2e child failed: {r.stderr[-2000:]}")
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    phases = {}
+    for line in r.stderr.splitlines():          # the last pass's phases win
+        if line.startswith("[capjwt] ") and line.rstrip().endswith("ms"):
+            parts = line[len("[capjwt] "):].rsplit(None, 2)
+            try:
+                phases[parts[0].strip()] = float(parts[1])
+            except (ValueError, IndexError):
+                pass
+    out["phases_ms_last_pass"] = phases
+    out["process"] = "fresh child process (bench.py --e2e-child)"
+    return out
+
+
 def cpu_info():
     """The host CPUs this process may use: nproc (cgroup-aware), the affinity
     mask, the cgroup v2 CPU quota, and the lscpu model."""
@@ -941,6 +985,7 @@ def main():
     ap.add_argument("--c5-legacy-pool", dest="c5_unique", action="store_false",
                     help="configs[4] from 1024 unique tokens per kid (round-2 layout)")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--e2e-child", metavar="TOKFILE", help=argparse.SUPPRESS)   # measure_e2e_fresh's child
     ap.add_argument("--no-refresh", action="store_true", help="skip configs[4]'s JWKS refresh timings "
                     "(profiling passes: they build key tables)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -948,6 +993,8 @@ def main():
     ap.add_argument("--table-budget-gb", type=float, default=110.0,
                     help="HBM for P-256 key comb tables (jg_set_table_budget): 110 GiB holds the 4 kids at W = 26")
     args = ap.parse_args()
+    if args.e2e_child:
+        return e2e_child_main(args.e2e_child, args.tokens)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -1110,10 +1157,18 @@ def main():
                                                                              C5_E2E["meta"], host_threads)
     C5_E2E.clear()
 
-    # ---- end-to-end Validator.ValidateBatch (host + GPU), rank 0 only
+    # ---- end-to-end Validator.ValidateBatch (host + GPU), rank 0 only: in a
+    # fresh child process (the line), and inside this long-running bench
+    # process beside it
     if rank == 0 and not args.no_e2e:
         jwk = [{"kty": "EC", "kid": f"kid-{i:02d}", "crv": "P-256", **xy} for i, xy in enumerate(p256_jwk_xy(kids))]
-        result["e2e"] = measure_e2e(pool, jwk, args.tokens, host_threads)
+        result["e2e"] = measure_e2e_fresh(pool, args.tokens)
+        inproc = measure_e2e(pool, jwk, args.tokens, host_threads)
+        result["e2e"]["in_bench_process"] = {
+            "value": inproc["value"], "ms_per_batch": inproc["ms_per_batch"],
+            "note": "the same measure_e2e inside this bench process after every other line (tens of GB of token "
+                    "pools and many contexts behind it); profiles/r04_s1_e2e_ab: the fresh-process rate is the "
+                    "path's, and the round-2 build measures the same there"}
 
     # ---- CPU baselines (rank 0, N = 1 only), both on every core the process
     # may use.  `cpu_baseline` is OpenSSL libcrypto (tools/cpuverify): the

@@ -49,6 +49,7 @@
 #include "kernels/ed25519.hpp"
 #include "kernels/hash.hpp"
 #include "kernels/prep.hpp"
+#include "host_mont.hpp"
 #include "kernels/rsa.hpp"
 
 static_assert(sizeof(jg_tok) == 24 && sizeof(jgk::JobDev) == 16, "job layouts");
@@ -1661,6 +1662,10 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
       K.n_off = blob_alloc(S.blob, L);
       K.rr_off = blob_alloc(S.blob, L);
       if (nl > 0) be_to_limbs(n, nl, S.blob.data() + K.n_off, L);
+      // R^2 mod n (R = 2^(28 L)) and n' on the host: ~0.2 ms for an RSA-4096
+      // key (host_mont.hpp; the device's 56 L modular doublings took ~200 ms
+      // for the 32-kid bench set, profiles/r04_s1_keyload_trace.log)
+      if (ok) hostmont::rsa_key_constants(S.blob.data() + K.n_off, L, S.blob.data() + K.rr_off, &K.np);
       if (ok) S.rsa_idx.push_back(i);
       hk.cls = cls;
       hk.valid = ok;
@@ -1849,7 +1854,6 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   if (nk) HIPCHK(hipMemcpyAsync(dk, S.dk.data(), sizeof(DevKey) * nk, hipMemcpyHostToDevice, s));
   if (!S.blob.empty()) HIPCHK(hipMemcpyAsync(blob, S.blob.data(), sizeof(uint32_t) * S.blob.size(), hipMemcpyHostToDevice, s));
   if (!idx.empty()) HIPCHK(hipMemcpyAsync(di, idx.data(), sizeof(int32_t) * idx.size(), hipMemcpyHostToDevice, s));
-  if (nk) launch_rsa_keyprep(dk, blob, (int)nk, s);
   for (int c = CLS_P256; c <= CLS_P521; ++c)
     launch_ec_keyprep(c, dk, blob, di + at[c - CLS_P256], (int)S.ec_idx[c].size(), s);
   launch_ed_keyprep(dk, blob, di + at[3], (int)S.ed_idx.size(), s);

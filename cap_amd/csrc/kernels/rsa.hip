@@ -652,47 +652,6 @@ __global__ void __launch_bounds__(64) JG_RSA_PAD_ATTR k_rsa_pad(RsaArgs a) {
   a.verdict_pad[p] = verdict;
 }
 
-// ------------------------------------------------------------------ key staging
-// One thread per RSA key: n' = -n^-1 mod 2^28 and R^2 mod n (R = 2^(28 L)) by
-// modular doubling.  Runs once per jg_keys_load.
-__global__ void k_rsa_keyprep(DevKey* keys, uint32_t* blob, int nkeys) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nkeys) return;
-  DevKey& K = keys[i];
-  if (K.kind != 1 || !K.valid) return;
-  const int L = (int)K.nlimbs;
-  const uint32_t* N = blob + K.n_off;
-  uint32_t* RR = blob + K.rr_off;
-  uint32_t inv = 1;
-  for (int k = 0; k < 5; ++k) inv *= 2u - N[0] * inv;       // N[0]^-1 mod 2^32
-  K.np = (0u - inv) & M28;
-  // r = 1; double 2*28*L times mod n
-  for (int j = 0; j < L; ++j) RR[j] = j == 0 ? 1u : 0u;
-  for (int it = 0; it < 2 * W28 * L; ++it) {
-    uint32_t c = 0;
-    for (int j = 0; j < L; ++j) {
-      const uint32_t t2 = (RR[j] << 1) | c;
-      c = t2 >> W28;
-      RR[j] = t2 & M28;
-    }
-    // compare (c, RR) >= N ?
-    bool ge = c != 0;
-    if (!ge) {
-      int cmp = 0;
-      for (int j = L - 1; j >= 0 && cmp == 0; --j) cmp = (RR[j] > N[j]) - (RR[j] < N[j]);
-      ge = cmp >= 0;
-    }
-    if (ge) {
-      int32_t br = 0;
-      for (int j = 0; j < L; ++j) {
-        const int32_t t2 = (int32_t)RR[j] - (int32_t)N[j] + br;
-        RR[j] = (uint32_t)t2 & M28;
-        br = t2 >> W28;
-      }
-    }
-  }
-}
-
 }  // namespace
 
 void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const Marker& mk) {
@@ -715,6 +674,3 @@ void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const Marker& mk) {
   mk("pad");
 }
 
-void launch_rsa_keyprep(jgk::DevKey* keys, uint32_t* blob, int nkeys, hipStream_t s) {
-  hipLaunchKernelGGL(k_rsa_keyprep, dim3((nkeys + 63) / 64), dim3(64), 0, s, keys, blob, nkeys);
-}

@@ -53,4 +53,3 @@ static_assert(rsa_sig_rows_l(rsa4k_layout_limbs(RSA4K_NLAYOUT - 1)) <= jgk::SIGW
               "RSA-16K signature rows exceed the scratch");
 
 void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const jgk::Marker& mk);
-void launch_rsa_keyprep(jgk::DevKey* keys, uint32_t* blob, int nkeys, hipStream_t s);

@@ -1,6 +1,7 @@
 // tk_rsa.hip -- TEST INFRASTRUCTURE (libcapjwt_tk.so only, never the product
 // path): the raw RSA public operation y = s^e mod n through the production
-// k_rsa_modexp kernel and k_rsa_keyprep, so tests/test_gpu_rsa.py can compare
+// k_rsa_modexp kernel and the key constants of host_mont.hpp (as jg_keys_load
+// stages them), so tests/test_gpu_rsa.py can compare
 // every output word with Python's pow() -- the EM compare of k_rsa_pad only
 // tells accept from reject.
 #include <hip/hip_runtime.h>
@@ -9,6 +10,7 @@
 #include <initializer_list>
 #include <vector>
 
+#include "../host_mont.hpp"
 #include "../kernels/rsa.hip"   // kernels in an anonymous namespace: this TU's own copy
 
 namespace {
@@ -38,7 +40,7 @@ extern "C" int tk_rsa_modexp(int cls, const uint32_t* n_le, int n_words, uint64_
   const int L = cls == CLS_RSA4K ? rsa4k_limbs_for_bits(bits) : rsa_limbs(cls);
   if (bits == 0 || L == 0 || bits > 28 * L - 2 || !(n_le[0] & 1)) return -1;
 
-  // key blob: n as 28-bit limbs, then R^2 (filled by k_rsa_keyprep)
+  // key blob: n as 28-bit limbs, then R^2 (host_mont.hpp, as jg_keys_load stages it)
   std::vector<uint32_t> blob(2 * (size_t)L, 0);
   for (int j = 0; j < L; ++j) {
     const int bit = 28 * j, q = bit >> 5, sh = bit & 31;
@@ -46,6 +48,7 @@ extern "C" int tk_rsa_modexp(int cls, const uint32_t* n_le, int n_words, uint64_
     blob[j] = (uint32_t)(((w1 << 32) | w0) >> sh) & 0x0fffffffu;
   }
   DevKey K{};
+  hostmont::rsa_key_constants(blob.data(), L, blob.data() + L, &K.np);
   K.kind = 1;
   K.cls = cls;
   K.valid = 1;
@@ -75,7 +78,6 @@ extern "C" int tk_rsa_modexp(int cls, const uint32_t* n_le, int n_words, uint64_
   uint32_t* rows = dev_upload(zero);
   int rc = (dk && dblob && dsig && djobs && dlen && dst && rows) ? 0 : -1;
   if (rc == 0) {
-    launch_rsa_keyprep(dk, dblob, 1, 0);
     RsaArgs a{};
     a.jobs = djobs; a.keys = dk; a.keyblob = dblob; a.sigw = dsig;
     a.xmw = rows; a.xlr = rows + (size_t)L * np; a.yw = rows + (size_t)2 * L * np;
