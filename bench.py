@@ -184,7 +184,7 @@ def ed25519_point_mads_per_token(wa=24):
 def rsa_modexp_mads_per_token(limbs, lanes):
     """k_rsa_modexp (e = 65537): 18 Montgomery products on L 28-bit limbs held
     by `lanes` lanes per token (H = L / lanes each; RSA-2048: L = 74 on 2 lanes,
-    RSA-3072: 112 on 4, RSA-4096: 148 on 4).  To-Montgomery and the final
+    RSA-3072: 112 on 2 (rsa.hpp RSA3K_G), RSA-4096: 148 on 4).  To-Montgomery and the final
     multiply (mont_mul) are 2 L^2 multiply-accumulates each; the 16 squarings
     (mont_sqr) issue each limb product once -- lanes^2 * H(H+1)/2 for the
     square (L(L+1)/2 plus the diagonal blocks' duplicated diagonal) + L^2 for
@@ -382,7 +382,10 @@ def measure_pcie(ctx, arena, toks, iters=5, chunks=(32768, 65536, 131072), warm=
     """jg_verify_batch end to end from PINNED host buffers: H2D of arena + jobs
     (chunked, copies overlapping the previous chunk's kernels), planning,
     kernels, verdict D2H.  `warm` untimed passes per chunk size, then the best
-    of `iters`.  Reported beside `value`, never as it."""
+    of `iters`.  A chunk entry "zc" runs the library's class-major zero-copy
+    plans (jg_set_zero_copy: mixed batches only; per-class gathers from the
+    pinned arena instead of chunk DMAs); integer entries run the chunked DMA
+    pipeline with zero-copy plans off.  Reported beside `value`, never as it."""
     from cap_amd import _lib
     L = _lib.lib()
     pa = _lib.PinnedBuffer(len(arena))
@@ -391,7 +394,11 @@ def measure_pcie(ctx, arena, toks, iters=5, chunks=(32768, 65536, 131072), warm=
     tp = toks.ctypes.data_as(ctypes.POINTER(_lib.JgTok))
     per_chunk = {}
     for ch in chunks:
-        ctx.set_chunk(ch)
+        if ch == "zc":
+            ctx.set_zero_copy(True)
+        else:
+            ctx.set_zero_copy(False)
+            ctx.set_chunk(ch)
         best = float("inf")
         # untimed passes first: the pipeline slots size their device and
         # pinned buffers once per process (a long-running stream never pays
@@ -407,6 +414,7 @@ def measure_pcie(ctx, arena, toks, iters=5, chunks=(32768, 65536, 131072), warm=
             best = min(best, time.perf_counter() - t0)
         per_chunk[ch] = best
     ctx.set_chunk(65536)
+    ctx.set_zero_copy(False)
     pa.free()
     ch, best = min(per_chunk.items(), key=lambda kv: kv[1])
     bw = h2d_bandwidth(len(arena))
@@ -415,8 +423,10 @@ def measure_pcie(ctx, arena, toks, iters=5, chunks=(32768, 65536, 131072), warm=
             "chunk": ch, "ms_by_chunk": {str(k): v * 1e3 for k, v in per_chunk.items()},
             "arena_bytes": len(arena), "h2d_bytes_per_token": bytes_per_tok,
             "raw_h2d_GBps": bw / 1e9, "h2d_bound": bw / bytes_per_tok,
-            "note": "jg_verify_batch from pinned host memory (chunked H2D overlapping kernels + plan + D2H), "
-                    f"best of {iters} after one warm-up pass; h2d_bound = raw pinned H2D bandwidth / bytes per token; not the headline"}
+            "note": "jg_verify_batch from pinned host memory (chunked H2D overlapping kernels + plan + D2H, or "
+                    "\"zc\": class-major zero-copy plans with per-class gathers over PCIe), "
+                    f"best of {iters} after {warm} warm-up pass(es); h2d_bound = raw pinned H2D bandwidth / bytes per token; "
+                    "not the headline"}
 
 
 def measure_e2e(pool, kids_jwk, total, threads):
@@ -838,7 +848,7 @@ def run_configs(ctx, args, threads, rank, world, dist):
     kcls = [key_class(m[4]) for m in meta]
     present = set(kcls)
     wof = {c: next(w for w, k in zip(c5w, kcls) if k == c) for c in ("p256", "p384", "p521", "ed25519") if c in kcls}
-    work = {"rsa2048_modexp": rsa_modexp_mads_per_token(74, 2), "rsa3072_modexp": rsa_modexp_mads_per_token(112, 4),
+    work = {"rsa2048_modexp": rsa_modexp_mads_per_token(74, 2), "rsa3072_modexp": rsa_modexp_mads_per_token(112, 2),
             "rsa4096_modexp": rsa_modexp_mads_per_token(148, 4), "p256_point": p256_point_mads_per_token(wof.get("p256")),
             "p384_point": p384_point_mads_per_token(wof.get("p384")),
             "p521_point": p521_point_mads_per_token(wof.get("p521")),
@@ -859,7 +869,7 @@ def run_configs(ctx, args, threads, rank, world, dist):
     # plan, kernels, verdicts back), chunks overlapping
     share = 10_000_000 // 8
     arena, toks = pack(pool, algs, keyidx, share)
-    st = measure_pcie(ctx, arena, toks, iters=4, chunks=(131072, 262144, 524288), warm=3)
+    st = measure_pcie(ctx, arena, toks, iters=4, chunks=("zc", 262144, 524288), warm=3)
     st["workload"] = f"{share} tokens per GPU (10M / 8) streamed with H2D"
     line["stream"] = st
     del arena, toks

@@ -21,7 +21,7 @@ CURVE_IDS = {"P-256": 1, "P-384": 2, "P-521": 3}
 EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_last_error",
            "jg_host_alloc", "jg_host_free", "jg_batch_stage", "jg_batch_run", "jg_batch_enqueue", "jg_batch_sync",
            "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
-           "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_table_budget", "jg_keys_wait_tables",
+           "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_zero_copy", "jg_set_table_budget", "jg_keys_wait_tables",
            "jg_keys_table_widths", "jg_debug_fail_alloc", "jg_debug_table_digest",
            "jg_debug_max_upgrades", "jg_debug_lifetime_check"]
 
@@ -76,6 +76,7 @@ def lib():
         L.jg_submit.argtypes = [vp, vp, sz, ctypes.POINTER(JgTok), sz, vp, ctypes.POINTER(vp)]
         L.jg_wait.argtypes = [vp, vp]
         L.jg_set_chunk.argtypes = [vp, sz]
+        L.jg_set_zero_copy.argtypes = [vp, ctypes.c_int, sz]
         L.jg_set_table_budget.argtypes = [vp, ctypes.c_uint64]
         L.jg_hash_batch.argtypes = [vp, vp, sz, vp, sz, vp]
         L.jg_keys_wait_tables.argtypes = [vp]
@@ -233,6 +234,12 @@ class Context:
     def set_chunk(self, jobs):
         if lib().jg_set_chunk(self.h, jobs) != 0:
             raise JgError("jg_set_chunk: chunk must be >= 64 jobs")
+
+    def set_zero_copy(self, enable, max_jobs=0):
+        """jg_set_zero_copy: class-major zero-copy plans for mixed batches whose
+        arena is a PinnedBuffer (off by default), and the jobs per plan."""
+        if lib().jg_set_zero_copy(self.h, 1 if enable else 0, max_jobs) != 0:
+            raise JgError("jg_set_zero_copy: max_jobs must be 0 or >= 64")
 
     def set_table_budget(self, nbytes):
         """jg_set_table_budget: HBM for all key comb tables (applies at the next load_keys)."""

@@ -61,6 +61,7 @@ namespace {
 constexpr size_t ARENA_SLACK = 256;   // aligned SHA word reads may run past the last string
 constexpr int NLANE = 3;              // compute streams per device (HW queues 1..3; the copy stream has 0)
 constexpr int NSLOT = 8;              // chunk buffer sets per device (pipeline depth)
+constexpr int NZSLOT = 2;             // buffer sets of zero-copy plans (whole items; after the NSLOT ring)
 constexpr int NALG = 16;              // alg ids 0..15 in the class table (jg_alg <= 10)
 
 #define HIPCHK(x)                                                                   \
@@ -102,6 +103,17 @@ struct PhaseClock {
     t = std::chrono::steady_clock::now();
   }
 };
+
+// initial zero-copy settings of a context (zc plans: see run_plan's zc_feed)
+bool zc_env_enabled() {
+  const char* e = std::getenv("CAPJWT_ZC");
+  return e && std::atoi(e) != 0;
+}
+size_t zc_env_max_jobs() {
+  const char* e = std::getenv("CAPJWT_ZC_MAX");
+  const long long v = e ? std::atoll(e) : 0;
+  return v >= 64 ? (size_t)v : (size_t)2 << 20;
+}
 
 size_t chunk_jobs() {
   static const size_t n = [] {
@@ -513,6 +525,7 @@ struct Plan {
 struct PlanScratch {              // reused across chunks
   std::vector<uint8_t> tcls;      // class per job (host fill only)
   std::vector<int64_t> start, total;   // per bucket [nkeys + 1]
+  std::vector<uint64_t> kmax;     // zero-copy plans: per key, the longest job span (bytes)
 };
 
 struct Ticket {
@@ -544,9 +557,11 @@ struct Slot {
   hipEvent_t copied = nullptr;     // copy stream: the chunk's inputs are on the device
   hipEvent_t tr_a = nullptr, tr_b = nullptr, tr_c = nullptr;   // CAPJWT_PIPE_TRACE: H2D start / end, kernels end
   hipEvent_t ev_planned = nullptr, ev_cls[NCLS] = {};            // class-grouped chunks (GroupFan)
+  hipEvent_t ev_fed[NCLS] = {};                                  // zero-copy plans: class gathered (GroupFan::fed)
   double host_ms[5] = {};                                       // wait, plan, enqueue, of which H2D calls, of which sizing
   int grows = 0;                                                // buffer reallocations while enqueuing (trace)
   int chunk_no = 0;
+  uint64_t seq = 0;                // enqueue order across both slot rings (oldest completes first)
   size_t reserved = 0;             // chunk capacity (jobs) the buffers were sized for
   uint64_t reserved_epoch = ~0ull; // key table they were sized against
   bool inflight = false;
@@ -568,6 +583,7 @@ struct Item {                     // one device's share of a submission
   size_t chunk = 0, nchunks = 0;
   std::vector<size_t> cuts;       // chunk boundaries (chunk_cuts)
   bool grouped = false;           // mixed classes: chunks run class-grouped (enqueue_chunk)
+  bool zc = false;                // class-major zero-copy plans (zc_enabled): no arena copy
 };
 
 struct Device {
@@ -590,8 +606,10 @@ struct Device {
   // kernels on its own stream once its copy event fires
   hipStream_t copy = nullptr;
   Lane lanes[NLANE];
-  Slot slots[NSLOT];
-  int next_slot = 0, next_lane = 0;
+  Slot slots[NSLOT + NZSLOT];      // the chunk ring, then the zero-copy plans' ring
+  int next_slot = 0, next_lane = 0, next_zslot = 0;
+  double gload[3] = {0, 0, 0};    // class-grouped chunks: class cost queued per group lane (relative)
+  uint64_t slot_seq = 0;
   int next_res = 0;                // resident batches staged (CAPJWT_BATCH_LANES)
   std::thread worker;
   std::mutex qmu;
@@ -634,6 +652,8 @@ struct jg_ticket {
 struct jg_ctx {
   std::vector<std::unique_ptr<Device>> devs;
   std::atomic<size_t> chunk{chunk_jobs()};   // jobs per pipeline chunk
+  std::atomic<bool> zc{zc_env_enabled()};    // class-major zero-copy plans (jg_set_zero_copy)
+  std::atomic<size_t> zc_max{zc_env_max_jobs()};
   std::atomic<uint64_t> table_budget{default_table_budget()};   // HBM for key comb tables, all curves
   std::atomic<int> fail_alloc{0};            // jg_debug_fail_alloc countdown
   // jg_debug_max_upgrades: background table upgrades left before the upgrader
@@ -750,12 +770,21 @@ bool class_grouping() {
   }();
   return on;
 }
-bool group_ctrl_copy() {
-  static const bool on = [] {
+// Where a class-grouped chunk's plan fill runs (everything of the chunk waits
+// for it).  Default: on the group lane expected to drain first -- the one
+// with the least class cost queued (Device::gload).  On the join lane (the
+// round-3 default, CAPJWT_GROUP_CTRL=join) it queued behind the previous
+// chunk's whole RSA-4K chain while the other lanes idled 2-4 ms
+// (profiles/r04_s3/zc_trace); CAPJWT_GROUP_CTRL=copy: on the copy stream.
+enum { CTRL_LEAST = 0, CTRL_JOIN = 1, CTRL_COPY = 2 };
+int group_ctrl() {
+  static const int m = [] {
     const char* e = std::getenv("CAPJWT_GROUP_CTRL");
-    return e && std::string(e) == "copy";
+    if (!e) return (int)CTRL_LEAST;
+    const std::string v(e);
+    return v == "copy" ? (int)CTRL_COPY : v == "join" ? (int)CTRL_JOIN : (int)CTRL_LEAST;
   }();
-  return on;
+  return m;
 }
 int cls_group(int c) { return c == CLS_RSA4K ? 1 : c <= CLS_RSA3K ? 0 : 2; }
 
@@ -817,6 +846,25 @@ const uint8_t* device_view(const void* p) {
     return nullptr;
   }
   return (const uint8_t*)dp;
+}
+
+// Blocks from jg_host_alloc: base -> usable size.  Each is allocated with
+// ARENA_SLACK more bytes than asked for, so a zero-copy plan's prep kernels
+// may read past the last token of an arena held in one (as they do past every
+// token of a device arena copy) without leaving the allocation.
+std::mutex g_hmu;
+std::map<uintptr_t, size_t>& g_hblocks = *new std::map<uintptr_t, size_t>();
+
+// an arena the prep kernels may read in place: inside one jg_host_alloc block
+// and under 4 GiB (JobDev offsets are 32-bit)
+bool zc_arena_ok(const uint8_t* arena, size_t len) {
+  if (!arena || ((uintptr_t)arena & 15) || len + ARENA_SLACK >= (uint64_t(1) << 32)) return false;
+  const uintptr_t a = (uintptr_t)arena;
+  std::lock_guard<std::mutex> g(g_hmu);
+  auto it = g_hblocks.upper_bound(a);
+  if (it == g_hblocks.begin()) return false;
+  --it;
+  return a >= it->first && a + len <= it->first + it->second;
 }
 
 // Dispatch plan of toks[0..ntok): a counting sort by (class, key) --
@@ -973,12 +1021,15 @@ void upload(Bufs* B, hipStream_t s, const Plan& P, const uint8_t* arena, size_t 
 
 // Plan block of a pipeline chunk (pinned staging and its device copy alike):
 // bucket cursors | padding ranges | the chunk's jg_tok jobs in caller order.
+// Zero-copy plans add, per bucket, the base offset, first padded slot and
+// slot stride of its region of the device arena (k_zc_gather).
 struct PlanBlock {
-  size_t cur_off, pad_off, toks_off, bytes;
+  size_t cur_off, pad_off, zc_off, toks_off, bytes;
   PlanBlock(size_t nbuckets, size_t n) {
     cur_off = 0;
     pad_off = sizeof(uint64_t) * nbuckets;
-    toks_off = (pad_off + 2 * sizeof(int64_t) * nbuckets + 63) & ~size_t(63);
+    zc_off = pad_off + 2 * sizeof(int64_t) * nbuckets;
+    toks_off = (zc_off + 3 * sizeof(uint64_t) * nbuckets + 63) & ~size_t(63);
     bytes = toks_off + sizeof(jg_tok) * std::max<size_t>(n, 1);
   }
 };
@@ -1059,6 +1110,40 @@ bool pipeline_fanout() {
   return on;
 }
 
+// Class-major zero-copy streams (round 4).  A mixed (class-grouped)
+// submission whose arena lies in memory from jg_host_alloc runs as ONE plan
+// over the whole item instead of arrival-order chunks, and its arena is never
+// DMAed: per class, a gather kernel (k_zc_gather) copies that class's token
+// bytes from the pinned arena over PCIe into the plan's device arena, and the
+// class's chain (prep, arithmetic) starts as soon as its own gather is done.
+// Every class gets one launch chain over all of its tokens.  Chunked, a mixed
+// stream's first chunk copy (~5.7 ms for 524 k tokens) was exposed and each
+// chunk's classes were too small to fill the chip
+// (profiles/r03_s22_c5_pipe_trace_524k.txt); a zero-copy gather of shuffled
+// 640-B records reads at the SDMA copy's rate (profiles/r04_s2_zc_gather.txt).
+// (A first form let the prep kernels read the pinned arena directly: their
+// 4-byte loads interleaved with SHA rounds drew ~15 GB/s from the link and
+// the stream ran at half the chunked rate, profiles/r04_s3/zc_prep_direct_*.)
+// Per context (jg_set_zero_copy), OFF by default: the chunked pipeline is
+// faster on configs[4] today (profiles/r04_s3/zc_gather_*: 42.6 vs 24.7 ms per
+// 1.25 M tokens).  The initial setting is CAPJWT_ZC (1 turns it on) and
+// CAPJWT_ZC_MAX, the jobs per zero-copy plan (a
+// longer item is cut into equal plans; device scratch grows with it, ~5 KB per
+// job with RSA-4K keys).
+//
+// Where the gathers of a zero-copy plan run.  1 (default): all on one feed
+// stream (the copy stream), the costliest class first, so each gather has the
+// link to itself and the longest arithmetic chain starts earliest; each
+// class's chain waits for its own gather on the lane of its class group.  0:
+// each class's gather heads its own chain on its group lane (A/B).
+bool zc_feed() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_ZC_FEED");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 // Runs of consecutive keys of class c (the plan's key order) whose comb tables
 // have one width: fn(begin, end, w) per run, over padded slots.  All of a
 // curve's keys share one width except while a background upgrade is widening
@@ -1116,6 +1201,14 @@ struct GroupFan {
   hipStream_t cls[NCLS] = {};
   hipEvent_t start = nullptr;
   hipEvent_t done[NCLS] = {};
+  // zero-copy plans: every class's k_zc_gather on `feed`, costliest class
+  // first (zc_feed; else at the head of its own chain); class c's chain on
+  // cls[c] waits for fed[c]
+  hipStream_t feed = nullptr;
+  hipEvent_t fed[NCLS] = {};
+  double cost[NCLS] = {};         // class device cost of the plan (feed order)
+  bool zc = false;
+  ZcGatherArgs gather{};          // begin / end set per class
 };
 
 void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, const Plan& P, jg_batch* marks,
@@ -1144,7 +1237,16 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
                            : nullptr;
   uint32_t* rows = (uint32_t*)B->rows.p;
   if (conc) HIPCHK(hipEventRecord(L->ev_start, s0));
-  for (int c = 1; c < NCLS; ++c) {
+  const bool zc = gf && gf->zc, feed = zc && gf->feed;
+  int order[NCLS - 1];
+  for (int i = 0; i < NCLS - 1; ++i) order[i] = i + 1;
+  if (feed) {
+    std::stable_sort(order, order + NCLS - 1, [&](int x, int y) { return gf->cost[x] > gf->cost[y]; });
+    if (gf->feed != gf->ctrl) HIPCHK(hipStreamWaitEvent(gf->feed, gf->start, 0));
+  }
+  std::vector<std::pair<int, EcArgs>> exact_later;      // class-grouped chunks: k_ec_exact on the join lane
+  for (int oi = 0; oi < NCLS - 1; ++oi) {
+    const int c = order[oi];
     const ClassRange r = P.ranges[c];
     if (r.end <= r.begin) continue;
     // every class reads and writes only columns [r.begin, r.end) of the shared
@@ -1155,7 +1257,18 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
       HIPCHK(hipStreamWaitEvent(s, L->ev_start, 0));
     } else if (gf) {
       s = gf->cls[c];
-      HIPCHK(hipStreamWaitEvent(s, gf->start, 0));
+      if (!feed) HIPCHK(hipStreamWaitEvent(s, gf->start, 0));
+    }
+    if (zc) {
+      // the class's token bytes from the caller's pinned arena into HBM
+      ZcGatherArgs za = gf->gather;
+      za.begin = r.begin;
+      za.end = r.end;
+      launch_zc_gather(za, feed ? gf->feed : s);
+      if (feed) {
+        HIPCHK(hipEventRecord(gf->fed[c], gf->feed));
+        HIPCHK(hipStreamWaitEvent(s, gf->fed[c], 0));
+      }
     }
     pa.begin = r.begin;
     pa.end = r.end;
@@ -1190,9 +1303,20 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
       ea.exc_count = (uint32_t*)B->exc_cnt.p + c;
       ea.npad = np;
       ea.exc_reset = 1;
+      // class-grouped chunks: the exact kernels wait for the join lane (below).
+      // A k_ec_exact launch needs a SIMD with ~290 VGPRs free even when it has
+      // no work; behind the RSA modexps (256 VGPRs, 2 waves per SIMD) it waited
+      // 0.8-1.4 ms for one, and every later class of the EC group's lane (and
+      // the next chunk's) waited behind it (profiles/r04_s3/zc_trace)
+      ea.part = gf ? EC_FAST : EC_ALL;
       width_runs(K, G, P, c, [&](int64_t b, int64_t e, int w) {
         ea.begin = b; ea.end = e; ea.wq = w;
         launch_ec(c, ea, s, marker(marks, c));
+        if (gf) {
+          EcArgs x = ea;
+          x.part = EC_EXACT;
+          exact_later.push_back({c, x});
+        }
         ea.exc_reset = 0;          // later runs of the class append to its exception list
       });
     } else {
@@ -1217,6 +1341,7 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
       if (s != s0) HIPCHK(hipStreamWaitEvent(s0, gf->done[c], 0));
     }
   }
+  for (const auto& [c, x] : exact_later) launch_ec(c, x, s0, Marker{});   // s0 waited for every class
   launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s0);
   mark(marks, "scatter");
   HIPCHK(hipGetLastError());
@@ -1227,6 +1352,7 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
       else if (gf) G.uses.record(gf->cls[c], "group lane", c);
     }
     if (gf) G.uses.record(gf->ctrl, "chunk control");
+    if (feed) G.uses.record(gf->feed, "zero-copy gather feed");
     G.uses.record(s0, gf ? "join lane" : "lane");
   }
 }
@@ -1274,7 +1400,7 @@ void finish_slot(Slot& S) {
 // and class mix never reallocate in the stream (a hipFree synchronises the
 // device, a hipHostMalloc page-locks): ~1 GB of device scratch per slot at
 // C = 64 k for a context with RSA-4K keys, far less for ES256 alone.
-void reserve_slot(const KeyState& K, Slot& S, size_t C, size_t nbuckets, double bytes_per_job) {
+void reserve_slot(const KeyState& K, Slot& S, size_t C, size_t nbuckets, double bytes_per_job, bool zc) {
   const PlanBlock L(nbuckets, C);
   S.h_meta.get(L.bytes);
   // the plan block's device copy too: grown per chunk size, its hipFree
@@ -1292,7 +1418,7 @@ void reserve_slot(const KeyState& K, Slot& S, size_t C, size_t nbuckets, double 
   }
   const size_t npad = C + (size_t)WAVE * nbuckets;
   Bufs* B = &S.bufs;
-  B->arena.get((size_t)(bytes_per_job * 1.25 * (double)C) + ARENA_SLACK);
+  B->arena.get(zc ? ARENA_SLACK : (size_t)(bytes_per_job * 1.25 * (double)C) + ARENA_SLACK);
   B->jobs.get(sizeof(JobDev) * npad);
   B->perm.get(sizeof(int32_t) * npad);
   B->sigw.get(sizeof(uint32_t) * sig_rows * npad);
@@ -1317,7 +1443,8 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   if (S.reserved != it.chunk || S.reserved_epoch != K.epoch) {
     double bpj = 0;
     for (size_t i = 0; i < std::min<size_t>(n, 256); ++i) bpj += (double)(tok_end(toks[i]) - toks[i].off);
-    reserve_slot(K, S, std::max(it.chunk, n), K.keys.size() + 1, n ? bpj / (double)std::min<size_t>(n, 256) : 512.0);
+    reserve_slot(K, S, std::max(it.chunk, n), K.keys.size() + 1, n ? bpj / (double)std::min<size_t>(n, 256) : 512.0,
+                 it.zc);
   }
   // One pass over the caller's jobs: the arena span they use, the bucket
   // counts of the plan, and their copy into the pinned plan block.  The span
@@ -1328,6 +1455,8 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   uint8_t* hb = (uint8_t*)S.h_meta.get(L.bytes);
   jg_tok* ht = (jg_tok*)(hb + L.toks_off);
   uint64_t amin = UINT64_MAX, amax = 0, need = 0, seen[2];
+  std::vector<uint64_t>& kmax = d->plan.kmax;
+  if (it.zc) kmax.assign(NB, 0);
   plan_count(K, toks, n, d->plan, false, seen, [&](size_t i) {
     const jg_tok& t = toks[i];
     const uint64_t e = tok_end(t);
@@ -1335,16 +1464,38 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
     amax = std::max<uint64_t>(amax, e);
     need += e - t.off;
     ht[i] = t;
+    if (it.zc && classify(K, t) != CLS_REJECT) kmax[t.key_idx] = std::max<uint64_t>(kmax[t.key_idx], e - t.off);
   });
   if (n == 0) amin = amax = 0;
   const uint64_t base = amin & ~uint64_t(255);
   const uint64_t span = amax - base;
   // JobDev offsets are 32-bit: a span that does not fit is repacked
   const bool compact = span <= 2 * need + 65536 && span < (uint64_t(1) << 32) - ARENA_SLACK;
-  const uint8_t* src;
+  const uint8_t* src = nullptr;
   size_t bytes;
   uint64_t dbase;                                  // subtracted from job offsets on the device
-  if (compact) {
+  // Zero-copy plan: the device arena holds each key's jobs at a fixed stride
+  // (its longest span + 30 bytes of 16-byte alignment, rounded to 16), filled
+  // by k_zc_gather from the caller's pinned arena.  A layout of 4 GiB or more
+  // (JobDev offsets are 32-bit) takes the DMA path instead.
+  bool zc = it.zc;
+  uint64_t zbytes = 0;
+  uint64_t* zc_tab = (uint64_t*)(hb + L.zc_off);   // [NB] base | [NB] first slot | [NB] stride
+  if (zc) {
+    const int64_t* tot = d->plan.total.data();
+    for (size_t k = 0; k < NB; ++k) {
+      const uint64_t slots = k + 1 < NB ? (uint64_t)(tot[k] + WAVE - 1) / WAVE * WAVE : 0;   // the reject bucket is never prepped
+      const uint64_t stride = slots ? (kmax[k] + 30 + 15) & ~uint64_t(15) : 0;
+      zc_tab[k] = zbytes;
+      zc_tab[2 * NB + k] = stride;
+      zbytes += slots * stride;
+    }
+    if (zbytes + ARENA_SLACK >= (uint64_t(1) << 32)) zc = false;
+  }
+  if (zc) {
+    bytes = (size_t)zbytes;                        // arena size; nothing is DMAed
+    dbase = base;
+  } else if (compact) {
     bytes = (size_t)span;
     dbase = base;
     if (it.dev_arena) {
@@ -1378,6 +1529,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
     cur[k] = (uint64_t)d->plan.start[k];
     pad[2 * k] = r.first;
     pad[2 * k + 1] = r.second;
+    if (zc) zc_tab[NB + k] = (uint64_t)d->plan.start[k];
   }
   Lane& LN = d->lanes[d->next_lane];
   d->next_lane = (d->next_lane + 1) % NLANE;
@@ -1398,7 +1550,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   const uint8_t* hbd = (const uint8_t*)S.h_meta.dp;
   const hipStream_t cs = d->copy;
   if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
-  if (bytes) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, cs));
+  if (bytes && !zc) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, cs));
   int nact = 0, jgrp = 0;
   double gcost[3] = {0, 0, 0};
   for (int c = 1; c < NCLS; ++c) {
@@ -1409,7 +1561,8 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   }
   for (int g = 1; g < 3; ++g)
     if (gcost[g] > gcost[jgrp]) jgrp = g;
-  const bool grouped = it.grouped && nact >= 2;
+  // a zero-copy plan always runs grouped: its classes' gathers ride on the GroupFan
+  const bool grouped = (it.grouped && nact >= 2) || zc;
   // grouped chunks: the whole plan block goes over by DMA behind the arena
   // (the plan fill then reads device memory); else the header by a copy
   // kernel and the jobs read in place from pinned memory
@@ -1419,11 +1572,33 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   if (tr) S.host_ms[3] = ms_since(t_enq);
   GroupFan gf;
   hipStream_t fs = s;                              // the plan fill's stream
+  if (zc) {
+    gf.zc = true;
+    gf.gather.src = it.dev_arena + base;
+    gf.gather.jobs = (JobDev*)S.bufs.jobs.p;
+    gf.gather.kbase = (const uint64_t*)(dm + L.zc_off);
+    gf.gather.kstart = (const int64_t*)(dm + L.zc_off + sizeof(uint64_t) * NB);
+    gf.gather.kstride = (const uint64_t*)(dm + L.zc_off + 2 * sizeof(uint64_t) * NB);
+    gf.gather.dst = (uint8_t*)S.bufs.arena.p;
+    if (zc_feed()) {
+      gf.feed = cs;                                // the copy stream carries no arena copies now
+      for (int c = 1; c < NCLS; ++c) {
+        gf.fed[c] = S.ev_fed[c];
+        gf.cost[c] = CLS_COST[c] * (double)(P.ranges[c].end - P.ranges[c].begin);
+      }
+    }
+  }
   if (grouped) {
     gf.join = d->lanes[jgrp].stream;
-    // CAPJWT_GROUP_CTRL=copy: plan fill on the copy stream (A/B); default:
-    // on the join lane once the copies have landed
-    gf.ctrl = group_ctrl_copy() ? cs : gf.join;
+    int least = 0;
+    for (int g = 1; g < 3; ++g)
+      if (d->gload[g] < d->gload[least]) least = g;
+    const int cm = group_ctrl();
+    gf.ctrl = cm == CTRL_COPY ? cs : cm == CTRL_JOIN ? gf.join : d->lanes[least].stream;
+    // queued class cost per group lane, relative (the smallest kept at 0)
+    double lo = 1e300;
+    for (int g = 0; g < 3; ++g) lo = std::min(lo, d->gload[g] += gcost[g]);
+    for (int g = 0; g < 3; ++g) d->gload[g] -= lo;
     for (int c = 1; c < NCLS; ++c) gf.cls[c] = d->lanes[cls_group(c)].stream;
     gf.start = S.ev_planned;
     for (int c = 0; c < NCLS; ++c) gf.done[c] = S.ev_cls[c];
@@ -1481,12 +1656,20 @@ void process_item(Device* d, size_t dslot, Item& it) {
         it.t->fail(-1, bad);
         break;
       }
-      Slot& S = d->slots[d->next_slot];
-      d->next_slot = (d->next_slot + 1) % NSLOT;
+      Slot* Sp;
+      if (it.zc) {
+        Sp = &d->slots[NSLOT + d->next_zslot];
+        d->next_zslot = (d->next_zslot + 1) % NZSLOT;
+      } else {
+        Sp = &d->slots[d->next_slot];
+        d->next_slot = (d->next_slot + 1) % NSLOT;
+      }
+      Slot& S = *Sp;
       const auto tw = std::chrono::steady_clock::now();
-      finish_slot(S);                 // the slot's previous chunk (NSLOT chunks ago)
+      finish_slot(S);                 // the slot's previous chunk (a ring length ago)
       const double wait_ms = pipe_trace() ? ms_since(tw) : 0.0;
       enqueue_chunk(d, dslot, S, it, it.toks + lo, hi - lo, it.out + lo);
+      S.seq = ++d->slot_seq;
       S.host_ms[0] = wait_ms;
       S.chunk_no = (int)enq;
       ++enq;
@@ -1517,12 +1700,12 @@ void worker_loop(Device* d, size_t dslot) {
     lk.unlock();
     {
       std::lock_guard<std::mutex> g(d->mu);
-      for (int k = 0; k < NSLOT; ++k) {
-        Slot& S = d->slots[(d->next_slot + k) % NSLOT];    // oldest first
-        if (!S.inflight) continue;
-        finish_slot(S);
+      Slot* oldest = nullptr;
+      for (auto& S : d->slots)
+        if (S.inflight && (!oldest || S.seq < oldest->seq)) oldest = &S;
+      if (oldest) {
+        finish_slot(*oldest);
         any = true;
-        break;
       }
     }
     lk.lock();
@@ -2118,6 +2301,8 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
     }
   }
   const uint8_t* dview = device_view(arena);
+  const bool zc_ok = ctx->zc.load() && dview && zc_arena_ok(arena, arena_len);
+  const size_t zmax = ctx->zc_max.load();
   const size_t C = ctx->chunk.load();
   std::vector<Item> items;
   for (size_t k = 0; k < nd; ++k) {
@@ -2137,7 +2322,16 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
     // grouped chunks serialise each class group's launches on one lane, so a
     // long ramp of small chunks would queue latency-bound launches (an
     // RSA-4096 modexp takes ~1.5 ms at any size): start at C / 4
-    it.cuts = chunk_cuts(it.lo, it.hi, C, it.grouped ? std::max<size_t>(4096, C / 4) : 4096, !it.grouped);
+    it.zc = zc_ok && it.grouped;
+    if (it.zc) {
+      // whole item as one plan (or equal plans of at most zc_max_jobs)
+      const size_t n = it.hi - it.lo, parts = (n + zmax - 1) / zmax;
+      it.cuts.clear();
+      for (size_t k = 0; k <= parts; ++k) it.cuts.push_back(it.lo + n * k / parts);
+      it.chunk = (n + parts - 1) / parts;
+    } else {
+      it.cuts = chunk_cuts(it.lo, it.hi, C, it.grouped ? std::max<size_t>(4096, C / 4) : 4096, !it.grouped);
+    }
     it.nchunks = it.cuts.size() - 1;
     t->pending += it.nchunks;
     items.push_back(std::move(it));
@@ -2195,6 +2389,7 @@ jg_ctx* jg_create(const int* devices, int ndev) {
         HIPCHK(hipEventCreate(&s.tr_c));
         HIPCHK(hipEventCreateWithFlags(&s.ev_planned, hipEventDisableTiming));
         for (auto& e : s.ev_cls) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (auto& e : s.ev_fed) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       }
       HIPCHK(hipStreamCreateWithFlags(&d->kstream, hipStreamNonBlocking));
       HIPCHK(hipStreamCreateWithFlags(&d->ustream, hipStreamNonBlocking));
@@ -2237,6 +2432,8 @@ void jg_destroy(jg_ctx* ctx) {
     for (auto& s : d->slots) {
       if (s.done) (void)hipEventDestroy(s.done);
       for (hipEvent_t e : s.ev_cls)
+        if (e) (void)hipEventDestroy(e);
+      for (hipEvent_t e : s.ev_fed)
         if (e) (void)hipEventDestroy(e);
       for (hipEvent_t e : {s.tr_a, s.tr_b, s.tr_c, s.copied, s.ev_planned})
         if (e) (void)hipEventDestroy(e);
@@ -2421,6 +2618,13 @@ int jg_wait(jg_ctx* ctx, jg_ticket* t) {
 int jg_set_chunk(jg_ctx* ctx, size_t jobs) {
   if (!ctx || jobs < 64) return -1;
   ctx->chunk.store(jobs);
+  return 0;
+}
+
+int jg_set_zero_copy(jg_ctx* ctx, int enable, size_t max_jobs) {
+  if (!ctx || (max_jobs != 0 && max_jobs < 64)) return -1;
+  ctx->zc.store(enable != 0);
+  if (max_jobs) ctx->zc_max.store(max_jobs);
   return 0;
 }
 
@@ -2632,12 +2836,21 @@ const char* jg_last_error(jg_ctx* ctx) {
 
 void* jg_host_alloc(size_t bytes) {
   void* p = nullptr;
-  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
+  if (bytes == 0) bytes = 1;
+  if (hipHostMalloc(&p, bytes + ARENA_SLACK, hipHostMallocPortable) != hipSuccess) return nullptr;
+  std::memset((uint8_t*)p + bytes, 0, ARENA_SLACK);
+  std::lock_guard<std::mutex> g(g_hmu);
+  g_hblocks[(uintptr_t)p] = bytes;
   return p;
 }
 
 void jg_host_free(void* p) {
-  if (p) (void)hipHostFree(p);
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> g(g_hmu);
+    g_hblocks.erase((uintptr_t)p);
+  }
+  (void)hipHostFree(p);
 }
 
 const char* jg_version(void) { return "capjwt 0.2 (gfx950, HIP)"; }

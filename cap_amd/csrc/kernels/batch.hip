@@ -69,7 +69,44 @@ __global__ void __launch_bounds__(256) k_copy1(const uint8_t* __restrict__ src, 
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
 }
 
+// 16 lanes per job, 16 B per lane, grid-stride over the class range: the
+// access pattern of tools/ubench/zc_read.hip's gather (56 GB/s from pinned
+// memory, the SDMA copy's rate).  A job's bytes [off, end) are copied as the
+// 16-byte-aligned span around them (src is 16-byte aligned: submit_to), so
+// the copy starts (off & 15) bytes into its slot.  Reads reach at most 15
+// bytes past the last token's end (inside the block's ARENA_SLACK).
+__global__ void __launch_bounds__(256) k_zc_gather(ZcGatherArgs a) {
+  const int sub = threadIdx.x & 15;
+  const int64_t g0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int64_t ng = ((int64_t)gridDim.x * blockDim.x) >> 4;
+  for (int64_t p = a.begin + g0; p < a.end; p += ng) {
+    const JobDev jb = a.jobs[p];
+    if (!job_live(jb)) continue;
+    const int key = job_key(jb);
+    const uint32_t end = max(jb.off + jb.sig_in_len, jb.sig_off + job_siglen(jb));
+    const uint32_t lo = jb.off & ~15u, hi = (end + 15u) & ~15u;
+    const uint64_t d0 = a.kbase[key] + (uint64_t)(p - a.kstart[key]) * a.kstride[key];
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(a.src + lo);
+    uint4* __restrict__ dst = reinterpret_cast<uint4*>(a.dst + d0);
+    const uint32_t n16 = (hi - lo) >> 4;
+    for (uint32_t i = (uint32_t)sub; i < n16; i += 16) dst[i] = src[i];
+    if (sub == 0) {
+      a.jobs[p].off = (uint32_t)(d0 + (jb.off - lo));
+      a.jobs[p].sig_off = (uint32_t)(d0 + (jb.sig_off - lo));
+    }
+  }
+}
+
 }  // namespace
+
+void launch_zc_gather(const ZcGatherArgs& a, hipStream_t s) {
+  const int64_t n = a.end - a.begin;
+  if (n <= 0) return;
+  // 2048 waves at most (~2 per SIMD): enough in flight for the link, few
+  // enough to leave the arithmetic kernels of earlier classes their slots
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(512, (n * 16 + 255) / 256));
+  hipLaunchKernelGGL(k_zc_gather, dim3(blocks), dim3(256), 0, s, a);
+}
 
 void launch_copy(const void* src, void* dst, size_t bytes, hipStream_t s) {
   if (bytes == 0) return;

@@ -31,3 +31,19 @@ void launch_plan_fill(const PlanFillArgs& a, hipStream_t s);
 // reads / writes, not through the DMA engines (whose command queue stalled
 // the host for ~1 ms every few chunks, profiles/r02_pipe_*).
 void launch_copy(const void* src, void* dst, size_t bytes, hipStream_t s);
+
+// Zero-copy plans (jg_runtime.cpp, jg_set_zero_copy): copy the token bytes of
+// the jobs of one class range [begin, end) from the caller's pinned arena --
+// read over PCIe -- into the plan's device arena, key by key at a fixed
+// stride per key, and point each job at its copy.  The prep kernels then read
+// HBM as in every other path.
+struct ZcGatherArgs {
+  const uint8_t* src;               // device view of the pinned arena at the plan's base offset
+  jgk::JobDev* jobs;                // padded jobs: offsets into src in, into dst out
+  int64_t begin, end;               // padded class range
+  const uint64_t* kbase;            // per key: byte offset of its region in dst
+  const int64_t* kstart;            // per key: first padded slot of its run
+  const uint64_t* kstride;          // per key: bytes per slot (a multiple of 16)
+  uint8_t* dst;
+};
+void launch_zc_gather(const ZcGatherArgs& a, hipStream_t s);

@@ -23,7 +23,11 @@ struct EcArgs {
   int64_t npad, begin, end;
   int32_t wq;                 // comb width of the launch's key tables (every key of [begin, end) has it)
   int32_t exc_reset;          // zero *exc_count first (the class's first launch)
+  // which kernels launch_ec enqueues: EC_ALL (scalar, point, exact), EC_FAST
+  // (scalar, point) or EC_EXACT (exact alone, later, on another stream)
+  int32_t part;
 };
+enum : int32_t { EC_ALL = 0, EC_FAST = 1, EC_EXACT = 2 };
 
 // table geometry per curve: words per entry (x,y Montgomery limbs, 16-B aligned)
 constexpr int ec_limbs(int cls) { return cls == jgk::CLS_P256 ? 10 : cls == jgk::CLS_P384 ? 15 : 20; }

@@ -785,6 +785,11 @@ template <class CV>
 void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   dim3 g((unsigned)waves), b(WAVE);
+  if (a.part == EC_EXACT) {
+    hipLaunchKernelGGL(k_ec_exact<CV>, dim3(64), b, 0, s, a);
+    mk("exact");
+    return;
+  }
   if (a.exc_reset) (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
   // tokens per thread for the batched inversion: keep >= ~8 waves per CU
   // (CAPJWT_EC_WAVES_PER_CU: A/B of that target)
@@ -801,6 +806,7 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   mk("scalar");
   hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
   mk("point");
+  if (a.part == EC_FAST) return;
   hipLaunchKernelGGL(k_ec_exact<CV>, dim3(64), b, 0, s, a);
   mk("exact");
 }

@@ -73,7 +73,7 @@ struct WinRegs { uint32_t v[33]; };
 // Without prefetch: every lane names its window start `w`, the wave copies
 // dwords [w, w+33) of all 64 windows into the slots (loads and LDS stores
 // interleaved, few live registers).
-__device__ __forceinline__ void stage(uint32_t* slots, uint64_t* wsh, const uint32_t* arena_w, uint64_t w) {
+__device__ __forceinline__ void stage(uint32_t* slots, uint32_t* wsh, const uint32_t* arena_w, uint32_t w) {
   const int lane = threadIdx.x;
   wsh[lane] = w;
   __syncthreads();
@@ -87,17 +87,17 @@ __device__ __forceinline__ void stage(uint32_t* slots, uint64_t* wsh, const uint
   __syncthreads();
 }
 
-__device__ __forceinline__ void fetch(WinRegs& r, const int64_t* base, const int32_t* nw, const uint32_t* arena_w,
+__device__ __forceinline__ void fetch(WinRegs& r, const uint32_t* base, const int32_t* nw, const uint32_t* arena_w,
                                       uint32_t c, uint32_t skip) {
   const int lane = threadIdx.x;
   const int half = lane >> 5, k = lane & 31;
-  const int32_t woff = (int32_t)(WIN * c - (c ? skip : 0u));
+  const uint32_t woff = WIN * c - (c ? skip : 0u);
 #pragma unroll
   for (int i = 0; i < 32; ++i) {
     const int tt = 2 * i + half;
-    r.v[i] = arena_w[base[tt] + ((int32_t)c < nw[tt] ? woff : 0) + k];
+    r.v[i] = arena_w[base[tt] + ((int32_t)c < nw[tt] ? woff : 0u) + (uint32_t)k];
   }
-  r.v[32] = arena_w[base[lane] + ((int32_t)c < nw[lane] ? woff : 0) + 32];
+  r.v[32] = arena_w[base[lane] + ((int32_t)c < nw[lane] ? woff : 0u) + 32u];
 }
 
 __device__ __forceinline__ void put(uint32_t* slots, const WinRegs& r) {
@@ -180,9 +180,11 @@ __global__ void __launch_bounds__(64) k_prep_mid(PrepArgs a) {
 template <int CLS, int HM>
 __device__ __forceinline__ void prep_body(const PrepArgs& a) {
   __shared__ uint32_t slots[WAVE * SLOT];
-  __shared__ int64_t sbase[WAVE], hbase[WAVE];    // window streams: signature, signing input
+  // window streams (signature, signing input): arena dword index of each
+  // lane's first window -- 32 bits (JobDev offsets are 32-bit byte offsets)
+  __shared__ uint32_t sbase[WAVE], hbase[WAVE];
   __shared__ int32_t snw[WAVE], hnw[WAVE];
-  __shared__ uint64_t wsh[WAVE];                  // stage(): this window's start per lane
+  __shared__ uint32_t wsh[WAVE];                  // stage(): this window's start per lane
   __shared__ int8_t b64tab[256];
   const int lane = threadIdx.x;
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + lane;
@@ -269,9 +271,9 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a) {
     nwin = hb == 256 ? (nblk + 1) / 2 : nblk;
   }
   // both window streams, for fetch(): every lane's base and window count
-  sbase[lane] = span ? (int64_t)sw0 : 0;
+  sbase[lane] = span ? (uint32_t)sw0 : 0u;
   snw[lane] = (int32_t)((span + 4 * WIN - 1) / (4 * WIN));
-  hbase[lane] = valid ? (int64_t)(jb.off >> 2) : 0;
+  hbase[lane] = valid ? (jb.off >> 2) : 0u;
   hnw[lane] = (int32_t)nwin;
   constexpr uint32_t HSKIP = CLS == CLS_ED25519 ? 16u : 0u;    // window c >= 1 starts at message word 32c - 16
   // Prefetch one window ahead where it measured faster (RSA: 3+ signature
@@ -290,7 +292,7 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a) {
   for (uint32_t c = 0;; ++c) {
     const bool need = !bad && span > 4u * WIN * c;
     if (__ballot(need) == 0ull) break;
-    if constexpr (!PF) stage(slots, wsh, arena_w, need ? sw0 + (uint64_t)WIN * c : (uint64_t)sbase[lane]);
+    if constexpr (!PF) stage(slots, wsh, arena_w, need ? (uint32_t)sw0 + WIN * c : sbase[lane]);
     else put(slots, wr);
     if (PF && __ballot(span > 4u * WIN * (c + 1)) != 0ull) fetch(wr, sbase, snw, arena_w, c + 1, 0);
     if (!need) continue;
@@ -405,7 +407,7 @@ __device__ __forceinline__ void prep_body(const PrepArgs& a) {
     const bool need = c < nwin;
     if (__ballot(need) == 0ull) break;
     const uint32_t i0 = hb == 256 ? 32u * c : (c == 0 ? 0u : 32u * c - pw);   // message word at window dword 0
-    if constexpr (!PF) stage(slots, wsh, arena_w, (uint64_t)hbase[lane] + (need ? i0 : 0u));
+    if constexpr (!PF) stage(slots, wsh, arena_w, hbase[lane] + (need ? i0 : 0u));
     else put(slots, wr);
     if (PF && __ballot(c + 1 < nwin) != 0ull) fetch(wr, hbase, hnw, arena_w, c + 1, HSKIP);
     if (!need) continue;

@@ -660,7 +660,9 @@ void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const Marker& mk) {
   dim3 g((unsigned)waves), b(WAVE);
   switch (cls) {
     case CLS_RSA2K: hipLaunchKernelGGL((k_rsa_modexp<RSA2K_H, RSA2K_G, 8>), dim3((unsigned)(waves * RSA2K_G)), b, 0, s, a); break;
-    case CLS_RSA3K: hipLaunchKernelGGL((k_rsa_modexp<28, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a); break;
+    case CLS_RSA3K:
+      hipLaunchKernelGGL((k_rsa_modexp<RSA3K_H, RSA3K_G, RSA3K_U>), dim3((unsigned)(waves * RSA3K_G)), b, 0, s, a);
+      break;
     case CLS_RSA4K:
       if (a.layouts & 1) hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 4, 8>), dim3((unsigned)(waves * 4)), b, 0, s, a);
       if (a.layouts & 2) hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 8, 8>), dim3((unsigned)(waves * 8)), b, 0, s, a);

@@ -30,6 +30,24 @@ struct RsaArgs {
 #endif
 constexpr int RSA2K_G = JG_RSA2K_G;
 constexpr int RSA2K_H = RSA2K_G == 2 ? 37 : 19;
+// RSA-3072 layout (112 limbs): JG_RSA3K_G lanes per token, 112 / G limbs per
+// lane, JG_RSA3K_U CIOS rows per unrolled block (compile-time A/B knobs).
+// Two lanes of 56 limbs (round 4) against four of 28: the class's modexp
+// 16.2 -> 14.8 ns per token alone (tools/class_costs.py), 1.97 -> 1.81 ms in
+// configs[4] (profiles/r04_s3/rsa3k_*), although the 56-limb accumulator
+// windows spill ~140 VGPRs at two waves per SIMD -- the 4-lane rows pay more
+// in cross-lane broadcasts and limb hand-offs per MAD than the spills cost.
+// U (4 / 8 / 14 / 16) measured within 1.5 %.
+#ifndef JG_RSA3K_G
+#define JG_RSA3K_G 2
+#endif
+#ifndef JG_RSA3K_U
+#define JG_RSA3K_U 8
+#endif
+constexpr int RSA3K_G = JG_RSA3K_G;
+constexpr int RSA3K_H = 112 / RSA3K_G;
+constexpr int RSA3K_U = JG_RSA3K_U;
+static_assert(RSA3K_G * RSA3K_H == 112, "RSA-3K layouts hold 112 limbs");
 // limbs of the class's (smallest) layout: 74 / 112 / 148
 constexpr int rsa_limbs(int cls) {
   return cls == jgk::CLS_RSA2K ? RSA2K_G * RSA2K_H : cls == jgk::CLS_RSA3K ? 112 : 148;

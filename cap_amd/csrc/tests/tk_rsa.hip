@@ -85,7 +85,7 @@ extern "C" int tk_rsa_modexp(int cls, const uint32_t* n_le, int n_words, uint64_
     const unsigned waves = (unsigned)(np / WAVE);
     switch (cls) {   // the launch shapes of launch_rsa, without the padding check
       case CLS_RSA2K: hipLaunchKernelGGL((k_rsa_modexp<RSA2K_H, RSA2K_G, 8>), dim3(waves * RSA2K_G), dim3(WAVE), 0, 0, a); break;
-      case CLS_RSA3K: hipLaunchKernelGGL((k_rsa_modexp<28, 4, 8>), dim3(waves * 4), dim3(WAVE), 0, 0, a); break;
+      case CLS_RSA3K: hipLaunchKernelGGL((k_rsa_modexp<RSA3K_H, RSA3K_G, RSA3K_U>), dim3(waves * RSA3K_G), dim3(WAVE), 0, 0, a); break;
       default:
         if (L == rsa4k_layout_limbs(0)) hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 4, 8>), dim3(waves * 4), dim3(WAVE), 0, 0, a);
         else if (L == rsa4k_layout_limbs(1)) hipLaunchKernelGGL((k_rsa_modexp<RSA4K_H, 8, 8>), dim3(waves * 8), dim3(WAVE), 0, 0, a);

@@ -142,7 +142,12 @@ int jg_debug_table_digest(jg_ctx* ctx, int key, uint64_t* digest);
 /* Verify ntok jobs, blocking (= jg_submit + jg_wait).  Host buffers; copied to
  * the device(s) in chunks whose H2D copies overlap the kernels of the previous
  * chunk (direct DMA when `arena` is pinned -- jg_host_alloc -- else through
- * pinned staging).  Returns 0 on success, -1 on bad arguments (a key_idx
+ * pinned staging).  A batch whose jobs span two or more kernel classes (e.g.
+ * RSA and ECDSA keys) and whose arena (16-byte aligned) lies in one
+ * jg_host_alloc block is not DMAed: it runs as one class-major plan, each
+ * class's token bytes gathered from the pinned arena over PCIe by a kernel,
+ * costliest class first, while earlier classes compute -- when zero-copy
+ * plans are on (jg_set_zero_copy; off by default, CAPJWT_ZC=1).  Returns 0 on success, -1 on bad arguments (a key_idx
  * outside the loaded table, a signing-input or signature span past
  * arena_len), -2 on an infrastructure error (see jg_last_error); per-token
  * outcomes are only in verdict_out[i] (JG_ACCEPT / JG_REJECT).  ntok == 0
@@ -173,6 +178,13 @@ int jg_wait(jg_ctx* ctx, jg_ticket* ticket);
  * CAPJWT_CHUNK; >= 64).  Applies to later submissions.  Returns 0 or -1. */
 int jg_set_chunk(jg_ctx* ctx, size_t jobs);
 
+/* Class-major zero-copy plans of jg_verify_batch / jg_submit (see above): on
+ * (enable != 0) or off (the default unless CAPJWT_ZC=1), and the jobs per plan
+ * (max_jobs >= 64; 0 keeps the current value; default 2M or CAPJWT_ZC_MAX) --
+ * a longer submission runs as equal plans of at most that many jobs.  Applies
+ * to later submissions.  Returns 0 or -1. */
+int jg_set_zero_copy(jg_ctx* ctx, int enable, size_t max_jobs);
+
 /* HBM (bytes per device, one total over all curves) the context may spend on
  * the comb tables of its EC and Ed25519 keys (default 32 GiB, or
  * CAPJWT_TABLE_BUDGET_GB).  The next jg_keys_load first gives every key its
@@ -194,7 +206,9 @@ int jg_set_table_budget(jg_ctx* ctx, uint64_t bytes);
 
 const char* jg_last_error(jg_ctx* ctx);
 
-/* Pinned host memory for arenas / job arrays (hipHostMalloc). */
+/* Pinned host memory for arenas / job arrays (hipHostMalloc).  The block
+ * carries 256 readable bytes past `bytes`, so kernels may read an arena in it
+ * in place (jg_verify_batch's zero-copy plans). */
 void* jg_host_alloc(size_t bytes);
 void jg_host_free(void* p);
 

@@ -174,3 +174,83 @@ def test_multi_device_split_on_two_slots():
     out = ctx.verify(arena2)
     assert [0 if s is None else out[s] for s in slots] == [t["verdict"] for t in toks]
     ctx.close()
+
+
+def _pinned_copy(arena, tail=0):
+    """The arena's bytes in a PinnedBuffer sized exactly to them (+ `tail`
+    spare bytes), so the last token ends at the block's end."""
+    from cap_amd import _lib
+    pa = _lib.PinnedBuffer(len(arena.buf) + tail)
+    ctypes.memmove(pa.ptr, bytes(arena.buf), len(arena.buf))
+    return pa
+
+
+def test_zero_copy_class_major_plans():
+    """Mixed batches from jg_host_alloc memory run as class-major zero-copy
+    plans (prep kernels read the pinned arena over PCIe; jg_set_zero_copy):
+    verdicts equal the oracle's and the chunked DMA path's -- whole-item plans,
+    items cut into several plans, several submissions in flight across both
+    zero-copy slots, the last token ending exactly at the block's end, and a
+    two-slot context whose items each read their own share in place."""
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    arena, want = _mixed_arena(keys, toks, reps=2)
+    L = _lib.lib()
+    n = len(arena.toks)
+    ta = arena.tok_array()
+    for slots in ([0], [0, 0]):
+        ctx = _lib.Context(slots)
+        ctx.load_keys([H.abi_key(k) for k in keys])
+        pa = _pinned_copy(arena)
+        for zc, zmax in ((False, 0), (True, 1 << 21), (True, 640), (True, 64)):
+            ctx.set_zero_copy(zc, zmax)
+            out = (ctypes.c_uint8 * n)()
+            assert L.jg_verify_batch(ctx.h, pa.ptr, len(arena.buf), ta, n, out) == 0
+            assert list(out) == want, (slots, zc, zmax)
+        # overlapping submissions (more than the two zero-copy slots in flight)
+        ctx.set_zero_copy(True, 1000)
+        outs, tickets = [], []
+        for _ in range(5):
+            o = (ctypes.c_uint8 * n)()
+            t = ctypes.c_void_p()
+            assert L.jg_submit(ctx.h, pa.ptr, len(arena.buf), ta, n, o, ctypes.byref(t)) == 0
+            outs.append(o)
+            tickets.append(t)
+        for t, o in zip(tickets, outs):
+            assert L.jg_wait(ctx.h, t) == 0
+            assert list(o) == want
+        pa.free()
+        with pytest.raises(_lib.JgError):
+            ctx.set_zero_copy(True, 8)
+        ctx.close()
+
+
+def test_zero_copy_only_inside_host_alloc_blocks():
+    """An arena that is pinned but reaches past its jg_host_alloc block's
+    usable bytes, or sits in pageable memory, takes the chunked path: the
+    verdicts are the same either way (the prep kernels never read outside
+    the caller's block plus its slack)."""
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    arena, want = _mixed_arena(keys, toks)
+    L = _lib.lib()
+    n = len(arena.toks)
+    ctx = _lib.Context()
+    ctx.load_keys([H.abi_key(k) for k in keys])
+    ctx.set_zero_copy(True, 0)
+    # arena at an offset inside a larger block, ending 1 byte before its end
+    big = _lib.PinnedBuffer(len(arena.buf) + 4097)
+    ctypes.memmove(big.ptr + 4096, bytes(arena.buf), len(arena.buf))
+    ta = arena.tok_array()
+    out = (ctypes.c_uint8 * n)()
+    assert L.jg_verify_batch(ctx.h, big.ptr + 4096, len(arena.buf), ta, n, out) == 0
+    assert list(out) == want
+    # arena_len claims one byte past the block (not eligible; the spans are in bounds)
+    out2 = (ctypes.c_uint8 * n)()
+    assert L.jg_verify_batch(ctx.h, big.ptr + 4096, len(arena.buf) + 2, ta, n, out2) == 0
+    assert list(out2) == want
+    big.free()
+    out3 = (ctypes.c_uint8 * n)()
+    assert L.jg_verify_batch(ctx.h, bytes(arena.buf), len(arena.buf), ta, n, out3) == 0
+    assert list(out3) == want
+    ctx.close()

@@ -2,7 +2,9 @@
 Ed25519 tokens, 5 % tampered, the 32 bench kids under bench.py's C5 table
 budget), timed over several passes per chunk size: the A/B harness of the
 pipeline's chunk scheduling (run once per CAPJWT_* setting).
-usage: python tools/c5_stream_probe.py out.json [passes] [chunk ...]"""
+usage: python tools/c5_stream_probe.py out.json [passes] [mode ...]
+mode: a chunk size (chunked DMA pipeline, zero-copy plans off), or zN:
+zero-copy class-major plans of at most N jobs (z0: the library default)"""
 import ctypes
 import json
 import os
@@ -19,7 +21,7 @@ import bench  # noqa: E402
 def main():
     out = sys.argv[1]
     passes = int(sys.argv[2]) if len(sys.argv) > 2 else 6
-    chunks = [int(c) for c in sys.argv[3:]] or [262144, 524288]
+    chunks = sys.argv[3:] or ["524288", "z0"]
     from cap_amd import _lib
     cpu = bench.cpu_info()
     ctx = _lib.Context([0])
@@ -36,7 +38,11 @@ def main():
     vout = (ctypes.c_uint8 * len(toks))()
     tp = toks.ctypes.data_as(ctypes.POINTER(_lib.JgTok))
     for ch in chunks:
-        ctx.set_chunk(ch)
+        if ch.startswith("z"):
+            ctx.set_zero_copy(True, int(ch[1:]))
+        else:
+            ctx.set_zero_copy(False)
+            ctx.set_chunk(int(ch))
         ms = []
         for _ in range(passes + 1):
             t0 = time.perf_counter()
@@ -44,7 +50,7 @@ def main():
                 raise RuntimeError(ctx.error())
             ms.append((time.perf_counter() - t0) * 1e3)
         acc = int(np.frombuffer(vout, dtype=np.uint8).sum())
-        res["ms"][str(ch)] = ms[1:]
+        res["ms"][ch] = ms[1:]
         print(ch, "accepted", acc, "ms", [round(x, 1) for x in ms], "best M/s", round(len(toks) / min(ms[1:]) / 1e3, 1),
               flush=True)
         if acc != res["expected_accepted"]:

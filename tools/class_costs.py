@@ -6,7 +6,7 @@ enough to fill the chip; the cost is the summed kernel time of its chain
 above 4096 bits (no private keys here) use tokens with random signature
 values < n: the modexp and pad run in full and reject, which costs the same.
 
-usage: python tools/class_costs.py out.json"""
+usage: python tools/class_costs.py out.json [label,label,...]"""
 import json
 import os
 import sys
@@ -45,13 +45,15 @@ def big_rsa_tokens(kid, count, template):
     return key, out
 
 
-def main(dst):
+def main(dst, only=None):
     from cap_amd import _lib
     th = bench.cpu_info()["cores_used"]
     ctx = _lib.Context([0])
     res = {}
     template = bench.gen_tokens("RS256", 1, bench.golden_keypaths(["rsa2048-a"]), 1, "cc")[0]
     for label, alg, kid, ntok in CASES:
+        if only and label not in only and label != "p256":
+            continue
         if kid.startswith("big-"):
             key, pool = big_rsa_tokens(kid, min(ntok, 4096), template)
             ctx.load_keys([key])
@@ -73,4 +75,5 @@ def main(dst):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "class_costs.json")
+    main(sys.argv[1] if len(sys.argv) > 1 else "class_costs.json",
+         sys.argv[2].split(",") if len(sys.argv) > 2 else None)
