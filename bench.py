@@ -1151,7 +1151,7 @@ def main():
                            "roofline": {"bound": "valu", "kernel": "k_rsa_modexp<37,2,8>", "achieved": rach,
                                         "peak": MAD_PEAK_T, "unit": "TMAD/s", "frac": rach / MAD_PEAK_T,
                                         "mads_per_token": rsa_modexp_mads_per_token(74, 2),
-                                        "traffic": load_traffic("rsa2048_modexp")},
+                                        "traffic": load_traffic("rsa2048_modexp"), "trace_window": LAST_WINDOW},
                            "roofline_other": roofline_line(rkms, len(rtoks),
                                                            {"rsa2048_prep": ("hbm", prep_bytes_per_token(598, 66))})}
         if racc != len(rtoks):

@@ -69,67 +69,131 @@ __device__ __forceinline__ bool zero_limbs(const uint32_t* a) {
 }
 
 // ------------------------------------------------------------------ scalar
-// Per-token checks and inputs of the scalar stage.  Returns ok; r, s, e as
+// Per-token inputs of the scalar stage, in two halves so the batched kernel
+// can issue one token's loads while it computes the previous one:
+// ec_scalar_load reads the raw words (job, status, key validity, r / s words,
+// digest words), ec_scalar_finish checks them and returns ok with r, s, e as
 // plain 28-bit limbs (s replaced by 1 when the token is rejected, so the batch
 // product stays invertible).
 template <class CV>
-__device__ __forceinline__ bool ec_scalar_inputs(const EcArgs& a, int64_t p, uint32_t* r, uint32_t* s, uint32_t* e) {
+struct ScalarRaw {
+  static constexpr int CW = ec_sig_words(CV::CLS);
+  static constexpr int EW = (CV::C::BYTES + 3) / 4 < 16 ? (CV::C::BYTES + 3) / 4 : 16;   // digest words used
+  JobDev jb;
+  uint32_t ok;                // status OK and the key valid
+  uint32_t rw[CW], sw[CW];
+  uint32_t ew[EW];            // e as little-endian words (digest words reversed), zero past the hash
+};
+
+template <class CV>
+__device__ __forceinline__ int ec_hash_words(int alg) {
+  constexpr int CB = CV::C::BYTES;
+  return (es_hash_bytes(alg) < CB ? es_hash_bytes(alg) : CB) / 4;   // hl / 4 (hl a multiple of 4)
+}
+
+template <class CV>
+__device__ __forceinline__ void ec_scalar_load(const EcArgs& a, int64_t p, ScalarRaw<CV>& R) {
+  constexpr int CW = ScalarRaw<CV>::CW, EW = ScalarRaw<CV>::EW;
+  const int64_t np = a.npad;
+  R.jb = a.jobs[p];
+  if (!job_live(R.jb)) return;
+  const int kidx = job_key(R.jb);
+  const int hw = ec_hash_words<CV>(job_alg(R.jb));
+  R.ok = a.status[p] == ST_OK && a.keys[kidx].valid;
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    R.rw[q] = a.sigw[(int64_t)q * np + p];
+    R.sw[q] = a.sigw[(int64_t)(EC_S_ROW + q) * np + p];
+  }
+#pragma unroll
+  for (int q = 0; q < EW; ++q) {
+    const int src = hw - 1 - q;
+    R.ew[q] = src >= 0 ? a.dig[(int64_t)(src < 0 ? 0 : src) * np + p] : 0u;
+  }
+}
+
+template <class CV>
+__device__ __forceinline__ bool ec_scalar_finish(const EcArgs& a, int64_t p, const ScalarRaw<CV>& R, uint32_t* r,
+                                                 uint32_t* s, uint32_t* e) {
   using Fn = typename CV::Fn;
   constexpr int L = Fn::L;
   constexpr int CB = CV::C::BYTES;
+  constexpr int CW = ScalarRaw<CV>::CW, EW = ScalarRaw<CV>::EW;
   const int64_t np = a.npad;
-  const JobDev jb = a.jobs[p];
-  if (!job_live(jb)) {
+  if (!job_live(R.jb)) {
 #pragma unroll
     for (int j = 0; j < L; ++j) { r[j] = 0; e[j] = 0; s[j] = j == 0 ? 1u : 0u; }
     return false;
   }
-  const int kidx = job_key(jb);
-  const int alg = job_alg(jb);
+  const int alg = job_alg(R.jb);
   // R18/R21: the signature size comes from the alg, the curve from the key
   // (go-jose ecEncrypterVerifier: keySize by alg, no curve check), so r and s
   // are es_size(alg)-byte integers that must be < n of the key's curve.  Prep
   // leaves them in rows [0, ..) and [EC_S_ROW, ..), zero above what it wrote
   // up to this curve's CW words; an alg whose r/s are longer than the curve's
   // (ES512 on a P-256 key) must have zero words past CB as well.
-  bool ok = a.status[p] == ST_OK && a.keys[kidx].valid;
-  constexpr int CW = ec_sig_words(CV::CLS);
-  uint32_t rw[CW], sw[CW];
-#pragma unroll
-  for (int q = 0; q < CW; ++q) {
-    rw[q] = a.sigw[(int64_t)q * np + p];
-    sw[q] = a.sigw[(int64_t)(EC_S_ROW + q) * np + p];
-  }
+  bool ok = R.ok != 0;
   if constexpr (4 * CW > CB) {
     const uint32_t hi = ~0u << (8 * (CB - 4 * (CW - 1)));
-    ok = ok && (rw[CW - 1] & hi) == 0 && (sw[CW - 1] & hi) == 0;
+    ok = ok && (R.rw[CW - 1] & hi) == 0 && (R.sw[CW - 1] & hi) == 0;
   }
   if (es_size(alg) > CB) {
     const int aw = (es_size(alg) + 3) / 4;      // words prep wrote for this alg
     for (int q = CW; q < aw; ++q)
       ok = ok && a.sigw[(int64_t)q * np + p] == 0 && a.sigw[(int64_t)(EC_S_ROW + q) * np + p] == 0;
   }
-  mp::words_to_limbs<L, CW>(r, rw);
-  mp::words_to_limbs<L, CW>(s, sw);
+  mp::words_to_limbs<L, CW>(r, R.rw);
+  mp::words_to_limbs<L, CW>(s, R.sw);
   uint32_t nl[L];
   mp::set_const<Fn>(nl, Fn::M);
   ok = ok && !zero_limbs<L>(r) && !zero_limbs<L>(s) && lt_limbs<L>(r, nl) && lt_limbs<L>(s, nl);
-  {
-    const int hl = es_hash_bytes(alg) < CB ? es_hash_bytes(alg) : CB;   // multiple of 4
-    uint32_t ew[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int src = hl / 4 - 1 - q;
-      ew[q] = src >= 0 ? a.dig[(int64_t)(src < 0 ? 0 : src) * np + p] : 0u;
-    }
-    mp::words_to_limbs<L, 16>(e, ew);
-    mp::csub<Fn>(e);
-  }
+  mp::words_to_limbs<L, EW>(e, R.ew);
+  mp::csub<Fn>(e);
   if (!ok) {
 #pragma unroll
     for (int j = 0; j < L; ++j) s[j] = j == 0 ? 1u : 0u;
   }
   return ok;
+}
+
+template <class CV>
+__device__ __forceinline__ bool ec_scalar_inputs(const EcArgs& a, int64_t p, uint32_t* r, uint32_t* s, uint32_t* e) {
+  ScalarRaw<CV> R;
+  ec_scalar_load<CV>(a, p, R);
+  return ec_scalar_finish<CV>(a, p, R, r, s, e);
+}
+
+// Pass 2 of the batched scalar stage (the checks are done): the prefix product
+// c_{j-1}, s_j (Montgomery) and the raw r / e words of token j, loaded one
+// token ahead like pass 1's inputs.
+template <class CV>
+struct ScalarRaw2 {
+  static constexpr int L = CV::Fn::L;
+  uint32_t cprev[L], sm[L];
+  uint32_t rw[ScalarRaw<CV>::CW], ew[ScalarRaw<CV>::EW];
+};
+
+template <class CV>
+__device__ __forceinline__ void ec_scalar_load2(const EcArgs& a, int64_t p, int64_t pprev, ScalarRaw2<CV>& R) {
+  using Fn = typename CV::Fn;
+  constexpr int L = Fn::L, CW = ScalarRaw<CV>::CW, EW = ScalarRaw<CV>::EW;
+  const int64_t np = a.npad;
+  if (pprev >= 0) {
+#pragma unroll
+    for (int k = 0; k < L; ++k) R.cprev[k] = a.u1w[(int64_t)k * np + pprev];
+  } else {
+    mp::set_const<Fn>(R.cprev, Fn::ONE);
+  }
+#pragma unroll
+  for (int k = 0; k < L; ++k) R.sm[k] = a.u2w[(int64_t)k * np + p];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) R.rw[q] = a.sigw[(int64_t)q * np + p];
+  const int hw = ec_hash_words<CV>(job_alg(a.jobs[p]));
+#pragma unroll
+  for (int q = 0; q < EW; ++q) {
+    const int src = hw - 1 - q;
+    R.ew[q] = src >= 0 ? a.dig[(int64_t)(src < 0 ? 0 : src) * np + p] : 0u;
+  }
 }
 
 // r and e of a token that passed ec_scalar_inputs (pass 2 of the batched
@@ -138,22 +202,10 @@ template <class CV>
 __device__ __forceinline__ void ec_scalar_re(const EcArgs& a, int64_t p, uint32_t* r, uint32_t* e) {
   using Fn = typename CV::Fn;
   constexpr int L = Fn::L;
-  constexpr int CB = CV::C::BYTES;
-  constexpr int CW = ec_sig_words(CV::CLS);
-  const int64_t np = a.npad;
-  uint32_t rw[CW];
-#pragma unroll
-  for (int q = 0; q < CW; ++q) rw[q] = a.sigw[(int64_t)q * np + p];
-  mp::words_to_limbs<L, CW>(r, rw);
-  const int alg = job_alg(a.jobs[p]);
-  const int hl = es_hash_bytes(alg) < CB ? es_hash_bytes(alg) : CB;
-  uint32_t ew[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int src = hl / 4 - 1 - q;
-    ew[q] = src >= 0 ? a.dig[(int64_t)(src < 0 ? 0 : src) * np + p] : 0u;
-  }
-  mp::words_to_limbs<L, 16>(e, ew);
+  ScalarRaw2<CV> R;
+  ec_scalar_load2<CV>(a, p, -1, R);
+  mp::words_to_limbs<L, ScalarRaw<CV>::CW>(r, R.rw);
+  mp::words_to_limbs<L, ScalarRaw<CV>::EW>(e, R.ew);
   mp::csub<Fn>(e);
 }
 
@@ -188,6 +240,13 @@ __device__ __forceinline__ void store_digit_rows(const EcArgs& a, int64_t p, con
 #ifndef JG_EC_SCALAR_WPB
 #define JG_EC_SCALAR_WPB 4
 #endif
+// JG_EC_SCALAR_PF=1: both passes load the next token's words before computing
+// the current one.  Measured no faster for P-256 (0.189-0.190 vs 0.192 ms per
+// 1 M, profiles/r04_s4/scalar_pf_ab.json) and it costs registers (P-256 138 ->
+// 203 VGPRs, P-384 past 256, P-521 spills), so it is off (A/B knob).
+#ifndef JG_EC_SCALAR_PF
+#define JG_EC_SCALAR_PF 0
+#endif
 constexpr int EC_SCALAR_WPB = JG_EC_SCALAR_WPB;
 template <class CV>
 // JG_EC_SCALAR_ATTR: per translation unit.  ecdsa_p521.hip caps the kernel at
@@ -210,6 +269,59 @@ __global__ void __launch_bounds__(64 * EC_SCALAR_WPB) JG_EC_SCALAR_ATTR k_ec_sca
   uint32_t acc[L];
   mp::set_const<Fn>(acc, Fn::ONE);
   int nb = 0;
+  constexpr int WG = ec_comb_w(CV::CLS, true), NG = ec_windows(CV::CLS, true);
+  constexpr int WQ = CV::WQ, NQ = ec_windows_w(CV::CLS, CV::WQ);
+#if JG_EC_SCALAR_PF
+  // Both passes load token j+1's (pass 2: j-1's) words before computing token j.
+  {
+    ScalarRaw<CV> cur, nxt;
+    int64_t p = a.begin + i;
+    bool have = B > 0 && i < S && p < a.end;
+    if (have) ec_scalar_load<CV>(a, p, cur);
+    for (int j = 0; have; ++j) {
+      const int64_t pn = p + S;
+      const bool more = j + 1 < B && pn < a.end;
+      if (more) ec_scalar_load<CV>(a, pn, nxt);
+      uint32_t r[L], s[L], e[L], sm[L];
+      const bool ok = ec_scalar_finish<CV>(a, p, cur, r, s, e);
+      if (!ok && job_live(cur.jb)) a.status[p] = ST_REJECT;
+      mp::to_mont<Fn>(sm, s);
+      mp::mul<Fn>(acc, acc, sm);
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+        a.u1w[(int64_t)k * np + p] = acc[k];
+        a.u2w[(int64_t)k * np + p] = sm[k];
+      }
+      ++nb;
+      if (!more) break;
+      cur = nxt;
+      p = pn;
+    }
+  }
+  uint32_t inv[L];
+  mp::block_inv<Fn, EC_SCALAR_WPB>(inv, acc);
+  if (nb > 0) {
+    ScalarRaw2<CV> cur, nxt;
+    int64_t p = a.begin + i + (int64_t)(nb - 1) * S;
+    ec_scalar_load2<CV>(a, p, nb > 1 ? p - S : -1, cur);
+    for (int j = nb - 1; j >= 0; --j) {
+      if (j > 0) ec_scalar_load2<CV>(a, p - S, j > 1 ? p - 2 * S : -1, nxt);
+      uint32_t w[L], r[L], e[L], u1[L], u2[L];
+      mp::mul<Fn>(w, inv, cur.cprev);              // s_j^-1 R
+      mp::mul<Fn>(inv, inv, cur.sm);
+      mp::words_to_limbs<L, ScalarRaw<CV>::CW>(r, cur.rw);
+      mp::words_to_limbs<L, ScalarRaw<CV>::EW>(e, cur.ew);
+      mp::csub<Fn>(e);
+      mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
+      mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
+      store_digit_rows<CV, WG, NG>(a, p, u1, 0);  // (the rare exact path recomputes u1, u2 itself)
+      store_digit_rows<CV, WQ, NQ>(a, p, u2, NG);
+      if (j == 0) break;
+      cur = nxt;
+      p -= S;
+    }
+  }
+#else
   for (int j = 0; j < B && i < S; ++j) {
     const int64_t p = a.begin + i + (int64_t)j * S;
     if (p >= a.end) break;
@@ -243,13 +355,12 @@ __global__ void __launch_bounds__(64 * EC_SCALAR_WPB) JG_EC_SCALAR_ATTR k_ec_sca
     mp::mul<Fn>(inv, inv, sm);
     uint32_t r[L], e[L], u1[L], u2[L];
     ec_scalar_re<CV>(a, p, r, e);
-    constexpr int WG = ec_comb_w(CV::CLS, true), NG = ec_windows(CV::CLS, true);
-    constexpr int WQ = CV::WQ, NQ = ec_windows_w(CV::CLS, CV::WQ);
     mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
     mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
     store_digit_rows<CV, WG, NG>(a, p, u1, 0);  // (the rare exact path recomputes u1, u2 itself)
     store_digit_rows<CV, WQ, NQ>(a, p, u2, NG);
   }
+#endif
 }
 
 // ------------------------------------------------------------------ point ops

@@ -39,7 +39,7 @@ MARKS = {
     "ed25519_finish": ["(anonymous namespace)::k_ed_finish("],
     "p384_prep": ["void (anonymous namespace)::k_prep<4, "],
     "rsa2048_modexp": ["void (anonymous namespace)::k_rsa_modexp<37, 2, 8>"],
-    "rsa3072_modexp": ["void (anonymous namespace)::k_rsa_modexp<28, 4, 8>"],
+    "rsa3072_modexp": ["void (anonymous namespace)::k_rsa_modexp<56, 2, 8>", "void (anonymous namespace)::k_rsa_modexp<28, 4, 8>"],
     "rsa4096_modexp": ["void (anonymous namespace)::k_rsa_modexp<37, 4, 8>"],
     "rsa4096_prep": ["void (anonymous namespace)::k_prep<1, ", "(anonymous namespace)::k_prep_mid("],
     "rsa4096_pad": ["void (anonymous namespace)::k_rsa_pad<"],
