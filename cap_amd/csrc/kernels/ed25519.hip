@@ -134,8 +134,13 @@ __device__ __forceinline__ void recode(int* dg, const uint32_t* s) {
   }
 }
 
+// JG_ED_POINT_ATTR: occupancy A/B hook (the compiler's choice, ~141 VGPRs,
+// gives 3 waves per SIMD)
+#ifndef JG_ED_POINT_ATTR
+#define JG_ED_POINT_ATTR
+#endif
 template <int WA>
-__global__ void __launch_bounds__(64) k_ed_point(EdArgs a) {
+__global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
   const JobDev jb = a.jobs[p];
