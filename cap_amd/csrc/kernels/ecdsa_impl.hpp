@@ -557,6 +557,44 @@ __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z
   }
 }
 
+// Packed (P-256) entries as raw words, for the one-entry-ahead loop of
+// k_ec_point (JG_EC_POINT_PF): the loads of the next addition's entry are in
+// flight while the current addition computes.
+template <class CV>
+__device__ __forceinline__ void load_raw(const uint32_t* __restrict__ ent, uint4* r) {
+  const uint4* e4 = reinterpret_cast<const uint4*>(ent);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = e4[i];
+}
+template <class CV, bool Z1ONE = false>
+__device__ __forceinline__ void add_raw(uint32_t* X, uint32_t* Y, uint32_t* Z, bool& empty, const uint4* r, int d) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  if (d == 0) return;
+  const uint32_t wx[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
+  const uint32_t wy[8] = {r[2].x, r[2].y, r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
+  uint32_t x2[L], y2[L];
+  mp::words_to_limbs<L, 8>(x2, wx);
+  mp::words_to_limbs<L, 8>(y2, wy);
+  if (d < 0) mp::neg<Fp>(y2, y2);
+  if (empty) {
+    mp::copy<Fp>(X, x2);
+    mp::copy<Fp>(Y, y2); mp::freduce<Fp>(Y);
+    mp::set_const<Fp>(Z, Fp::ONE);
+    empty = false;
+  } else if constexpr (Z1ONE) {
+    madd_z1<Fp>(X, Y, Z, x2, y2);
+  } else {
+    madd<Fp>(X, Y, Z, x2, y2);
+  }
+}
+// JG_EC_POINT_PF=1 (P-256 at equal G / key widths): 128 VGPRs, still 4 waves
+// per SIMD, point kernel 1.282-1.288 -> 1.270-1.284 ms per 1 M tokens
+// (profiles/r04_s6/point_pf_ab.json) -- within noise, so off (A/B knob)
+#ifndef JG_EC_POINT_PF
+#define JG_EC_POINT_PF 0
+#endif
+
 // JG_EC_POINT_ATTR: per translation unit, as JG_EC_SCALAR_ATTR (occupancy A/Bs)
 #ifndef JG_EC_POINT_ATTR
 #define JG_EC_POINT_ATTR
@@ -579,12 +617,48 @@ __global__ void __launch_bounds__(64) JG_EC_POINT_ATTR k_ec_point(EcArgs a) {
 
   uint32_t X[L], Y[L], Z[L];
   bool empty = true;
+#if JG_EC_POINT_PF
+  if constexpr (ec_packed(CV::CLS) && NG == NQ) {
+    // additions k = 0 .. 2 NG - 1 alternate G window k/2 and Q window k/2;
+    // digit k+2 and entry k+1 are loaded while addition k computes
+    constexpr int NS = 2 * NG, STRIDE = ec_stride(CV::CLS);
+    constexpr int NEG = ec_entries(CV::CLS, true), NEQ = 1 << (CV::WQ - 1);
+    auto dig = [&](int k) { return (int)a.digs[(int64_t)((k & 1) ? NG + (k >> 1) : (k >> 1)) * np + p]; };
+    auto ent = [&](int k, int d) {
+      const int ad = d < 0 ? -d : d;
+      const int64_t idx = ad == 0 ? 0 : ad - 1;          // a zero digit adds nothing (its load is harmless)
+      return (k & 1) ? qtab + ((int64_t)(k >> 1) * NEQ + idx) * STRIDE : gtab + ((int64_t)(k >> 1) * NEG + idx) * STRIDE;
+    };
+    uint4 rc[4], rn[4];
+    int dc = dig(0), dn = dig(1);
+    load_raw<CV>(ent(0, dc), rc);
+    load_raw<CV>(ent(1, dn), rn);
+    int dnn = dig(2);
+    add_raw<CV>(X, Y, Z, empty, rc, dc);                 // window 0: G is an assignment,
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rc[i] = rn[i];
+    dc = dn; dn = dnn;
+    load_raw<CV>(ent(2, dn), rn);
+    dnn = dig(3);
+    add_raw<CV, true>(X, Y, Z, empty, rc, dc);           // so Q adds onto Z == 1
+    for (int k = 2; k < NS; ++k) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rc[i] = rn[i];
+      dc = dn; dn = dnn;
+      if (k + 1 < NS) load_raw<CV>(ent(k + 1, dn), rn);
+      if (k + 2 < NS) dnn = dig(k + 2);
+      add_raw<CV>(X, Y, Z, empty, rc, dc);
+    }
+  } else
+#endif
+  {
   // window 0 peeled: its G entry is an assignment, so its Q entry adds onto Z == 1
   add_window<CV, true>(X, Y, Z, empty, gtab, 0, (int)a.digs[p]);
   add_window<CV, false, true>(X, Y, Z, empty, qtab, 0, (int)a.digs[(int64_t)NG * np + p]);
   for (int w = 1; w < NWIN; ++w) {
     if (w < NG) add_window<CV, true>(X, Y, Z, empty, gtab, w, (int)a.digs[(int64_t)w * np + p]);
     if (w < NQ) add_window<CV, false>(X, Y, Z, empty, qtab, w, (int)a.digs[(int64_t)(NG + w) * np + p]);
+  }
   }
   if (empty) { a.verdict_pad[p] = 0; return; }           // R = infinity (unreachable: u2 != 0)
   uint32_t zc[L];

@@ -134,8 +134,9 @@ __device__ __forceinline__ void recode(int* dg, const uint32_t* s) {
   }
 }
 
-// JG_ED_POINT_ATTR: occupancy A/B hook (the compiler's choice, ~141 VGPRs,
-// gives 3 waves per SIMD)
+// JG_ED_POINT_ATTR: occupancy A/B hook.  The compiler's choice, ~141 VGPRs,
+// gives 3 waves per SIMD; capped at 4 waves (128 VGPRs, 14-18 spilled) the
+// Ed25519 class cost went 1.53 -> 1.59 ns per token (profiles/r04_s6/)
 #ifndef JG_ED_POINT_ATTR
 #define JG_ED_POINT_ATTR
 #endif

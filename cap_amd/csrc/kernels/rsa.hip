@@ -35,15 +35,6 @@ using namespace jgk;
 #ifndef JG_RSA_BLOCKS
 #define JG_RSA_BLOCKS 1
 #endif
-// JG_RSA_NLDS=1: the modulus limbs live in LDS (one copy per wave: every
-// token of a wave has the same key) instead of H VGPRs per lane; each CIOS
-// row reads them again -- a broadcast read, all lanes of one group lane index
-// read one address -- which frees H VGPRs (the 2-lane RSA-3K layout spills
-// ~140 without it).  nrow() re-derives the pointer per row through an opaque
-// asm so the compiler cannot hoist the reads back into registers.
-#ifndef JG_RSA_NLDS
-#define JG_RSA_NLDS 0
-#endif
 
 namespace {
 
@@ -129,13 +120,6 @@ __device__ __forceinline__ uint32_t opaque_mask(bool keep) {
   return m;
 }
 
-__device__ __forceinline__ const uint32_t* nrow(const uint32_t* n) {
-#if JG_RSA_NLDS
-  asm volatile("" : "+v"(n));
-#endif
-  return n;
-}
-
 // The limb shift that ends a CIOS row: every lane keeps T[0]'s bits above
 // 28 in its own T[1] (same weight) and hands the low 28 bits to the lane below,
 // which places them in its fresh top slot T[H] (the top lane's fresh slot is
@@ -166,7 +150,7 @@ __device__ __forceinline__ void cios_step(uint64_t* T, uint32_t ai, const uint32
 #if JG_RSA_BLOCKS
   madv_run(T, ai, v, H);
   const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
-  madv_run(T, m, nrow(n), H);
+  madv_run(T, m, n, H);
 #else
 #pragma unroll
   for (int j = 0; j < H; ++j) mad64(T[j], ai, v[j], j & 1);
@@ -275,7 +259,7 @@ __device__ __forceinline__ void mont_sqr(uint32_t* v, const uint32_t* la, const 
 #if JG_RSA_BLOCKS
       madv_run(T + x + 1, a2, v + x + 1, H - x - 1);
       const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
-      madv_run(T, m, nrow(n), H);
+      madv_run(T, m, n, H);
 #else
 #pragma unroll
       for (int k = x + 1; k < H; ++k) mad64(T[k], a2, v[k], SQR_SLOT(k));
@@ -357,17 +341,9 @@ __global__ void __launch_bounds__(64) JG_RSA_MODEXP_ATTR k_rsa_modexp(RsaArgs a)
   const uint64_t e = ((uint64_t)K.e_hi << 32) | K.e_lo;
   uint32_t* la = lds + tl;
 
-#if JG_RSA_NLDS
-  __shared__ uint32_t lds_n[L];
-  for (int j = lane; j < L; j += WAVE) lds_n[j] = N[j];
-  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
-  __builtin_amdgcn_wave_barrier();      // one wave per block: its LDS writes are visible to it
-  const uint32_t* n = lds_n + g * H;
-#else
   uint32_t n[H];
 #pragma unroll
   for (int j = 0; j < H; ++j) n[j] = N[g * H + j];
-#endif
 
   bool act = job_live(a.jobs[p]) && a.status[p] == ST_OK && a.siglen[p] == (uint16_t)K.kbytes && K.valid;
 

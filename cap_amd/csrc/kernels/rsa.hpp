@@ -37,7 +37,10 @@ constexpr int RSA2K_H = RSA2K_G == 2 ? 37 : 19;
 // configs[4] (profiles/r04_s3/rsa3k_*), although the 56-limb accumulator
 // windows spill ~140 VGPRs at two waves per SIMD -- the 4-lane rows pay more
 // in cross-lane broadcasts and limb hand-offs per MAD than the spills cost.
-// U (4 / 8 / 14 / 16) measured within 1.5 %.
+// U (4 / 8 / 14 / 16) measured within 1.5 %.  Keeping the modulus limbs in
+// LDS instead of VGPRs (re-read every CIOS row, a broadcast read) freed 20-30
+// VGPRs per layout but made every modexp 2-6x slower
+// (profiles/r04_s6/class_costs_nlds*.json): not kept.
 #ifndef JG_RSA3K_G
 #define JG_RSA3K_G 2
 #endif
