@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 
 #include "batch.hpp"
 #include "common.hpp"
@@ -55,6 +57,63 @@ __global__ void __launch_bounds__(256) k_plan_fill(PlanFillArgs a) {
     a.jobs[p] = JobDev{0, 0, 0, job_pack(b == a.nkeys ? 0u : (uint32_t)b, JOB_PAD, 0)};
     a.perm[p] = -1;
   }
+}
+
+// Two-level form for chunks of many jobs over few buckets (a mixed JWKS
+// stream): a block of 256 threads takes PF_ITEMS jobs per thread, counts its
+// jobs per bucket with LDS atomics, reserves each bucket's run with ONE global
+// atomic per (block, bucket), and places its jobs there.  The one-level
+// kernel above issues one global atomic per (wave, bucket) -- ~25 per wave of
+// a 32-kid mixed stream, all on the same 33 cursors: 1.2 ms per 524 k-job
+// chunk on the critical path of every chunk (profiles/r04_s3/zc_trace_*).
+constexpr int PF_THREADS = 256, PF_ITEMS = 4, PF_MAX_BUCKETS = 2048;
+__global__ void __launch_bounds__(PF_THREADS) k_plan_fill_blocked(PlanFillArgs a) {
+  __shared__ uint32_t cnt[PF_MAX_BUCKETS];
+  __shared__ unsigned long long gbase[PF_MAX_BUCKETS];
+  const int nb = a.nkeys + 1;
+  for (int b = threadIdx.x; b < nb; b += PF_THREADS) cnt[b] = 0;
+  __syncthreads();
+  const int64_t j0 = (int64_t)blockIdx.x * PF_THREADS * PF_ITEMS;
+  int bk[PF_ITEMS];
+  uint32_t loc[PF_ITEMS];
+#pragma unroll
+  for (int it = 0; it < PF_ITEMS; ++it) {
+    const int64_t j = j0 + (int64_t)it * PF_THREADS + threadIdx.x;
+    bk[it] = -1;
+    if (j < a.n) {
+      const jg_tok t = a.toks[j];
+      const int alg = t.alg;
+      const int c = alg < 16 ? a.cls_tab[(size_t)t.key_idx * 16 + alg] : 0;
+      bk[it] = c == 0 ? a.nkeys : (int)t.key_idx;
+      loc[it] = atomicAdd(&cnt[bk[it]], 1u);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += PF_THREADS)
+    if (cnt[b]) gbase[b] = atomicAdd(&a.cursor[b], (unsigned long long)cnt[b]);
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < PF_ITEMS; ++it) {
+    if (bk[it] < 0) continue;
+    const int64_t j = j0 + (int64_t)it * PF_THREADS + threadIdx.x;
+    const jg_tok t = a.toks[j];
+    const int64_t p = (int64_t)gbase[bk[it]] + loc[it];
+    const uint64_t o = t.off - a.base;
+    a.jobs[p] = JobDev{(uint32_t)o, t.sig_in_len, (uint32_t)(o + t.sig_rel_off),
+                       job_pack(bk[it] == a.nkeys ? 0u : t.key_idx, (uint32_t)t.alg, t.sig_b64_len)};
+    a.perm[p] = (int32_t)j;
+  }
+}
+
+// the padding lanes of every bucket (the second half of k_plan_fill)
+__global__ void __launch_bounds__(256) k_plan_pad(PlanFillArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = k >> 6;
+  if (b > a.nkeys) return;
+  const int64_t p = a.pad[2 * b] + (k & 63);
+  if (p >= a.pad[2 * b + 1]) return;
+  a.jobs[p] = JobDev{0, 0, 0, job_pack(b == a.nkeys ? 0u : (uint32_t)b, JOB_PAD, 0)};
+  a.perm[p] = -1;
 }
 
 __global__ void __launch_bounds__(256) k_copy16(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16,
@@ -130,6 +189,17 @@ void launch_scatter(const int32_t* perm, const uint8_t* verdict_pad, uint8_t* ve
 }
 
 void launch_plan_fill(const PlanFillArgs& a, hipStream_t s) {
+  static const bool blocked = [] {
+    const char* e = std::getenv("CAPJWT_PLAN_FILL");
+    return !(e && std::string(e) == "wave");          // A/B: the one-level kernel
+  }();
+  if (blocked && a.nkeys + 1 <= PF_MAX_BUCKETS) {
+    constexpr int64_t per = PF_THREADS * PF_ITEMS;
+    if (a.n > 0) hipLaunchKernelGGL(k_plan_fill_blocked, dim3((unsigned)((a.n + per - 1) / per)), dim3(PF_THREADS), 0, s, a);
+    const int64_t pads = (int64_t)(a.nkeys + 1) * 64;
+    hipLaunchKernelGGL(k_plan_pad, dim3((unsigned)((pads + 255) / 256)), dim3(256), 0, s, a);
+    return;
+  }
   const int64_t threads = a.n + (int64_t)(a.nkeys + 1) * 64;
   hipLaunchKernelGGL(k_plan_fill, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, a);
 }
