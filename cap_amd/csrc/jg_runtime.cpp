@@ -23,6 +23,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -786,7 +787,21 @@ int group_ctrl() {
   }();
   return m;
 }
-int cls_group(int c) { return c == CLS_RSA4K ? 1 : c <= CLS_RSA3K ? 0 : 2; }
+// Class -> group lane of a class-grouped chunk.  Default: RSA-2K and RSA-3K on
+// lane 0, RSA-4K+ on lane 1, the EC and Ed25519 classes on lane 2.
+// CAPJWT_CLASS_GROUP (A/B): one digit 0-2 per class 1..7 (RSA-2K, RSA-3K,
+// RSA-4K+, P-256, P-384, P-521, Ed25519), e.g. "0012222" (the default).
+int cls_group(int c) {
+  static const std::array<int, NCLS> g = [] {
+    std::array<int, NCLS> t{};
+    const char* d = "0012222";
+    const char* e = std::getenv("CAPJWT_CLASS_GROUP");
+    if (e && std::strlen(e) == NCLS - 1 && std::strspn(e, "012") == NCLS - 1) d = e;
+    for (int k = 1; k < NCLS; ++k) t[k] = d[k - 1] - '0';
+    return t;
+  }();
+  return g[c];
+}
 
 // two or more kernel classes among (a sample of) the jobs
 bool mixed_classes(const KeyState& K, const jg_tok* toks, size_t n) {
