@@ -563,6 +563,11 @@ struct Slot {
   int grows = 0;                                                // buffer reallocations while enqueuing (trace)
   int chunk_no = 0;
   uint64_t seq = 0;                // enqueue order across both slot rings (oldest completes first)
+  // early arena DMA (process_item): this slot's next chunk's arena span
+  // [pre_base, pre_base + pre_span) is already on its way to bufs.arena
+  bool pre = false;
+  const uint8_t* pre_src = nullptr;
+  uint64_t pre_base = 0, pre_span = 0;
   size_t reserved = 0;             // chunk capacity (jobs) the buffers were sized for
   uint64_t reserved_epoch = ~0ull; // key table they were sized against
   bool inflight = false;
@@ -1565,7 +1570,10 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   const uint8_t* hbd = (const uint8_t*)S.h_meta.dp;
   const hipStream_t cs = d->copy;
   if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
-  if (bytes && !zc) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, cs));
+  const bool pre = S.pre && compact && !zc && it.dev_arena && src == S.pre_src && dbase == S.pre_base &&
+                   bytes == S.pre_span;
+  S.pre = false;
+  if (bytes && !zc && !pre) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, cs));
   int nact = 0, jgrp = 0;
   double gcost[3] = {0, 0, 0};
   for (int c = 1; c < NCLS; ++c) {
@@ -1655,6 +1663,52 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   S.inflight = true;
 }
 
+// Early arena DMA: right after chunk c is enqueued, the compact arena span of
+// chunk c + 1 goes on the copy stream into the slot that chunk will use, so it
+// travels while the host plans chunk c + 1 (~4 ms of host work for a 524 k-job
+// chunk) and the copies of a pinned stream run back to back
+// (profiles/r04_s9/stream_trace_*).  Only for spans that enqueue_chunk would
+// DMA as they are (compact, inside the caller's arena); it checks that the
+// span it computes matches and otherwise copies as usual.  CAPJWT_EARLY_DMA=0
+// turns it off (A/B).
+bool early_dma() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_EARLY_DMA");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
+void prefetch_arena(Device* d, size_t dslot, Slot& N, const Item& it, size_t lo, size_t hi) {
+  const size_t n = hi - lo;
+  if (n == 0) return;
+  const jg_tok* toks = it.toks + lo;
+  uint64_t amin = UINT64_MAX, amax = 0, need = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t e = tok_end(toks[i]);
+    amin = std::min<uint64_t>(amin, toks[i].off);
+    amax = std::max<uint64_t>(amax, e);
+    need += e - toks[i].off;
+  }
+  if (amax > it.arena_len) return;                 // a bad job: enqueue_chunk's checks report it
+  const uint64_t base = amin & ~uint64_t(255), span = amax - base;
+  if (!(span <= 2 * need + 65536 && span < (uint64_t(1) << 32) - ARENA_SLACK)) return;
+  finish_slot(N);                                  // its previous chunk (a ring length ago)
+  const KeyState& K = *it.ks;
+  if (N.reserved != it.chunk || N.reserved_epoch != K.epoch) {
+    double bpj = 0;
+    for (size_t i = 0; i < std::min<size_t>(n, 256); ++i) bpj += (double)(tok_end(toks[i]) - toks[i].off);
+    reserve_slot(K, N, std::max(it.chunk, n), K.keys.size() + 1, bpj / (double)std::min<size_t>(n, 256), false);
+  }
+  N.bufs.arena.get((size_t)span + ARENA_SLACK);
+  HIPCHK(hipMemcpyAsync(N.bufs.arena.p, it.arena + base, (size_t)span, hipMemcpyHostToDevice, d->copy));
+  N.pre = true;
+  N.pre_src = it.arena + base;
+  N.pre_base = base;
+  N.pre_span = span;
+  (void)dslot;
+}
+
 void process_item(Device* d, size_t dslot, Item& it) {
   size_t enq = 0;
   try {
@@ -1684,6 +1738,11 @@ void process_item(Device* d, size_t dslot, Item& it) {
       finish_slot(S);                 // the slot's previous chunk (a ring length ago)
       const double wait_ms = pipe_trace() ? ms_since(tw) : 0.0;
       enqueue_chunk(d, dslot, S, it, it.toks + lo, hi - lo, it.out + lo);
+      // after chunk c's own copies (the copy stream is in order: issued before
+      // them, chunk c + 1's span delayed chunk c by a whole copy, 22.9 -> 26.4 ms
+      // per configs[4] stream, profiles/r04_s11/)
+      if (!it.zc && it.dev_arena && early_dma() && c + 2 < it.cuts.size())
+        prefetch_arena(d, dslot, d->slots[d->next_slot], it, it.cuts[c + 1], it.cuts[c + 2]);
       S.seq = ++d->slot_seq;
       S.host_ms[0] = wait_ms;
       S.chunk_no = (int)enq;
@@ -1694,6 +1753,7 @@ void process_item(Device* d, size_t dslot, Item& it) {
     it.t->fail(-2, e.what());
     it.t->done_chunks(it.nchunks - enq);
   }
+  for (auto& S : d->slots) S.pre = false;         // an early DMA whose chunk was never enqueued (a bad job)
 }
 
 void worker_loop(Device* d, size_t dslot) {
