@@ -759,10 +759,10 @@ void rebuild_class_tables(KeyState& K) {
 }
 
 // Pipeline chunks whose jobs fall into two or more kernel classes run
-// class-grouped: the chunk's plan fill on the copy stream, then each class
-// chain on the lane of its group -- RSA-2K/3K, RSA-4K+, the EC and Ed25519
-// classes -- and the verdict scatter on the lane of the chunk's costliest
-// group once every class is done.  A group's launches from consecutive chunks
+// class-grouped: the chunk's plan fill on the least-loaded group lane
+// (group_ctrl), then each class chain on the lane of its group (cls_group:
+// three groups of classes), the exact kernels and the verdict scatter on the
+// lane of the chunk's costliest group once every class is done.  A group's launches from consecutive chunks
 // queue on one lane (one hardware queue each) while the three groups run side
 // by side; lane-per-chunk instead ran each chunk's classes one after another
 // (~6 ms of serial latency per 262 k mixed chunk).  CAPJWT_CLASS_GROUPS=0:
@@ -792,14 +792,20 @@ int group_ctrl() {
   }();
   return m;
 }
-// Class -> group lane of a class-grouped chunk.  Default: RSA-2K and RSA-3K on
-// lane 0, RSA-4K+ on lane 1, the EC and Ed25519 classes on lane 2.
-// CAPJWT_CLASS_GROUP (A/B): one digit 0-2 per class 1..7 (RSA-2K, RSA-3K,
-// RSA-4K+, P-256, P-384, P-521, Ed25519), e.g. "0012222" (the default).
+// Class -> group lane of a class-grouped chunk: RSA-2K and RSA-4K+ on lane 0,
+// RSA-3K and P-384 on lane 1, P-256, P-521 and Ed25519 on lane 2.  In a
+// mixed chunk the small EC launches run far below their stand-alone rate
+// beside the RSA modexps (the round-3 split, all EC / Ed25519 classes on one
+// lane, made that lane the chunk's critical path: 6.8 of ~7 ms per 524 k
+// chunk, profiles/r04_s9/stream_trace_timeline.txt); this split measured
+// 20.8-21.2 ms per configs[4] stream at 262 k chunks against 22.8-23.2 ms
+// (profiles/r04_s10-s12).  CAPJWT_CLASS_GROUP (A/B): one digit 0-2 per class
+// 1..7 (RSA-2K, RSA-3K, RSA-4K+, P-256, P-384, P-521, Ed25519); the round-3
+// split is "0012222".
 int cls_group(int c) {
   static const std::array<int, NCLS> g = [] {
     std::array<int, NCLS> t{};
-    const char* d = "0012222";
+    const char* d = "0102122";
     const char* e = std::getenv("CAPJWT_CLASS_GROUP");
     if (e && std::strlen(e) == NCLS - 1 && std::strspn(e, "012") == NCLS - 1) d = e;
     for (int k = 1; k < NCLS; ++k) t[k] = d[k - 1] - '0';
@@ -1669,12 +1675,13 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
 // chunk) and the copies of a pinned stream run back to back
 // (profiles/r04_s9/stream_trace_*).  Only for spans that enqueue_chunk would
 // DMA as they are (compact, inside the caller's arena); it checks that the
-// span it computes matches and otherwise copies as usual.  CAPJWT_EARLY_DMA=0
-// turns it off (A/B).
+// span it computes matches and otherwise copies as usual.  Measured neutral on
+// the configs[4] stream (20.9-21.6 vs 21.0-21.2 ms at 262 k chunks,
+// profiles/r04_s12/), so off unless CAPJWT_EARLY_DMA=1.
 bool early_dma() {
   static const bool on = [] {
     const char* e = std::getenv("CAPJWT_EARLY_DMA");
-    return !(e && std::atoi(e) == 0);
+    return e && std::atoi(e) != 0;
   }();
   return on;
 }
