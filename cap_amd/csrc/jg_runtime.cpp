@@ -646,8 +646,11 @@ struct jg_batch {
   size_t marks_used = 0;
   std::vector<std::string> tnames;
   std::vector<float> tms;
+  // class-grouped resident runs (resident_groups): the GroupFan's events
+  std::vector<hipEvent_t> gev;      // [0] lane -> ctrl, [1] start, [2] join -> lane, [3 ..) class done
   ~jg_batch() {
     for (auto e : mark_events) (void)hipEventDestroy(e);
+    for (auto e : gev) (void)hipEventDestroy(e);
   }
 };
 
@@ -2770,13 +2773,59 @@ namespace {
 // A resident batch runs against the current key state when its key list is
 // the one it was planned for (a comb-width upgrade since staging is fine: the
 // run picks up the wider tables); a reload with another key list invalidates it.
+// CAPJWT_RESIDENT_GROUPS=1 (A/B): untimed resident runs of mixed batches use
+// the pipeline's class groups (cls_group) on the device's three group lanes,
+// as streamed chunks do, instead of one stream per class on the batch's lane.
+bool resident_groups() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAPJWT_RESIDENT_GROUPS");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 void run_resident(jg_ctx* ctx, jg_batch* b, bool timed) {
   HIPCHK(hipSetDevice(b->dev->id));
   KeyStateP ks = ctx->state();
   if (b->epoch != ks->epoch) throw std::runtime_error("key table reloaded since this batch was staged");
   b->timing = timed;
   b->marks_used = 0;
-  run_plan(b->dev, *ks, *ks->dev[b->dslot], b->lane, b->b, b->plan, b);
+  int nact = 0;
+  double gcost[3] = {0, 0, 0};
+  for (int c = 1; c < NCLS; ++c) {
+    const int64_t m = b->plan.ranges[c].end - b->plan.ranges[c].begin;
+    if (m <= 0) continue;
+    ++nact;
+    gcost[cls_group(c)] += CLS_COST[c] * (double)m;
+  }
+  if (!timed && nact >= 2 && resident_groups()) {
+    Device* d = b->dev;
+    if (b->gev.empty()) {
+      b->gev.resize(3 + NCLS);
+      for (auto& e : b->gev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    int jgrp = 0, least = 0;
+    for (int g = 1; g < 3; ++g) {
+      if (gcost[g] > gcost[jgrp]) jgrp = g;
+      if (d->gload[g] < d->gload[least]) least = g;
+    }
+    double lo = 1e300;
+    for (int g = 0; g < 3; ++g) lo = std::min(lo, d->gload[g] += gcost[g]);
+    for (int g = 0; g < 3; ++g) d->gload[g] -= lo;
+    GroupFan gf;
+    gf.join = d->lanes[jgrp].stream;
+    gf.ctrl = d->lanes[least].stream;
+    for (int c = 1; c < NCLS; ++c) gf.cls[c] = d->lanes[cls_group(c)].stream;
+    gf.start = b->gev[1];
+    for (int c = 0; c < NCLS; ++c) gf.done[c] = b->gev[3 + c];
+    HIPCHK(hipEventRecord(b->gev[0], b->lane->stream));        // after the batch's staging / previous run
+    HIPCHK(hipStreamWaitEvent(gf.ctrl, b->gev[0], 0));
+    run_plan(d, *ks, *ks->dev[b->dslot], b->lane, b->b, b->plan, nullptr, false, &gf);
+    HIPCHK(hipEventRecord(b->gev[2], gf.join));
+    HIPCHK(hipStreamWaitEvent(b->lane->stream, b->gev[2], 0));   // verdict copies and syncs stay on the lane
+  } else {
+    run_plan(b->dev, *ks, *ks->dev[b->dslot], b->lane, b->b, b->plan, b);
+  }
   if (b->ks_run && b->ks_run != ks) HIPCHK(hipStreamSynchronize(b->lane->stream));   // its kernels may read the old state
   b->ks_run = std::move(ks);
 }
