@@ -62,3 +62,18 @@ def test_p521_point_mads():
     assert abs((m[16] - m[18]) / 3 - per_add) < 1
     # a mixed addition: 8 mul + 3 sqr (L = 20) under 10 one-constant reductions + one fold MAD
     assert abs(per_add - (8 * 400 + 3 * 210 + 10 * 20 + 1)) < 1
+
+
+def test_rsa_modexp_layouts_match_the_library():
+    """bench.py prices each RSA class's modexp on the lanes per token the
+    library launches it with (kernels/rsa.hpp: RSA-2048 2 lanes, RSA-3072
+    JG_RSA3K_G lanes, RSA-4096 4): a squaring's partial products depend on it."""
+    src = open(os.path.join(ROOT, "cap_amd", "csrc", "kernels", "rsa.hpp")).read()
+    g3k = int(re.search(r"#define JG_RSA3K_G (\d+)", src).group(1))
+    g2k = int(re.search(r"#define JG_RSA2K_G (\d+)", src).group(1))
+    bsrc = open(os.path.join(ROOT, "bench.py")).read()
+    assert f'"rsa3072_modexp": rsa_modexp_mads_per_token(112, {g3k})' in bsrc
+    assert f'"rsa2048_modexp": rsa_modexp_mads_per_token(74, {g2k})' in bsrc
+    # e = 65537: 2 full products (2 L^2 each) + 16 squarings (lanes^2 H(H+1)/2 + L^2)
+    h = 112 // g3k
+    assert bench.rsa_modexp_mads_per_token(112, g3k) == 4 * 112 * 112 + 16 * (g3k * g3k * h * (h + 1) // 2 + 112 * 112)
