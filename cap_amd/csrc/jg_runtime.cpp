@@ -1362,6 +1362,12 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
         launch_ed(ea, s, marker(marks, c));
       });
     }
+    // a class stream's key-memory use is logged BEFORE its done event: what the
+    // join lane (and so every release of the generation) waits for covers it.
+    // Logged after the done event, the use could still be pending behind other
+    // work on a shared hardware queue when the join completed (a false
+    // lifetime violation, seen once in a full GPU session).
+    if (s != s0) G.uses.record(s, conc ? "class stream" : "group lane", c);
     if (conc) {
       HIPCHK(hipEventRecord(L->ev_done[c], s));
       HIPCHK(hipStreamWaitEvent(s0, L->ev_done[c], 0));
@@ -1374,16 +1380,10 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
   launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s0);
   mark(marks, "scatter");
   HIPCHK(hipGetLastError());
-  if (g_lifetime_on.load(std::memory_order_relaxed)) {
-    for (int c = 1; c < NCLS; ++c) {
-      if (P.ranges[c].end <= P.ranges[c].begin) continue;
-      if (conc) G.uses.record(L->cstream[c], "class stream", c);
-      else if (gf) G.uses.record(gf->cls[c], "group lane", c);
-    }
-    if (gf) G.uses.record(gf->ctrl, "chunk control");
-    if (feed) G.uses.record(gf->feed, "zero-copy gather feed");
-    G.uses.record(s0, gf ? "join lane" : "lane");
-  }
+  // the class streams logged their uses above; the chunk's control stream
+  // logged its plan fill (enqueue_chunk, before `start`); the zero-copy feed's
+  // gathers read no key memory
+  G.uses.record(s0, gf ? "join lane" : "lane");
 }
 
 void collect_times(jg_batch* b) {
