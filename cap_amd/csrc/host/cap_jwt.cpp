@@ -121,6 +121,53 @@ void run_chunks(const Chunks& c, F&& fn) {
 
 }  // namespace
 
+namespace {
+struct BlockCache {
+  std::mutex mu;
+  std::vector<std::pair<void*, size_t>> blocks;   // (block, capacity)
+  size_t bytes = 0;
+};
+BlockCache& block_cache() {
+  static BlockCache* c = new BlockCache();        // never destroyed: blocks outlive static teardown
+  return *c;
+}
+constexpr size_t kCacheMin = size_t(1) << 20, kCacheMaxBytes = size_t(4) << 30;
+constexpr size_t kCacheMaxBlocks = 8;
+}  // namespace
+
+void* batch_block_alloc(size_t bytes) {
+  if (bytes >= kCacheMin) {
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    size_t best = c.blocks.size();
+    for (size_t i = 0; i < c.blocks.size(); ++i) {
+      const size_t cap = c.blocks[i].second;
+      if (cap >= bytes && cap / 2 <= bytes && (best == c.blocks.size() || cap < c.blocks[best].second)) best = i;
+    }
+    if (best < c.blocks.size()) {
+      void* p = c.blocks[best].first;
+      c.bytes -= c.blocks[best].second;
+      c.blocks.erase(c.blocks.begin() + (std::ptrdiff_t)best);
+      return p;
+    }
+  }
+  return ::operator new(bytes);
+}
+
+void batch_block_free(void* p, size_t bytes) {
+  if (!p) return;
+  if (bytes >= kCacheMin) {
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    if (c.blocks.size() < kCacheMaxBlocks && c.bytes + bytes <= kCacheMaxBytes) {
+      c.blocks.emplace_back(p, bytes);
+      c.bytes += bytes;
+      return;
+    }
+  }
+  ::operator delete(p);
+}
+
 void batch_parallel(size_t n, int threads, const std::function<void(size_t, size_t)>& fn) {
   parallel_for(n, threads, fn);
 }
@@ -278,7 +325,7 @@ template <class T>
 void ParArray<T>::init(size_t count, int th) {
   release();
   threads = th;
-  p = static_cast<T*>(::operator new(sizeof(T) * (count ? count : 1)));
+  p = static_cast<T*>(batch_block_alloc(sizeof(T) * (count ? count : 1)));
   n = count;
   parallel_for(n, threads, [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) new (p + i) T();
@@ -291,7 +338,7 @@ void ParArray<T>::release() {
   parallel_for(n, threads, [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) p[i].~T();
   });
-  ::operator delete(p);
+  batch_block_free(p, sizeof(T) * (n ? n : 1));
   p = nullptr;
   n = 0;
 }

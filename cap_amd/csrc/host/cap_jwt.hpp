@@ -55,6 +55,17 @@ struct Result {
 void batch_parallel(size_t n, int threads, const std::function<void(size_t, size_t)>& fn);
 int host_threads();
 
+// Storage of the batch arrays (BatchArray, the key sets' per-token records):
+// blocks of 1 MiB and more are kept in a small process-wide cache when freed
+// and handed out again to the next batch, instead of going back to the OS.
+// A 1M-token batch frees ~200 MB of records twice per ValidateBatch call;
+// returned to the OS each time, the unmap cost ~30 ms per array and the next
+// call paid the page faults again (bench e2e phases "free-toks",
+// "blob release").  At most 8 blocks and 4 GiB are kept; a block is reused
+// for a request of at least half its size.
+void* batch_block_alloc(size_t bytes);
+void batch_block_free(void* p, size_t bytes);
+
 // The per-token records of a batch, constructed and destroyed by all host
 // threads: a 1M-token batch's results are ~150 MB of records plus their claims
 // maps, and a serial std::vector construction or free of that costs more than
@@ -64,7 +75,7 @@ class BatchArray {
  public:
   BatchArray() = default;
   explicit BatchArray(size_t n, int threads = host_threads()) : threads_(threads) {
-    p_ = static_cast<T*>(::operator new(sizeof(T) * (n ? n : 1)));
+    p_ = static_cast<T*>(batch_block_alloc(sizeof(T) * (n ? n : 1)));
     batch_parallel(n, threads_, [this](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) new (p_ + i) T();
     });
@@ -87,7 +98,7 @@ class BatchArray {
     batch_parallel(n_, threads_, [this](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) p_[i].~T();
     });
-    ::operator delete(p_);
+    batch_block_free(p_, sizeof(T) * (n_ ? n_ : 1));
     p_ = nullptr;
     n_ = 0;
   }
