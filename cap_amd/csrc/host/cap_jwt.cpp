@@ -499,6 +499,11 @@ struct Verified {
   ParArray<Tok> toks;
   std::vector<ByteArena> payloads;   // one per parse range
   std::vector<uint8_t> any;          // some candidate key verified
+  // degraded path (SURVEY §5 failure row): when the device call fails (a HIP
+  // error, a lost device) the tokens it carried are marked here and get
+  // dev_err as their error -- no CPU verification, no exception out of the batch
+  std::vector<uint8_t> failed;
+  std::string dev_err;
 };
 
 template <class Cand>
@@ -511,6 +516,7 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
   if (!subset) {
     V->toks.init(tokens.size(), eng.threads());
     V->any.assign(tokens.size(), 0);
+    V->failed.assign(tokens.size(), 0);
     V->payloads.resize(ch.count());
     run_chunks(ch, [&](size_t c, size_t lo, size_t hi) {
       HdrCache cache;
@@ -572,7 +578,16 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
     }
   });
   pt.lap("pack");
-  eng.verify(arena, arena_len, jobs.get(), total_jobs, verdict.get());
+  try {
+    eng.verify(arena, arena_len, jobs.get(), total_jobs, verdict.get());
+  } catch (const std::exception& e) {
+    V->dev_err = std::string("capjwt: signature verification unavailable: ") + e.what();
+    run_chunks(ch, [&](size_t, size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i)
+        if (V->toks[tok_index(i)].ncand) V->failed[tok_index(i)] = 1;
+    });
+    return;
+  }
   pt.lap("gpu");
   run_chunks(ch, [&](size_t, size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
@@ -611,6 +626,8 @@ class StaticKeySet final : public KeySet {
         Result& r = res[i];
         if (!t.parsed) {
           r.err = t.parse_err;                                           // jwt.ParseSigned error
+        } else if (V.failed[i]) {
+          r.err = V.dev_err;
         } else {
           std::string jerr;
           // parsedJWT.Claims(key, &allClaims): verify, then unmarshal; a JSON
@@ -680,6 +697,8 @@ class JSONWebKeySet final : public KeySet {
         Result& r = res[i];
         if (!t.parsed) {
           r.err = "oidc: malformed jwt: " + t.parse_err;
+        } else if (V.failed[i]) {
+          r.err = V.dev_err;
         } else if (!V.any[i]) {
           r.err = miss_err;
         } else {
@@ -707,6 +726,7 @@ class JSONWebKeySet final : public KeySet {
       for (size_t i = lo; i < hi; ++i) {
         Tok& t = V.toks[i];
         if (!t.parsed) res[i].err = "oidc: malformed jwt: " + t.parse_err;
+        else if (V.failed[i]) res[i].err = V.dev_err;
         else if (!V.any[i]) res[i].err = miss_err;
         else { res[i].ok = true; res[i].payload = std::string(t.payload); }
       }
@@ -731,10 +751,12 @@ class JSONWebKeySet final : public KeySet {
       gpu_verify(eng_, tokens, V, [](const Tok&, std::vector<uint16_t>&) {});
     }
     // tokens that parsed but did not verify: refresh once if the cache has
-    // expired (now + keysExpiryDelta(30s) after expiry), then retry them
+    // expired (now + keysExpiryDelta(30s) after expiry), then retry them.  A
+    // token whose device call failed is no miss: it keeps the device error and
+    // triggers no refetch
     std::vector<size_t> miss;
     for (size_t i = 0; i < tokens.size(); ++i)
-      if (V->toks[i].parsed && !V->any[i]) miss.push_back(i);
+      if (V->toks[i].parsed && !V->any[i] && !V->failed[i]) miss.push_back(i);
     std::string fetch_err;
     bool refreshed = false;
     if (!miss.empty() && (!have_keys_ || wall_now_ns() + 30 * kSecond > expiry_ns_)) {
