@@ -1364,7 +1364,14 @@ std::vector<HashClaimResult> verify_hash_claim_batch(Engine& eng, const std::str
       arena.append(values[idx[k]]);
     }
     std::vector<uint8_t> dig(64 * idx.size());
-    eng.hash((const uint8_t*)arena.data(), arena.size(), jobs.data(), jobs.size(), dig.data());
+    try {
+      eng.hash((const uint8_t*)arena.data(), arena.size(), jobs.data(), jobs.size(), dig.data());
+    } catch (const std::exception& e) {
+      // degraded path, as the key sets': the pairs that needed the device get
+      // its error, the batch returns
+      for (size_t i : idx) out[i].err = std::string("capjwt: hash unavailable: ") + e.what();
+      idx.clear();
+    }
     parallel_for(idx.size(), host_threads(), [&](size_t lo, size_t hi) {
       for (size_t k = lo; k < hi; ++k) {
         const size_t i = idx[k];

@@ -65,6 +65,16 @@ int main() {
   jr = jw->VerifySignatureBatch({ed_tok});
   check(!jr[0].ok && has(jr[0].err, dev), "jwks: device error again", jr[0].err);
   check(fetches == 1, "jwks: no refetch for a device failure", std::to_string(fetches));
+  // oidc hash claims: a failed jg_hash_batch becomes each pair's error
+  {
+    Engine eng({});
+    // {"alg":"RS256"} . {"at_hash":"x"} . "AAAA"
+    const std::string idt = "eyJhbGciOiJSUzI1NiJ9.eyJhdF9oYXNoIjoieCJ9.AAAA";
+    auto hr = VerifyAccessTokenBatch(eng, {idt, "not-a-jwt"}, {"access-token", "access-token"});
+    check(!hr[0].verified && has(hr[0].err, "VerifyAccessToken: capjwt: hash unavailable: capjwt: jg_hash_batch: "),
+          "hash: device error", hr[0].err);
+    check(!hr[1].verified && !hr[1].err.empty() && !has(hr[1].err, "unavailable"), "hash: parse error", hr[1].err);
+  }
   std::printf(fails ? "degraded: %d failures\n" : "degraded: ok\n", fails);
   return fails ? 1 : 0;
 }
