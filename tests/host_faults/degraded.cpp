@@ -65,6 +65,13 @@ int main() {
   jr = jw->VerifySignatureBatch({ed_tok});
   check(!jr[0].ok && has(jr[0].err, dev), "jwks: device error again", jr[0].err);
   check(fetches == 1, "jwks: no refetch for a device failure", std::to_string(fetches));
+  // go-oidc adapter (remoteKeySet.VerifySignature, payload bytes)
+  {
+    auto rk = NewRemoteKeySet("https://issuer.example/keys", f);
+    auto pr = rk->VerifySignatureBatch({ed_tok, "not-a-jwt"});
+    check(!pr[0].ok && has(pr[0].err, dev), "remote: device error", pr[0].err);
+    check(!pr[1].ok && has(pr[1].err, "oidc: malformed jwt: "), "remote: parse error", pr[1].err);
+  }
   // oidc hash claims: a failed jg_hash_batch becomes each pair's error
   {
     Engine eng({});
