@@ -429,6 +429,55 @@ def measure_pcie(ctx, arena, toks, iters=5, chunks=(32768, 65536, 131072), warm=
                     "not the headline"}
 
 
+def host_snapshot():
+    """Process-level host counters around an e2e pass:
+    cgroup v2 CPU throttling, rusage (page faults, context switches, CPU time)
+    and CPU time per thread name.  Linux only; missing files are skipped."""
+    import resource
+    snap = {"t": time.perf_counter()}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            snap["cg"] = {k: int(v) for k, v in (ln.split() for ln in f if len(ln.split()) == 2)}
+    except OSError:
+        snap["cg"] = {}
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    snap["ru"] = {"minflt": ru.ru_minflt, "majflt": ru.ru_majflt, "nvcsw": ru.ru_nvcsw, "nivcsw": ru.ru_nivcsw,
+                  "utime": ru.ru_utime, "stime": ru.ru_stime}
+    thr = {}
+    tick = os.sysconf("SC_CLK_TCK")
+    try:
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                with open(f"/proc/self/task/{tid}/stat") as f:
+                    s = f.read()
+                name = s[s.index("(") + 1:s.rindex(")")]
+                fields = s[s.rindex(")") + 2:].split()
+                thr[tid] = (name, (int(fields[11]) + int(fields[12])) / tick)
+            except (OSError, ValueError, IndexError):
+                pass
+    except OSError:
+        pass
+    snap["thr"] = thr
+    return snap
+
+
+def host_delta(a, b):
+    """What changed between two host_snapshot()s: wall, CPU, faults, throttling
+    and the threads that used the most CPU in between (by name)."""
+    d = {"wall_s": b["t"] - a["t"]}
+    d.update({k: b["ru"][k] - a["ru"][k] for k in a["ru"]})
+    d.update({"cg_" + k: b["cg"].get(k, 0) - a["cg"].get(k, 0) for k in ("nr_throttled", "throttled_usec",
+                                                                       "usage_usec", "nr_periods")})
+    by_name = {}
+    for tid, (name, cpu) in b["thr"].items():
+        used = cpu - a["thr"].get(tid, (name, 0.0))[1]
+        if used > 0:
+            by_name[name] = by_name.get(name, 0.0) + used
+    d["threads_now"] = len(b["thr"])
+    d["cpu_by_thread_name"] = dict(sorted(by_name.items(), key=lambda kv: -kv[1])[:8])
+    return d
+
+
 def measure_e2e(pool, kids_jwk, total, threads):
     """Validator.ValidateBatch through the C++ host mirror (JWKS key set, host
     parse + kid routing + one GPU batch + claims validation), tokens handed
@@ -449,19 +498,61 @@ def measure_e2e(pool, kids_jwk, total, threads):
     # passes that overlap those ~1 s of table builds measure the load, not the
     # validation rate (round 3's e2e line did)
     ks.WaitTables()
-    best, acc = float("inf"), 0
+    best, acc, diag = float("inf"), 0, []
     for _ in range(2):
+        s0 = host_snapshot()
         t0 = time.perf_counter()
         ok = v.ValidateBlob(blob, e)
-        best = min(best, time.perf_counter() - t0)
+        dt = time.perf_counter() - t0
+        diag.append(host_delta(s0, host_snapshot()))
+        best = min(best, dt)
         acc = sum(ok)
     if acc != total:
         raise RuntimeError(f"e2e accepted {acc}/{total}")
     from cap_amd import _capjwt_host
     return {"value": total / best, "unit": "validated JWTs/s", "ms_per_batch": best * 1e3, "tokens": total,
-            "host_threads": _capjwt_host.host_threads(),
+            "host_threads": _capjwt_host.host_threads(), "host_diag": diag,
             "note": "Validator.ValidateBatch (jwt/jwt.go:95 semantics) end to end: host parse/kid routing/claims "
                     "on host_threads cores + one jg_verify_batch (H2D included); not the headline value"}
+
+
+def measure_single(pool, kids_jwk, threads, callers_list=None, total=1 << 18):
+    """The drop-in path of an unchanged cap caller: C++
+    threads, each calling Validator.Validate once per token -- Go's
+    goroutine-per-request pattern -- on the configs[1] pool (ES256, 4-kid
+    JWKS).  The key set coalesces concurrent calls into device batches
+    (KeySet coalescer, default settings).  Per-call latency percentiles and
+    the aggregate rate for host_threads callers (the headline of this line)
+    and for more concurrent requests."""
+    from cap_amd import jwt
+    jwks = json.dumps({"keys": kids_jwk}).encode()
+    ks, err = jwt.NewJSONWebKeySet(None, "https://bench.example/jwks", "",
+                                   lambda url, ca: {"status": 200, "body": jwks, "max_age": 3600})
+    assert err is None, err
+    v, _ = jwt.NewValidator(ks)
+    e = jwt.Expected(Issuer="https://example.com/", Audiences=["www.example.com"], SigningAlgorithms=["ES256"],
+                     Now=lambda: 1611699344 + 60)
+    blob = b"\n".join(pool[:1 << 18])
+    v.ValidateBlob(blob[:1 << 20], e)                # first fetch + key staging
+    ks.WaitTables()
+    out = {}
+    for c in callers_list or (threads, 256, 1024):
+        v._impl._concurrent_validate(blob, e._native(), c, min(total, 1 << 15))      # warm the callers' path
+        st0 = ks.CoalescingStats()
+        r = dict(v._impl._concurrent_validate(blob, e._native(), c, total))
+        st1 = ks.CoalescingStats()
+        batches = st1["batches"] - st0["batches"]
+        r["value"] = r["calls"] / r["wall_s"]
+        r["mean_batch"] = r["calls"] / max(1, batches)
+        if r["accepted"] != r["calls"]:
+            r["error"] = f"accepted {r['accepted']} of {r['calls']}"
+        out[str(c)] = r
+    head = out[str(threads)]
+    return {"value": head["value"], "unit": "validated JWTs/s", "callers": threads, "p50_us": head["p50_us"],
+            "p99_us": head["p99_us"], "by_callers": out,
+            "note": "Validator.Validate per token from N concurrent host threads (one call per token, as Go callers "
+                    "do), coalesced into device batches by the key set; value/p50/p99 at N = host_threads; "
+                    "by_callers: the same at more concurrent requests. Not the headline."}
 
 
 E2E_KIDS = ["p256-a", "p256-b", "p256-c", "p256-d"]
@@ -495,17 +586,49 @@ def measure_e2e_fresh(pool, total):
     if r.returncode != 0:
         raise RuntimeError(f"e2e child failed: {r.stderr[-2000:]}")
     out = json.loads(r.stdout.strip().splitlines()[-1])
-    phases = {}
-    for line in r.stderr.splitlines():          # the last pass's phases win
-        if line.startswith("[capjwt] ") and line.rstrip().endswith("ms"):
-            parts = line[len("[capjwt] "):].rsplit(None, 2)
-            try:
-                phases[parts[0].strip()] = float(parts[1])
-            except (ValueError, IndexError):
-                pass
-    out["phases_ms_last_pass"] = phases
+    out["phases_ms_last_pass"] = trace_phases(r.stderr)
     out["process"] = "fresh child process (bench.py --e2e-child)"
     return out
+
+
+def trace_phases(text):
+    """CAPJWT_TRACE phase lines -> {phase: ms} (and {phase + " flt": minor
+    page faults} where the line carries them); the last pass's phases win."""
+    import re
+    pat = re.compile(r"^\[capjwt\] (.+?)\s+(?:(-?\d+) flt\s+)?(-?[\d.]+) ms\s*$")
+    phases = {}
+    for line in text.splitlines():
+        m = pat.match(line)
+        if m:
+            name = " ".join(m.group(1).split())
+            phases[name] = float(m.group(3))
+            if m.group(2) is not None:
+                phases[name + " flt"] = int(m.group(2))
+    return phases
+
+
+def with_trace_phases(fn):
+    """Run fn() in this process with CAPJWT_TRACE=1 and fd 2 sent to a temp
+    file; returns (fn's result, its last pass's phase times)."""
+    import tempfile
+    sys.stderr.flush()
+    saved = os.dup(2)
+    old = os.environ.get("CAPJWT_TRACE")
+    with tempfile.TemporaryFile() as tf:
+        os.dup2(tf.fileno(), 2)
+        os.environ["CAPJWT_TRACE"] = "1"
+        try:
+            res = fn()
+        finally:
+            os.dup2(saved, 2)
+            os.close(saved)
+            if old is None:
+                os.environ.pop("CAPJWT_TRACE", None)
+            else:
+                os.environ["CAPJWT_TRACE"] = old
+        tf.seek(0)
+        text = tf.read().decode(errors="replace")
+    return res, trace_phases(text)
 
 
 def cpu_info():
@@ -1173,12 +1296,13 @@ def main():
     if rank == 0 and not args.no_e2e:
         jwk = [{"kty": "EC", "kid": f"kid-{i:02d}", "crv": "P-256", **xy} for i, xy in enumerate(p256_jwk_xy(kids))]
         result["e2e"] = measure_e2e_fresh(pool, args.tokens)
-        inproc = measure_e2e(pool, jwk, args.tokens, host_threads)
+        inproc, phases = with_trace_phases(lambda: measure_e2e(pool, jwk, args.tokens, host_threads))
         result["e2e"]["in_bench_process"] = {
             "value": inproc["value"], "ms_per_batch": inproc["ms_per_batch"],
+            "host_diag": inproc["host_diag"], "phases_ms_last_pass": phases,
             "note": "the same measure_e2e inside this bench process after every other line (tens of GB of token "
-                    "pools and many contexts behind it); profiles/r04_s1_e2e_ab: the fresh-process rate is the "
-                    "path's, and the round-2 build measures the same there"}
+                    "pools and many contexts behind it)"}
+        result["single"] = measure_single(pool, jwk, host_threads)
 
     # ---- CPU baselines (rank 0, N = 1 only), both on every core the process
     # may use.  `cpu_baseline` is OpenSSL libcrypto (tools/cpuverify): the
@@ -1216,6 +1340,8 @@ def main():
         result["cpu_baseline_openssl"] = ossl
         speed["note"] = ("GPU value / all-core CPU rate on the same tokens. Neither CPU leg is Go (absent on the GPU "
                          "box): 'openssl' = OpenSSL libcrypto (cpu_baseline), 'port' = the repo's clarity-first C oracle")
+        if "single" in result and "es256" in ossl:
+            result["single"]["cpu_baseline_openssl"] = ossl["es256"]["value"]
         result["speedup_vs_cpu"] = speed
     if rank == 0:
         print(json.dumps(result))

@@ -23,7 +23,7 @@ EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_las
            "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
            "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_zero_copy", "jg_set_table_budget", "jg_keys_wait_tables",
            "jg_keys_table_widths", "jg_debug_fail_alloc", "jg_debug_table_digest",
-           "jg_debug_max_upgrades", "jg_debug_lifetime_check"]
+           "jg_debug_max_upgrades", "jg_debug_lifetime_check", "jg_debug_fail_verify"]
 
 
 class JgKey(ctypes.Structure):
@@ -83,6 +83,7 @@ def lib():
         L.jg_keys_table_widths.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.jg_debug_fail_alloc.argtypes = [vp, ctypes.c_int]
         L.jg_debug_max_upgrades.argtypes = [vp, ctypes.c_int]
+        L.jg_debug_fail_verify.argtypes = [vp, ctypes.c_int]
         L.jg_debug_lifetime_check.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                               ctypes.POINTER(ctypes.c_uint64)]
         L.jg_debug_table_digest.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
@@ -221,6 +222,12 @@ class Context:
         """jg_debug_fail_alloc: the n-th device allocation of later key loads fails (0 = off)."""
         if lib().jg_debug_fail_alloc(self.h, int(n)) != 0:
             raise JgError("jg_debug_fail_alloc failed")
+
+    def debug_fail_verify(self, n):
+        """jg_debug_fail_verify: the n-th later submission fails as a device fault and the
+        context stays unusable (0 = off)."""
+        if lib().jg_debug_fail_verify(self.h, int(n)) != 0:
+            raise JgError("jg_debug_fail_verify failed")
 
     def verify(self, arena: Arena):
         n = len(arena.toks)

@@ -16,6 +16,7 @@
 #include "cap_jwt.hpp"
 
 #include <sched.h>
+#include <sys/resource.h>
 
 #include <algorithm>
 #include <atomic>
@@ -29,6 +30,7 @@
 #include <unordered_map>
 
 #include "../../../include/jg.h"
+#include "hostmem.hpp"
 
 namespace capjwt {
 
@@ -121,52 +123,21 @@ void run_chunks(const Chunks& c, F&& fn) {
 
 }  // namespace
 
-namespace {
-struct BlockCache {
-  std::mutex mu;
-  std::vector<std::pair<void*, size_t>> blocks;   // (block, capacity)
-  size_t bytes = 0;
-};
-BlockCache& block_cache() {
-  static BlockCache* c = new BlockCache();        // never destroyed: blocks outlive static teardown
-  return *c;
-}
-constexpr size_t kCacheMin = size_t(1) << 20, kCacheMaxBytes = size_t(4) << 30;
-constexpr size_t kCacheMaxBlocks = 8;
-}  // namespace
-
-void* batch_block_alloc(size_t bytes) {
-  if (bytes >= kCacheMin) {
-    BlockCache& c = block_cache();
-    std::lock_guard<std::mutex> g(c.mu);
-    size_t best = c.blocks.size();
-    for (size_t i = 0; i < c.blocks.size(); ++i) {
-      const size_t cap = c.blocks[i].second;
-      if (cap >= bytes && cap / 2 <= bytes && (best == c.blocks.size() || cap < c.blocks[best].second)) best = i;
-    }
-    if (best < c.blocks.size()) {
-      void* p = c.blocks[best].first;
-      c.bytes -= c.blocks[best].second;
-      c.blocks.erase(c.blocks.begin() + (std::ptrdiff_t)best);
-      return p;
-    }
-  }
+void* batch_block_alloc(size_t bytes, size_t* cap) {
+  if (bytes >= (size_t(1) << 20)) return hostmem::big_get(bytes, cap);
+  *cap = bytes;
   return ::operator new(bytes);
 }
 
-void batch_block_free(void* p, size_t bytes) {
+void batch_block_free(void* p, size_t cap) {
   if (!p) return;
-  if (bytes >= kCacheMin) {
-    BlockCache& c = block_cache();
-    std::lock_guard<std::mutex> g(c.mu);
-    if (c.blocks.size() < kCacheMaxBlocks && c.bytes + bytes <= kCacheMaxBytes) {
-      c.blocks.emplace_back(p, bytes);
-      c.bytes += bytes;
-      return;
-    }
-  }
-  ::operator delete(p);
+  if (cap >= (size_t(1) << 20)) hostmem::big_put(p, cap);
+  else ::operator delete(p);
 }
+
+void SetHostMemoryRetention(size_t bytes) { hostmem::set_retention_cap(bytes); }
+void TrimHostMemory() { hostmem::trim(); }
+size_t HostMemoryRetained() { return hostmem::retained(); }
 
 void batch_parallel(size_t n, int threads, const std::function<void(size_t, size_t)>& fn) {
   parallel_for(n, threads, fn);
@@ -238,17 +209,27 @@ struct HdrCache {
 // decoded length of a base64url segment with no '=' (Go RawURLEncoding)
 inline size_t b64_decoded_len(size_t n) { return n / 4 * 3 + (n % 4 == 2 ? 1 : n % 4 == 3 ? 2 : 0); }
 
-struct PhaseTimer {            // CAPJWT_TRACE=1: per-phase wall times on stderr
+struct PhaseTimer {            // CAPJWT_TRACE=1: per-phase wall times (and page faults) on stderr
   bool on;
   std::chrono::steady_clock::time_point t0;
+  long flt0 = 0;
   const char* what;
-  explicit PhaseTimer(const char* w) : on(std::getenv("CAPJWT_TRACE") != nullptr), t0(std::chrono::steady_clock::now()), what(w) {}
+  static long minflt() {
+    rusage ru;
+    getrusage(RUSAGE_SELF, &ru);
+    return ru.ru_minflt;
+  }
+  explicit PhaseTimer(const char* w) : on(std::getenv("CAPJWT_TRACE") != nullptr), t0(std::chrono::steady_clock::now()), what(w) {
+    if (on) flt0 = minflt();
+  }
   void lap(const char* phase) {
     if (!on) return;
     const auto t1 = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[capjwt] %s %-12s %8.2f ms\n", what, phase,
+    const long f = minflt();
+    std::fprintf(stderr, "[capjwt] %s %-12s %7ld flt %8.2f ms\n", what, phase, f - flt0,
                  std::chrono::duration<double, std::milli>(t1 - t0).count());
     t0 = t1;
+    flt0 = f;
   }
 };
 
@@ -258,7 +239,7 @@ struct PhaseTimer {            // CAPJWT_TRACE=1: per-phase wall times on stderr
 template <class T>
 struct ParArray {
   T* p = nullptr;
-  size_t n = 0;
+  size_t n = 0, cap = 0;
   int threads = 1;
   ParArray() = default;
   ParArray(const ParArray&) = delete;
@@ -271,25 +252,43 @@ struct ParArray {
   size_t size() const { return n; }
 };
 
-// Decoded payloads of one parse range, in a few large blocks (one free per
-// block instead of one per token)
+// Decoded payloads of one parse range, in pooled hostmem blocks (one return
+// per block instead of one free per token; no page faults in steady state)
 struct ByteArena {
-  std::vector<std::unique_ptr<char[]>> blocks;
+  std::vector<void*> blocks;                      // hostmem::kBlock each
+  std::vector<std::unique_ptr<char[]>> big;       // payloads larger than a block
   char* cur = nullptr;
   size_t left = 0;
+  ByteArena() = default;
+  ByteArena(ByteArena&& o) noexcept
+      : blocks(std::move(o.blocks)), big(std::move(o.big)), cur(o.cur), left(o.left), last_big(o.last_big) {
+    o.cur = nullptr;
+    o.left = 0;
+  }
+  ByteArena(const ByteArena&) = delete;
+  ByteArena& operator=(const ByteArena&) = delete;
+  ~ByteArena() {
+    for (void* b : blocks) hostmem::block_put(b);
+  }
+  bool last_big = false;
   char* alloc(size_t n) {
+    last_big = n > hostmem::kBlock / 2;
+    if (last_big) {
+      big.emplace_back(new char[n]);
+      return big.back().get();
+    }
     if (n > left) {
-      const size_t sz = std::max<size_t>(n, (size_t)1 << 20);
-      blocks.emplace_back(new char[sz]);
-      cur = blocks.back().get();
-      left = sz;
+      blocks.push_back(hostmem::block_get());
+      cur = static_cast<char*>(blocks.back());
+      left = hostmem::kBlock;
     }
     char* r = cur;
     cur += n;
     left -= n;
     return r;
   }
-  void give_back(size_t n) {     // the unused tail of the last alloc
+  void give_back(size_t n) {     // the unused tail of the last alloc (a block's, not a big one's)
+    if (last_big) return;
     cur -= n;
     left += n;
   }
@@ -325,7 +324,7 @@ template <class T>
 void ParArray<T>::init(size_t count, int th) {
   release();
   threads = th;
-  p = static_cast<T*>(batch_block_alloc(sizeof(T) * (count ? count : 1)));
+  p = static_cast<T*>(batch_block_alloc(sizeof(T) * (count ? count : 1), &cap));
   n = count;
   parallel_for(n, threads, [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) new (p + i) T();
@@ -338,7 +337,7 @@ void ParArray<T>::release() {
   parallel_for(n, threads, [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) p[i].~T();
   });
-  batch_block_free(p, sizeof(T) * (n ? n : 1));
+  batch_block_free(p, cap);
   p = nullptr;
   n = 0;
 }
@@ -494,23 +493,38 @@ int key_family(const PublicKey& k) {
 }
 
 // The GPU half shared by both key sets: parse, pack, verify.  `cand(t, push)`
-// pushes the key indices to try for token t.
+// pushes the key indices to try for token t.  `keys_lock` (may be null) is the
+// caller's lock on its key list, held from the first cand() call until the
+// jobs are queued on the device and released there (jg_submit captures the
+// device key table that the candidate indices refer to).
+}  // namespace
+
+// A batch after parse and device verification, before claims (KeySet::verify_raw)
 struct Verified {
   ParArray<Tok> toks;
   std::vector<ByteArena> payloads;   // one per parse range
   std::vector<uint8_t> any;          // some candidate key verified
   // degraded path (SURVEY §5 failure row): when the device call fails (a HIP
   // error, a lost device) the tokens it carried are marked here and get
-  // dev_err as their error -- no CPU verification, no exception out of the batch
+  // dev_err as their error -- no CPU verification, no exception out of the
+  // batch; dev_seen = the engine's error count then (for Engine::recover)
   std::vector<uint8_t> failed;
   std::string dev_err;
+  uint64_t dev_seen = 0;
+  bool dev_failed = false;
+  std::string miss_err;              // JWKS: the error of a parsed token no key verified
 };
+
+namespace {
 
 template <class Cand>
 void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verified* V, Cand&& cand,
-                const std::vector<size_t>* subset = nullptr) {
+                const std::vector<size_t>* subset = nullptr, std::shared_lock<std::shared_mutex>* keys_lock = nullptr) {
   const size_t n = subset ? subset->size() : tokens.size();
   auto tok_index = [&](size_t i) { return subset ? (*subset)[i] : i; };
+  auto release_keys = [&] {
+    if (keys_lock && keys_lock->owns_lock()) keys_lock->unlock();
+  };
   PhaseTimer pt("verify");
   const Chunks ch = make_chunks(n, eng.threads());
   if (!subset) {
@@ -519,7 +533,10 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
     V->failed.assign(tokens.size(), 0);
     V->payloads.resize(ch.count());
     run_chunks(ch, [&](size_t c, size_t lo, size_t hi) {
-      HdrCache cache;
+      // per thread and kept across batches: a coalesced single-token batch
+      // finds its issuer's header decoded already (make_hdr is a pure function
+      // of the segment; entries are immutable and shared)
+      thread_local HdrCache cache;
       for (size_t i = lo; i < hi; ++i) parse_one(tokens[i], cache, V->payloads[c], &V->toks[i]);
     });
     pt.lap("parse");
@@ -546,9 +563,12 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
   }
   const size_t total_jobs = rjobs[ch.count()];
   pt.lap("plan");
-  if (total_jobs == 0) return;
+  if (total_jobs == 0) {
+    release_keys();
+    return;
+  }
   const uint64_t arena_len = rbytes[ch.count()];
-  uint8_t* arena = eng.arena_buffer(arena_len);
+  Engine::Pinned arena = eng.pinned(arena_len);
   std::unique_ptr<jg_tok[]> jobs(new jg_tok[total_jobs]);      // filled below, not zeroed first
   std::unique_ptr<uint8_t[]> verdict(new uint8_t[total_jobs]);
   // pass 2: pack the arena and the jobs, each range from its own offsets
@@ -559,7 +579,7 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
       Tok& t = V->toks[tok_index(i)];
       if (!t.ncand) continue;
       const size_t len = t.entry_len();
-      std::memcpy(arena + off, t.lit ? t.lit : t.owned.data(), len);
+      std::memcpy(arena.get() + off, t.lit ? t.lit : t.owned.data(), len);
       ks.clear();
       cand(t, ks);
       t.job0 = jn;
@@ -579,9 +599,12 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
   });
   pt.lap("pack");
   try {
-    eng.verify(arena, arena_len, jobs.get(), total_jobs, verdict.get());
-  } catch (const std::exception& e) {
+    eng.verify(arena.get(), arena_len, jobs.get(), total_jobs, verdict.get(), release_keys);
+  } catch (const DeviceError& e) {
+    release_keys();
     V->dev_err = std::string("capjwt: signature verification unavailable: ") + e.what();
+    V->dev_seen = eng.errors();
+    V->dev_failed = true;
     run_chunks(ch, [&](size_t, size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i)
         if (V->toks[tok_index(i)].ncand) V->failed[tok_index(i)] = 1;
@@ -600,6 +623,12 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
   pt.lap("verdicts");
 }
 
+// After a batch whose device call failed: recreate the context so that the
+// next call verifies again (Engine::recover; no key refetch)
+void recover_after(Engine& eng, const Verified& V) {
+  if (V.dev_failed) (void)eng.recover(V.dev_seen);
+}
+
 // ---------------------------------------------------------------- static key set
 class StaticKeySet final : public KeySet {
  public:
@@ -608,51 +637,46 @@ class StaticKeySet final : public KeySet {
     for (const auto& k : keys_) fam_.push_back(key_family(k));
   }
   void WaitTables() override { eng_.wait_tables(); }
-  Results verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
-    std::lock_guard<std::mutex> g(mu_);
-    Verified V;
-    gpu_verify(eng_, tokens, &V, [&](const Tok& t, std::vector<uint16_t>& out) {
+  std::string DeviceStatus() override { return eng_.status(); }
+  int DeviceRecoveries() override { return eng_.recoveries(); }
+  int DebugFailVerify(int n) override { return eng_.debug_fail_verify(n); }
+  // The key list never changes: no lock; concurrent calls pipeline on the device.
+  std::shared_ptr<Verified> verify_raw(const std::vector<std::string_view>& tokens) override {
+    auto V = std::make_shared<Verified>();
+    gpu_verify(eng_, tokens, V.get(), [&](const Tok& t, std::vector<uint16_t>& out) {
       // staticKeySet: every key in order (jwt/keyset.go:162-168); a key of
       // another family fails newVerifier/verifyPayload without arithmetic (R10)
       const int fam = alg_key_kind(t.alg);
       for (size_t k = 0; k < keys_.size(); ++k)
         if (fam_[k] == fam) out.push_back((uint16_t)k);
     });
-    Results res(tokens.size(), eng_.threads());
-    PhaseTimer pt("static");
-    parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) {
-        const Tok& t = V.toks[i];
-        Result& r = res[i];
-        if (!t.parsed) {
-          r.err = t.parse_err;                                           // jwt.ParseSigned error
-        } else if (V.failed[i]) {
-          r.err = V.dev_err;
-        } else {
-          std::string jerr;
-          // parsedJWT.Claims(key, &allClaims): verify, then unmarshal; a JSON
-          // error moves on to the next key, so it ends as "no known key"
-          if (V.any[i] && claims_map(t.payload, &r.claims, &jerr)) {
-            r.ok = true;
-          } else {
-            r.claims = json::Value();
-            r.err = "no known key successfully validated the token signature";
-          }
-        }
-        if (post) (*post)(r, t.view());
-      }
-    });
-    pt.lap("payload-json");
-    V.toks.release();
-    pt.lap("free-toks");
-    return res;
+    recover_after(eng_, *V);
+    return V;
   }
+  void finish(const Verified& V, size_t i, Result& r) override {
+    const Tok& t = V.toks[i];
+    if (!t.parsed) {
+      r.err = t.parse_err;                                           // jwt.ParseSigned error
+    } else if (V.failed[i]) {
+      r.err = V.dev_err;
+    } else {
+      std::string jerr;
+      // parsedJWT.Claims(key, &allClaims): verify, then unmarshal; a JSON
+      // error moves on to the next key, so it ends as "no known key"
+      if (V.any[i] && claims_map(t.payload, &r.claims, &jerr)) {
+        r.ok = true;
+      } else {
+        r.claims = json::Value();
+        r.err = "no known key successfully validated the token signature";
+      }
+    }
+  }
+  const char* trace_name() const override { return "static"; }
 
  private:
   std::vector<PublicKey> keys_;
   std::vector<int> fam_;
   Engine eng_;
-  std::mutex mu_;
 };
 
 // ---------------------------------------------------------------- JWKS key set (go-oidc v2.2.1 remoteKeySet)
@@ -684,52 +708,45 @@ class JSONWebKeySet final : public KeySet {
       : url_(std::move(url)), ca_(std::move(ca)), fetch_(std::move(f)), eng_(devices) {}
 
   void WaitTables() override { eng_.wait_tables(); }
-  Results verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) override {
-    std::lock_guard<std::mutex> g(mu_);
-    Verified V;
-    std::string miss_err;
-    remote_verify(tokens, &V, &miss_err);
-    Results res(tokens.size(), eng_.threads());
-    PhaseTimer pt("jwks");
-    parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) {
-        const Tok& t = V.toks[i];
-        Result& r = res[i];
-        if (!t.parsed) {
-          r.err = "oidc: malformed jwt: " + t.parse_err;
-        } else if (V.failed[i]) {
-          r.err = V.dev_err;
-        } else if (!V.any[i]) {
-          r.err = miss_err;
-        } else {
-          std::string jerr;       // jsonWebKeySet.VerifySignature: json.Unmarshal(payload)
-          if (claims_map(t.payload, &r.claims, &jerr)) r.ok = true;
-          else { r.claims = json::Value(); r.err = jerr; }
-        }
-        if (post) (*post)(r, t.view());
-      }
-    });
-    pt.lap("payload-json");
-    V.toks.release();
-    pt.lap("free-toks");
-    return res;
+  std::string DeviceStatus() override { return eng_.status(); }
+  int DeviceRecoveries() override { return eng_.recoveries(); }
+  int DebugFailVerify(int n) override { return eng_.debug_fail_verify(n); }
+  std::shared_ptr<Verified> verify_raw(const std::vector<std::string_view>& tokens) override {
+    auto V = std::make_shared<Verified>();
+    remote_verify(tokens, V.get(), &V->miss_err);
+    return V;
   }
+  void finish(const Verified& V, size_t i, Result& r) override {
+    const Tok& t = V.toks[i];
+    if (!t.parsed) {
+      r.err = "oidc: malformed jwt: " + t.parse_err;
+    } else if (V.failed[i]) {
+      r.err = V.dev_err;
+    } else if (!V.any[i]) {
+      r.err = V.miss_err;
+    } else {
+      std::string jerr;       // jsonWebKeySet.VerifySignature: json.Unmarshal(payload)
+      if (claims_map(t.payload, &r.claims, &jerr)) r.ok = true;
+      else { r.claims = json::Value(); r.err = jerr; }
+    }
+  }
+  const char* trace_name() const override { return "jwks"; }
 
-  // go-oidc remoteKeySet.VerifySignature itself: the verified payload bytes
+  // go-oidc remoteKeySet.VerifySignature itself: token i's verified payload bytes
+  static PayloadResult payload_result(const Verified& V, size_t i) {
+    PayloadResult r;
+    const Tok& t = V.toks[i];
+    if (!t.parsed) r.err = "oidc: malformed jwt: " + t.parse_err;
+    else if (V.failed[i]) r.err = V.dev_err;
+    else if (!V.any[i]) r.err = V.miss_err;
+    else { r.ok = true; r.payload = std::string(t.payload); }
+    return r;
+  }
   std::vector<PayloadResult> verify_payload_batch(const std::vector<std::string_view>& tokens) {
-    std::lock_guard<std::mutex> g(mu_);
-    Verified V;
-    std::string miss_err;
-    remote_verify(tokens, &V, &miss_err);
+    auto V = verify_raw(tokens);
     std::vector<PayloadResult> res(tokens.size());
     parallel_for(tokens.size(), eng_.threads(), [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) {
-        Tok& t = V.toks[i];
-        if (!t.parsed) res[i].err = "oidc: malformed jwt: " + t.parse_err;
-        else if (V.failed[i]) res[i].err = V.dev_err;
-        else if (!V.any[i]) res[i].err = miss_err;
-        else { res[i].ok = true; res[i].payload = std::string(t.payload); }
-      }
+      for (size_t i = lo; i < hi; ++i) res[i] = payload_result(*V, i);
     });
     return res;
   }
@@ -738,6 +755,15 @@ class JSONWebKeySet final : public KeySet {
   // remoteKeySet.verify over a batch: kid-filtered keys from the cache, then
   // (for the tokens that missed) one refresh if the cache has expired and a
   // retry.  *miss_err = the error every unverified, parsed token gets.
+  //
+  // Concurrency: the key list (keys_, fam_) is read under a shared lock from
+  // candidate selection until the jobs are queued (gpu_verify), and replaced
+  // under the exclusive lock by refresh() -- a refresh never waits for a device
+  // call, and no call's jobs can name a key of a list the device does not hold.
+  // Refreshes are serialised.  As in go-oidc, the expiry a call tests is the
+  // one it read with the cached keys; a call that needs remote keys while
+  // another call's refresh completed since its read takes that refresh's
+  // outcome (go-oidc's keysFromRemote shares an in-flight request the same way).
   void remote_verify(const std::vector<std::string_view>& tokens, Verified* V, std::string* miss_err) {
     auto cand = [&](const Tok& t, std::vector<uint16_t>& out) {
       // remoteKeySet.verify: keyID == "" || key.KeyID == keyID   [R31, R34]
@@ -745,11 +771,18 @@ class JSONWebKeySet final : public KeySet {
       for (size_t k = 0; k < keys_.size(); ++k)
         if ((t.kid.empty() || keys_[k].kid == t.kid) && fam_[k] == fam) out.push_back((uint16_t)k);
     };
-    if (have_keys_) {
-      gpu_verify(eng_, tokens, V, cand);
-    } else {
-      gpu_verify(eng_, tokens, V, [](const Tok&, std::vector<uint16_t>&) {});
+    uint64_t seen_refreshes;
+    int64_t seen_expiry;
+    bool seen_have;
+    {
+      std::shared_lock<std::shared_mutex> lk(keys_mu_);
+      seen_refreshes = refreshes_;
+      seen_expiry = expiry_ns_;
+      seen_have = have_keys_;
+      if (have_keys_) gpu_verify(eng_, tokens, V, cand, nullptr, &lk);
+      else gpu_verify(eng_, tokens, V, [](const Tok&, std::vector<uint16_t>&) {}, nullptr, &lk);
     }
+    recover_after(eng_, *V);
     // tokens that parsed but did not verify: refresh once if the cache has
     // expired (now + keysExpiryDelta(30s) after expiry), then retry them.  A
     // token whose device call failed is no miss: it keeps the device error and
@@ -759,15 +792,31 @@ class JSONWebKeySet final : public KeySet {
       if (V->toks[i].parsed && !V->any[i] && !V->failed[i]) miss.push_back(i);
     std::string fetch_err;
     bool refreshed = false;
-    if (!miss.empty() && (!have_keys_ || wall_now_ns() + 30 * kSecond > expiry_ns_)) {
+    if (!miss.empty() && (!seen_have || wall_now_ns() + 30 * kSecond > seen_expiry)) {
       refreshed = true;
-      if (refresh(&fetch_err)) gpu_verify(eng_, tokens, V, cand, &miss);
+      std::lock_guard<std::mutex> rg(refresh_mu_);
+      bool ok;
+      if (refreshes_ != seen_refreshes) {            // joined a refresh that completed meanwhile
+        ok = last_refresh_ok_;
+        fetch_err = last_fetch_err_;
+      } else {
+        ok = refresh(&fetch_err);
+        std::unique_lock<std::shared_mutex> lk(keys_mu_);
+        ++refreshes_;
+        last_refresh_ok_ = ok;
+        last_fetch_err_ = fetch_err;
+      }
+      if (ok) {
+        std::shared_lock<std::shared_mutex> lk(keys_mu_);
+        gpu_verify(eng_, tokens, V, cand, &miss, &lk);
+      }
     }
+    recover_after(eng_, *V);
     *miss_err = refreshed && !fetch_err.empty() ? "fetching keys " + fetch_err : "failed to verify id token signature";
   }
 
+  // go-oidc updateKeys; the caller holds refresh_mu_
   bool refresh(std::string* err) {
-    // go-oidc updateKeys
     FetchResponse resp;
     try {
       resp = fetch_(url_, ca_);
@@ -779,11 +828,15 @@ class JSONWebKeySet final : public KeySet {
       *err = "oidc: get keys failed: " + resp.status_text + " " + resp.body;
       return false;
     }
+    const int64_t expiry = wall_now_ns() + (resp.max_age_s > 0 ? resp.max_age_s * kSecond : 0);
     // an unchanged document (the usual refresh-on-miss answer for a tampered
     // token): the cached keys stand as they are -- no decode, no device work
-    if (have_keys_ && resp.body == body_) {
-      expiry_ns_ = wall_now_ns() + (resp.max_age_s > 0 ? resp.max_age_s * kSecond : 0);
-      return true;
+    {
+      std::unique_lock<std::shared_mutex> lk(keys_mu_);
+      if (have_keys_ && resp.body == body_) {
+        expiry_ns_ = expiry;
+        return true;
+      }
     }
     std::vector<JSONWebKey> keys;
     std::string derr;
@@ -801,6 +854,7 @@ class JSONWebKeySet final : public KeySet {
       pk.push_back(k.key);
       fam.push_back(key_family(k.key));
     }
+    std::unique_lock<std::shared_mutex> lk(keys_mu_);
     try {
       eng_.load(pk);
     } catch (const std::exception& e) {
@@ -811,19 +865,23 @@ class JSONWebKeySet final : public KeySet {
     keys_ = std::move(keys);
     body_ = std::move(resp.body);
     have_keys_ = true;
-    expiry_ns_ = wall_now_ns() + (resp.max_age_s > 0 ? resp.max_age_s * kSecond : 0);
+    expiry_ns_ = expiry;
     return true;
   }
 
   std::string url_, ca_;
   Fetcher fetch_;
   Engine eng_;
-  std::mutex mu_;
+  std::shared_mutex keys_mu_;     // keys_, fam_, body_, have_keys_, expiry_ns_, refreshes_, last_*
+  std::mutex refresh_mu_;         // one refresh at a time
   std::vector<JSONWebKey> keys_;
   std::vector<int> fam_;
   std::string body_;              // the JWKS document keys_ came from
   bool have_keys_ = false;
   int64_t expiry_ns_ = 0;
+  uint64_t refreshes_ = 0;        // refresh attempts completed
+  bool last_refresh_ok_ = false;  // ... and the last one's outcome
+  std::string last_fetch_err_;
 };
 
 // ---------------------------------------------------------------- Go time arithmetic
@@ -885,46 +943,264 @@ bool fold_eq(const std::string& key, const char* upper_field) {
 }  // namespace
 
 // ====================================================================== Engine
-Engine::Engine(const std::vector<int>& devices) {
+Engine::Engine(const std::vector<int>& devices) : devices_(devices) {
   ctx_ = jg_create(devices.empty() ? nullptr : devices.data(), (int)devices.size());
   if (!ctx_) throw std::runtime_error(std::string("capjwt: no GPU verifier: ") + jg_last_error(nullptr));
   threads_ = host_threads();
 }
 
 Engine::~Engine() {
-  if (pinned_) jg_host_free(pinned_);
+  for (auto& b : pin_free_) jg_host_free(b.first);
   if (ctx_) jg_destroy(ctx_);
 }
 
-void Engine::wait_tables() { (void)jg_keys_wait_tables(ctx_); }
+void Engine::wait_tables() {
+  std::shared_lock<std::shared_mutex> life(life_);
+  if (ctx_) (void)jg_keys_wait_tables(ctx_);
+}
 
 void Engine::load(const std::vector<PublicKey>& keys) {
   std::vector<jg_key> jk;
   jk.reserve(keys.size());
   for (const auto& k : keys) jk.push_back(to_jg(k));
-  if (jg_keys_load(ctx_, jk.data(), (int)jk.size()) != 0)
-    throw std::runtime_error(std::string("capjwt: jg_keys_load: ") + jg_last_error(ctx_));
+  std::shared_lock<std::shared_mutex> life(life_);
+  std::lock_guard<std::mutex> g(load_mu_);
+  if (!ctx_) throw DeviceError("capjwt: device lost: " + lost_);
+  const int rc = jg_keys_load(ctx_, jk.data(), (int)jk.size());
+  if (rc != 0) throw std::runtime_error(std::string("capjwt: jg_keys_load: ") + jg_last_error(ctx_));
+  keys_ = keys;
+  has_keys_ = true;
 }
 
-uint8_t* Engine::arena_buffer(size_t bytes) {
-  if (bytes > pinned_cap_) {
-    if (pinned_) jg_host_free(pinned_);
-    pinned_cap_ = std::max(bytes, pinned_cap_ * 3 / 2);
-    pinned_ = (uint8_t*)jg_host_alloc(pinned_cap_);
-    if (!pinned_) throw std::runtime_error("capjwt: pinned host allocation failed");
+Engine::Pinned Engine::pinned(size_t bytes) {
+  bytes = std::max<size_t>(bytes, 1);
+  {
+    std::lock_guard<std::mutex> g(pin_mu_);
+    // the smallest free block that holds it
+    size_t best = pin_free_.size();
+    for (size_t i = 0; i < pin_free_.size(); ++i)
+      if (pin_free_[i].second >= bytes && (best == pin_free_.size() || pin_free_[i].second < pin_free_[best].second))
+        best = i;
+    if (best < pin_free_.size()) {
+      auto b = pin_free_[best];
+      pin_free_.erase(pin_free_.begin() + (std::ptrdiff_t)best);
+      return Pinned(this, b.first, b.second);
+    }
   }
-  return pinned_;
+  // 64 KiB granules, 1/8 headroom: a stream of similar batches reuses one block
+  const size_t cap = ((bytes + bytes / 8) + 65535) & ~size_t(65535);
+  uint8_t* p = (uint8_t*)jg_host_alloc(cap);
+  if (!p) throw std::runtime_error("capjwt: pinned host allocation failed");
+  return Pinned(this, p, cap);
 }
 
-void Engine::verify(const uint8_t* arena, size_t arena_len, const void* jobs, size_t njobs, uint8_t* verdicts) {
-  std::lock_guard<std::mutex> g(mu_);
-  const int rc = jg_verify_batch(ctx_, arena, arena_len, (const jg_tok*)jobs, njobs, verdicts);
-  if (rc != 0) throw std::runtime_error(std::string("capjwt: jg_verify_batch: ") + jg_last_error(ctx_));
+Engine::Pinned::~Pinned() {
+  if (!p_) return;
+  std::lock_guard<std::mutex> g(e_->pin_mu_);
+  // keep a few blocks (one per concurrent call, typically); drop the smallest beyond that
+  e_->pin_free_.emplace_back(p_, cap_);
+  if (e_->pin_free_.size() > 4) {
+    auto it = std::min_element(e_->pin_free_.begin(), e_->pin_free_.end(),
+                               [](const auto& x, const auto& y) { return x.second < y.second; });
+    jg_host_free(it->first);
+    e_->pin_free_.erase(it);
+  }
+}
+
+void Engine::fail_device(const std::string& what) {
+  errors_.fetch_add(1);
+  throw DeviceError(what);
+}
+
+void Engine::verify(const uint8_t* arena, size_t arena_len, const void* jobs, size_t njobs, uint8_t* verdicts,
+                    const std::function<void()>& submitted) {
+  // a lost context: try to recreate it (at most once a second) before failing
+  bool lost;
+  uint64_t seen;
+  {
+    std::shared_lock<std::shared_mutex> life(life_);
+    lost = ctx_ == nullptr;
+    seen = errors_.load();
+  }
+  if (lost) {
+    bool retry;
+    {
+      std::unique_lock<std::shared_mutex> life(life_);
+      retry = std::chrono::steady_clock::now() - last_try_ > std::chrono::seconds(1);
+    }
+    if (retry) (void)recover(seen + 1);
+  }
+  std::shared_lock<std::shared_mutex> life(life_);
+  if (!ctx_) {
+    if (submitted) submitted();
+    fail_device("capjwt: device lost: " + lost_);
+  }
+  jg_ticket* t = nullptr;
+  const int rc = jg_submit(ctx_, arena, arena_len, (const jg_tok*)jobs, njobs, verdicts, &t);
+  if (submitted) submitted();
+  if (rc == -1) throw std::logic_error(std::string("capjwt: jg_submit rejected the host's jobs: ") + jg_last_error(ctx_));
+  if (rc != 0) fail_device(std::string("capjwt: jg_verify_batch: ") + jg_last_error(ctx_));
+  const int wc = jg_wait(ctx_, t);
+  if (wc == -1) throw std::logic_error(std::string("capjwt: jg_wait rejected the host's jobs: ") + jg_last_error(ctx_));
+  if (wc != 0) fail_device(std::string("capjwt: jg_verify_batch: ") + jg_last_error(ctx_));
+}
+
+bool Engine::recover(uint64_t seen) {
+  std::unique_lock<std::shared_mutex> life(life_);
+  if (recovered_at_ >= seen && ctx_) return true;          // already recovered since that error
+  last_try_ = std::chrono::steady_clock::now();
+  if (ctx_) jg_destroy(ctx_);                              // its streams, workers, staged tables
+  ctx_ = jg_create(devices_.empty() ? nullptr : devices_.data(), (int)devices_.size());
+  recovered_at_ = errors_.load();
+  if (!ctx_) {
+    lost_ = std::string("jg_create: ") + jg_last_error(nullptr);
+    return false;
+  }
+  if (has_keys_) {
+    std::vector<jg_key> jk;
+    jk.reserve(keys_.size());
+    for (const auto& k : keys_) jk.push_back(to_jg(k));
+    if (jg_keys_load(ctx_, jk.data(), (int)jk.size()) != 0) {
+      lost_ = std::string("jg_keys_load: ") + jg_last_error(ctx_);
+      jg_destroy(ctx_);
+      ctx_ = nullptr;
+      return false;
+    }
+  }
+  lost_.clear();
+  recoveries_.fetch_add(1);
+  return true;
+}
+
+std::string Engine::status() {
+  std::shared_lock<std::shared_mutex> life(life_);
+  return ctx_ ? std::string() : lost_.empty() ? std::string("device lost") : lost_;
+}
+
+int Engine::debug_fail_verify(int n) {
+  std::shared_lock<std::shared_mutex> life(life_);
+  return ctx_ ? jg_debug_fail_verify(ctx_, n) : -1;
+}
+
+// ====================================================================== request coalescing
+void Coalescer::configure(const CoalesceConfig& c) {
+  std::lock_guard<std::mutex> g(m_);
+  cfg_ = c;
+  cfg_.max_inflight = std::max(1, cfg_.max_inflight);
+  cfg_.max_batch = std::max<size_t>(1, cfg_.max_batch);
+  cfg_.window_us = std::max<int64_t>(0, cfg_.window_us);
+}
+
+CoalesceConfig Coalescer::config() {
+  std::lock_guard<std::mutex> g(m_);
+  return cfg_;
+}
+
+Coalescer::Stats Coalescer::stats() {
+  std::lock_guard<std::mutex> g(m_);
+  return st_;
+}
+
+void Coalescer::run(Req* r) {
+  std::unique_lock<std::mutex> lk(m_);
+  q_.push_back(r);
+  ++st_.calls;
+  window_cv_.notify_one();                       // a leader collecting a window may want it
+  while (!r->done) {
+    if (leaders_ < cfg_.max_inflight && !q_.empty()) {
+      // lead one batch: everything queued (FIFO), up to max_batch
+      ++leaders_;
+      if (cfg_.window_us > 0 && q_.size() < cfg_.max_batch) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(cfg_.window_us);
+        window_cv_.wait_until(lk, until, [&] { return q_.size() >= cfg_.max_batch; });
+      }
+      std::vector<Req*> batch;
+      const size_t take = std::min(q_.size(), cfg_.max_batch);
+      batch.assign(q_.begin(), q_.begin() + (std::ptrdiff_t)take);
+      q_.erase(q_.begin(), q_.begin() + (std::ptrdiff_t)take);
+      ++st_.batches;
+      st_.max_batch_seen = std::max<uint64_t>(st_.max_batch_seen, take);
+      lk.unlock();
+      std::exception_ptr ex;
+      std::shared_ptr<const Verified> V;
+      try {
+        std::vector<std::string_view> toks;
+        toks.reserve(batch.size());
+        for (Req* x : batch) toks.push_back(x->tok);
+        V = exec_(toks);
+      } catch (...) {
+        ex = std::current_exception();
+      }
+      lk.lock();
+      for (size_t i = 0; i < batch.size(); ++i) {
+        Req* x = batch[i];
+        x->batch = V;
+        x->idx = i;
+        x->ex = ex;                              // a host-side bug in the batch reaches every caller in it
+        x->done = true;
+        if (x != r) x->cv.notify_one();
+      }
+      --leaders_;
+      // hand the lead to the oldest waiting caller, if any
+      if (!q_.empty()) q_.front()->cv.notify_one();
+    } else {
+      r->cv.wait(lk);
+    }
+  }
+  if (r->ex) std::rethrow_exception(r->ex);
 }
 
 // ====================================================================== KeySet
+KeySet::KeySet()
+    : co_([this](const std::vector<std::string_view>& toks) -> std::shared_ptr<const Verified> {
+        return verify_raw(toks);
+      }) {}
+
+Results KeySet::verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) {
+  std::shared_ptr<Verified> V = verify_raw(tokens);
+  const int th = host_threads();
+  Results res(tokens.size(), th);
+  PhaseTimer pt(trace_name());
+  parallel_for(tokens.size(), th, [&](size_t lo, size_t hi) {
+    auto arena = std::make_unique<json::Arena>();   // this range's claims trees (owned by res)
+    json::ArenaScope scope(arena.get());
+    res.adopt(std::move(arena));
+    for (size_t i = lo; i < hi; ++i) {
+      finish(*V, i, res[i]);
+      if (post) (*post)(i, res[i], V->toks[i].view());
+    }
+  });
+  pt.lap("payload-json");
+  V->toks.release();
+  pt.lap("free-toks");
+  return res;
+}
+
+// One token of a coalesced batch: the leader ran parse + device verify for
+// everyone; the claims map is built here, on the caller's own thread, straight
+// into heap storage (it leaves the batch with the caller)
 Result KeySet::VerifySignature(std::string_view token) {
-  return std::move(verify_batch({token}, nullptr)[0]);
+  Coalescer::Req q;
+  q.tok = token;
+  co_.run(&q);
+  Result r;
+  finish(*q.batch, q.idx, r);
+  return r;
+}
+
+Result KeySet::verify_one(std::string_view token, TokenInfo* info) {
+  Coalescer::Req q;
+  q.tok = token;
+  co_.run(&q);
+  Result r;
+  finish(*q.batch, q.idx, r);
+  const TokenView t = q.batch->toks[q.idx].view();
+  info->parsed = t.parsed;
+  info->parse_err = std::string(t.parse_err);
+  info->nsigs = t.nsigs;
+  info->sig0_len = t.sig0_len;
+  info->alg = std::string(t.alg);
+  return r;
 }
 
 Results KeySet::VerifySignatureBatch(const std::vector<std::string_view>& tokens) {
@@ -948,16 +1224,27 @@ std::unique_ptr<KeySet> NewJSONWebKeySet(const std::string& jwks_url, const std:
 // go-oidc's oidc.KeySet over the same GPU JWKS machinery
 class RemoteKeySet::Impl {
  public:
-  Impl(const std::string& url, Fetcher f, const std::vector<int>& devices) : ks(url, "", std::move(f), devices) {}
+  Impl(const std::string& url, Fetcher f, const std::vector<int>& devices)
+      : ks(url, "", std::move(f), devices),
+        co([this](const std::vector<std::string_view>& toks) -> std::shared_ptr<const Verified> {
+          return ks.verify_raw(toks);
+        }) {}
   JSONWebKeySet ks;
+  Coalescer co;
 };
 RemoteKeySet::RemoteKeySet(const std::string& jwks_url, Fetcher fetch, const std::vector<int>& devices)
     : impl_(std::make_unique<Impl>(jwks_url, std::move(fetch), devices)) {}
 RemoteKeySet::~RemoteKeySet() = default;
-PayloadResult RemoteKeySet::VerifySignature(std::string_view jwt) { return impl_->ks.verify_payload_batch({jwt})[0]; }
+PayloadResult RemoteKeySet::VerifySignature(std::string_view jwt) {
+  Coalescer::Req q;
+  q.tok = jwt;
+  impl_->co.run(&q);
+  return JSONWebKeySet::payload_result(*q.batch, q.idx);
+}
 std::vector<PayloadResult> RemoteKeySet::VerifySignatureBatch(const std::vector<std::string_view>& jwts) {
   return impl_->ks.verify_payload_batch(jwts);
 }
+void RemoteKeySet::SetCoalescing(const CoalesceConfig& c) { impl_->co.configure(c); }
 std::unique_ptr<RemoteKeySet> NewRemoteKeySet(const std::string& jwks_url, Fetcher fetch,
                                               const std::vector<int>& devices) {
   return std::make_unique<RemoteKeySet>(jwks_url, std::move(fetch), devices);
@@ -1186,8 +1473,20 @@ Result validate_claims(const json::Value& all_claims, const TokenView& info, con
 
 void release_results(Results& rs) { rs.release(); }
 
+// jwt/jwt.go:95-202 for one token: the signature through the key set's
+// coalescer (concurrent Validate calls share device batches), the claim
+// checks on the caller's thread with the caller's Expected
 Result Validator::Validate(std::string_view token, const Expected& expected) {
-  return std::move(ValidateBatch({token}, expected)[0]);
+  TokenInfo info;
+  Result r = ks_->verify_one(token, &info);
+  if (!r.ok) {
+    r.err = "error verifying token signature: " + r.err;
+    return r;
+  }
+  const int64_t now = expected.has_now ? expected.now_unix_ns : wall_now_ns();
+  Result v = validate_claims(r.claims, info, expected, now);
+  if (v.ok) v.claims = std::move(r.claims);
+  return v;
 }
 
 Results Validator::ValidateBatch(const std::vector<std::string_view>& tokens, const Expected& expected) {
@@ -1195,7 +1494,7 @@ Results Validator::ValidateBatch(const std::vector<std::string_view>& tokens, co
   // the claim checks run inside the key set's per-token pass, on the host
   // threads, while each token's claims map is still in cache; a claims map
   // that fails validation is destroyed there
-  const PostFn post = [&](Result& r, const TokenView& t) {
+  const PostFn post = [&](size_t, Result& r, const TokenView& t) {
     if (!r.ok) {
       r.err = "error verifying token signature: " + r.err;
       return;
@@ -1209,9 +1508,11 @@ Results Validator::ValidateBatch(const std::vector<std::string_view>& tokens, co
 
 // ====================================================================== oidc hash claims
 void Engine::hash(const uint8_t* arena, size_t arena_len, const void* jobs, size_t njobs, uint8_t* digests) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::shared_lock<std::shared_mutex> life(life_);
+  if (!ctx_) fail_device("capjwt: device lost: " + lost_);
   const int rc = jg_hash_batch(ctx_, arena, arena_len, (const jg_hjob*)jobs, njobs, digests);
-  if (rc != 0) throw std::runtime_error(std::string("capjwt: jg_hash_batch: ") + jg_last_error(ctx_));
+  if (rc == -1) throw std::logic_error(std::string("capjwt: jg_hash_batch rejected the host's jobs: ") + jg_last_error(ctx_));
+  if (rc != 0) fail_device(std::string("capjwt: jg_hash_batch: ") + jg_last_error(ctx_));
 }
 
 namespace {
@@ -1366,11 +1667,12 @@ std::vector<HashClaimResult> verify_hash_claim_batch(Engine& eng, const std::str
     std::vector<uint8_t> dig(64 * idx.size());
     try {
       eng.hash((const uint8_t*)arena.data(), arena.size(), jobs.data(), jobs.size(), dig.data());
-    } catch (const std::exception& e) {
+    } catch (const DeviceError& e) {
       // degraded path, as the key sets': the pairs that needed the device get
-      // its error, the batch returns
+      // its error, the batch returns, and the context is recreated for the next
       for (size_t i : idx) out[i].err = std::string("capjwt: hash unavailable: ") + e.what();
       idx.clear();
+      (void)eng.recover(eng.errors());
     }
     parallel_for(idx.size(), host_threads(), [&](size_t lo, size_t hi) {
       for (size_t k = lo; k < hi; ++k) {

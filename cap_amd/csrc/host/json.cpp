@@ -3,6 +3,8 @@
 // decodes anything, so a syntax error anywhere rejects the document).
 #include "json.hpp"
 
+#include "hostmem.hpp"
+
 #include <algorithm>
 #include <cerrno>
 #include <charconv>
@@ -14,6 +16,38 @@
 
 namespace capjwt {
 namespace json {
+
+// ---------------------------------------------------------------- arenas
+namespace {
+thread_local Arena* tl_arena = nullptr;
+}  // namespace
+
+Arena* current_arena() { return tl_arena; }
+ArenaScope::ArenaScope(Arena* a) : prev_(tl_arena) { tl_arena = a; }
+ArenaScope::~ArenaScope() { tl_arena = prev_; }
+
+Arena::~Arena() {
+  for (void* b : blocks_) hostmem::block_put(b);
+  for (void* b : big_) ::operator delete(b);
+}
+
+void* Arena::alloc(size_t bytes) {
+  bytes = (bytes + 15) & ~size_t(15);
+  used_ += bytes;
+  if (bytes > hostmem::kBlock / 4) {               // a huge object: its own allocation
+    big_.push_back(::operator new(bytes));
+    return big_.back();
+  }
+  if (bytes > left_) {
+    blocks_.push_back(hostmem::block_get());
+    cur_ = static_cast<char*>(blocks_.back());
+    left_ = hostmem::kBlock;
+  }
+  void* r = cur_;
+  cur_ += bytes;
+  left_ -= bytes;
+  return r;
+}
 
 const Value* Value::get(std::string_view key) const {
   if (kind != Object) return nullptr;

@@ -10,7 +10,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
 
 #include "cap_jwt.hpp"
 
@@ -273,6 +276,9 @@ PYBIND11_MODULE(_capjwt_host, m) {
     return result_py(r);
   });
   m.def("host_threads", &host_threads);
+  m.def("set_host_memory_retention", &SetHostMemoryRetention);
+  m.def("trim_host_memory", &TrimHostMemory);
+  m.def("host_memory_retained", &HostMemoryRetained);
   m.def("available_cpus", &available_cpus);
 
   // ---- GPU-backed key sets and validator
@@ -298,6 +304,29 @@ PYBIND11_MODULE(_capjwt_host, m) {
       .def("wait_tables", [](PyKeySet& s) {
         py::gil_scoped_release rel;
         s.ks->WaitTables();
+      })
+      .def("set_coalescing", [](PyKeySet& s, int max_inflight, size_t max_batch, int64_t window_us) {
+        CoalesceConfig c;
+        c.max_inflight = max_inflight;
+        c.max_batch = max_batch;
+        c.window_us = window_us;
+        s.ks->SetCoalescing(c);
+      }, py::arg("max_inflight") = 2, py::arg("max_batch") = 65536, py::arg("window_us") = 0)
+      .def("coalescing_stats", [](PyKeySet& s) {
+        const auto st = s.ks->CoalescingStats();
+        py::dict d;
+        d["calls"] = st.calls;
+        d["batches"] = st.batches;
+        d["max_batch"] = st.max_batch_seen;
+        return d;
+      })
+      .def("device_status", [](PyKeySet& s) {
+        py::gil_scoped_release rel;
+        return s.ks->DeviceStatus();
+      })
+      .def("device_recoveries", [](PyKeySet& s) { return s.ks->DeviceRecoveries(); })
+      .def("_debug_fail_verify", [](PyKeySet& s, int n) {
+        if (s.ks->DebugFailVerify(n) != 0) throw py::value_error("jg_debug_fail_verify failed");
       });
 
   m.def("new_static_keyset", [](const std::vector<PublicKey>& keys, const std::vector<int>& devices) {
@@ -379,7 +408,61 @@ PYBIND11_MODULE(_capjwt_host, m) {
           lap("release");
         }
         return py::bytes(ok);
-      });
+      })
+      .def("_concurrent_validate", [](PyValidator& s, py::bytes blob, const Expected& e, int callers,
+                                      int64_t total) {
+        // Measurement helper (bench.py `single`): `callers` host threads, each
+        // calling Validator::Validate once per token -- the goroutine-per-
+        // request pattern of an unchanged cap caller -- over `total` tokens
+        // taken round-robin from the newline-separated pool.  Returns the
+        // wall time, accepts and per-call latency percentiles.
+        char* bp = nullptr;
+        Py_ssize_t bn = 0;
+        if (PyBytes_AsStringAndSize(blob.ptr(), &bp, &bn) != 0) throw py::error_already_set();
+        callers = std::max(1, callers);
+        std::vector<std::vector<int64_t>> lat(callers);
+        std::vector<int64_t> acc(callers, 0);
+        double wall = 0;
+        {
+          py::gil_scoped_release rel;
+          const auto toks = split_lines(bp, (size_t)bn);
+          if (toks.empty()) throw std::runtime_error("empty token pool");
+          std::atomic<int64_t> next{0};
+          std::vector<std::thread> th;
+          const auto t0 = std::chrono::steady_clock::now();
+          for (int c = 0; c < callers; ++c)
+            th.emplace_back([&, c] {
+              lat[c].reserve((size_t)(total / callers + 16));
+              while (true) {
+                const int64_t i = next.fetch_add(1);
+                if (i >= total) break;
+                const auto a = std::chrono::steady_clock::now();
+                Result r = s.v->Validate(toks[(size_t)i % toks.size()], e);
+                const auto b = std::chrono::steady_clock::now();
+                lat[c].push_back(std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count());
+                acc[c] += r.ok;
+              }
+            });
+          for (auto& t : th) t.join();
+          wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        }
+        std::vector<int64_t> all;
+        for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+        std::sort(all.begin(), all.end());
+        auto pct = [&](double q) { return all.empty() ? 0.0 : (double)all[std::min(all.size() - 1, (size_t)(q * (double)all.size()))] / 1e3; };
+        int64_t accepted = 0;
+        for (auto a : acc) accepted += a;
+        py::dict d;
+        d["wall_s"] = wall;
+        d["calls"] = (int64_t)all.size();
+        d["accepted"] = accepted;
+        d["p50_us"] = pct(0.50);
+        d["p90_us"] = pct(0.90);
+        d["p99_us"] = pct(0.99);
+        d["p999_us"] = pct(0.999);
+        d["max_us"] = all.empty() ? 0.0 : (double)all.back() / 1e3;
+        return d;
+      }, py::arg("blob"), py::arg("expected"), py::arg("callers"), py::arg("total"));
 
   // ---- go-oidc oidc.KeySet adapter (NewRemoteKeySet): payload bytes out
   struct PyRemoteKeySet {
@@ -409,7 +492,14 @@ PYBIND11_MODULE(_capjwt_host, m) {
         py::list out;
         for (const auto& r : rs) out.append(payload_py(r));
         return out;
-      });
+      })
+      .def("set_coalescing", [](PyRemoteKeySet& s, int max_inflight, size_t max_batch, int64_t window_us) {
+        CoalesceConfig c;
+        c.max_inflight = max_inflight;
+        c.max_batch = max_batch;
+        c.window_us = window_us;
+        s.ks->SetCoalescing(c);
+      }, py::arg("max_inflight") = 2, py::arg("max_batch") = 65536, py::arg("window_us") = 0);
   m.def("new_remote_keyset", [](const std::string& url, py::object fetch, const std::vector<int>& devices) {
     auto p = std::make_unique<PyRemoteKeySet>();
     p->ks = NewRemoteKeySet(url, wrap_fetch(std::move(fetch)), devices);

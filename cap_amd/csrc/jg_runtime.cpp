@@ -152,12 +152,8 @@ std::vector<size_t> chunk_cuts(size_t lo, size_t hi, size_t C, size_t first = 40
   std::vector<size_t> cut{lo};
   for (size_t ramp = std::min<size_t>(C, first); cut.back() < hi; ramp = std::min(C, 2 * ramp))
     cut.push_back(std::min(hi, cut.back() + ramp));
-  static const bool split_tail = [] {           // CAPJWT_TAIL_SPLIT=0: never a short last chunk (A/B)
-    const char* e = std::getenv("CAPJWT_TAIL_SPLIT");
-    return !(e && std::atoi(e) == 0);
-  }();
   const size_t tail = C / 4;
-  if (split_tail && tail_chunk && cut.size() > 2 && tail >= 1024 && cut.back() - cut[cut.size() - 2] > tail)
+  if (tail_chunk && cut.size() > 2 && tail >= 1024 && cut.back() - cut[cut.size() - 2] > tail)
     cut.insert(cut.end() - 1, cut.back() - tail);
   return cut;
 }
@@ -563,11 +559,6 @@ struct Slot {
   int grows = 0;                                                // buffer reallocations while enqueuing (trace)
   int chunk_no = 0;
   uint64_t seq = 0;                // enqueue order across both slot rings (oldest completes first)
-  // early arena DMA (process_item): this slot's next chunk's arena span
-  // [pre_base, pre_base + pre_span) is already on its way to bufs.arena
-  bool pre = false;
-  const uint8_t* pre_src = nullptr;
-  uint64_t pre_base = 0, pre_span = 0;
   size_t reserved = 0;             // chunk capacity (jobs) the buffers were sized for
   uint64_t reserved_epoch = ~0ull; // key table they were sized against
   bool inflight = false;
@@ -646,11 +637,8 @@ struct jg_batch {
   size_t marks_used = 0;
   std::vector<std::string> tnames;
   std::vector<float> tms;
-  // class-grouped resident runs (resident_groups): the GroupFan's events
-  std::vector<hipEvent_t> gev;      // [0] lane -> ctrl, [1] start, [2] join -> lane, [3 ..) class done
   ~jg_batch() {
     for (auto e : mark_events) (void)hipEventDestroy(e);
-    for (auto e : gev) (void)hipEventDestroy(e);
   }
 };
 
@@ -665,6 +653,11 @@ struct jg_ctx {
   std::atomic<size_t> zc_max{zc_env_max_jobs()};
   std::atomic<uint64_t> table_budget{default_table_budget()};   // HBM for key comb tables, all curves
   std::atomic<int> fail_alloc{0};            // jg_debug_fail_alloc countdown
+  // jg_debug_fail_verify: countdown to an injected device failure of a
+  // submission; once it fires the context is `poisoned` (every later
+  // submission fails, as after a sticky HIP error) until it is destroyed
+  std::atomic<int> fail_verify{0};
+  std::atomic<bool> poisoned{false};
   // jg_debug_max_upgrades: background table upgrades left before the upgrader
   // stops (-1 = no limit); CAPJWT_DEBUG_MAX_UPGRADES sets the initial value
   std::atomic<int> upgrades_left{[] {
@@ -768,33 +761,13 @@ void rebuild_class_tables(KeyState& K) {
 // lane of the chunk's costliest group once every class is done.  A group's launches from consecutive chunks
 // queue on one lane (one hardware queue each) while the three groups run side
 // by side; lane-per-chunk instead ran each chunk's classes one after another
-// (~6 ms of serial latency per 262 k mixed chunk).  CAPJWT_CLASS_GROUPS=0:
-// lane per chunk for every submission (A/B).  (The wrong ES512 verdicts once
-// seen in this mode were the P-521 W = 18 lost top-window carry, ecdsa.hpp
-// ec_windows_w, which hit lane-per-chunk runs the same way.)
-bool class_grouping() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPJWT_CLASS_GROUPS");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
-// Where a class-grouped chunk's plan fill runs (everything of the chunk waits
-// for it).  Default: on the group lane expected to drain first -- the one
-// with the least class cost queued (Device::gload).  On the join lane (the
-// round-3 default, CAPJWT_GROUP_CTRL=join) it queued behind the previous
-// chunk's whole RSA-4K chain while the other lanes idled 2-4 ms
-// (profiles/r04_s3/zc_trace); CAPJWT_GROUP_CTRL=copy: on the copy stream.
-enum { CTRL_LEAST = 0, CTRL_JOIN = 1, CTRL_COPY = 2 };
-int group_ctrl() {
-  static const int m = [] {
-    const char* e = std::getenv("CAPJWT_GROUP_CTRL");
-    if (!e) return (int)CTRL_LEAST;
-    const std::string v(e);
-    return v == "copy" ? (int)CTRL_COPY : v == "join" ? (int)CTRL_JOIN : (int)CTRL_LEAST;
-  }();
-  return m;
-}
+// (~6 ms of serial latency per 262 k mixed chunk; profiles/r03_s12).
+// A class-grouped chunk's plan fill (everything of the chunk waits for it)
+// runs on the group lane expected to drain first -- the one with the least
+// class cost queued (Device::gload).  On the join lane (round 3) it queued
+// behind the previous chunk's whole RSA-4K chain while the other lanes idled
+// 2-4 ms; on the copy stream it measured no better (profiles/r04_s3/zc_trace,
+// r04_s4/stream_ctrl_*).
 // Class -> group lane of a class-grouped chunk: RSA-2K and RSA-4K+ on lane 0,
 // RSA-3K and P-384 on lane 1, P-256, P-521 and Ed25519 on lane 2.  In a
 // mixed chunk the small EC launches run far below their stand-alone rate
@@ -802,20 +775,10 @@ int group_ctrl() {
 // lane, made that lane the chunk's critical path: 6.8 of ~7 ms per 524 k
 // chunk, profiles/r04_s9/stream_trace_timeline.txt); this split measured
 // 20.8-21.2 ms per configs[4] stream at 262 k chunks against 22.8-23.2 ms
-// (profiles/r04_s10-s12).  CAPJWT_CLASS_GROUP (A/B): one digit 0-2 per class
-// 1..7 (RSA-2K, RSA-3K, RSA-4K+, P-256, P-384, P-521, Ed25519); the round-3
-// split is "0012222".
-int cls_group(int c) {
-  static const std::array<int, NCLS> g = [] {
-    std::array<int, NCLS> t{};
-    const char* d = "0102122";
-    const char* e = std::getenv("CAPJWT_CLASS_GROUP");
-    if (e && std::strlen(e) == NCLS - 1 && std::strspn(e, "012") == NCLS - 1) d = e;
-    for (int k = 1; k < NCLS; ++k) t[k] = d[k - 1] - '0';
-    return t;
-  }();
-  return g[c];
-}
+// (profiles/r04_s10-s12; the round-3 split put every EC / Ed25519 class on
+// lane 2 and RSA-3K on lane 0).  Indexed by class 0..7.
+constexpr int CLS_GROUP[NCLS] = {0, 0, 1, 0, 2, 1, 2, 2};
+inline int cls_group(int c) { return CLS_GROUP[c]; }
 
 // two or more kernel classes among (a sample of) the jobs
 bool mixed_classes(const KeyState& K, const jg_tok* toks, size_t n) {
@@ -1106,38 +1069,15 @@ Marker marker(jg_batch* b, int cls) {
 // timed resident run) the classes run in sequence on L.stream with a HIP event
 // after each kernel; otherwise classes with work run on their own streams.
 // fanout: run the classes of a mixed plan on the lane's per-class streams
-// (resident batches); pipeline chunks keep them in order on the lane's own
-// stream unless CAPJWT_FANOUT=1 (measurement A/B)
-// CAPJWT_MIDSTATE=0 turns the shared block-0 midstate of the prep kernel off (A/B)
-bool prep_midstate() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPJWT_MIDSTATE");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
+// (resident batches); pipeline chunks that are not class-grouped keep them in
+// order on the lane's own stream (per-class fan-out streams measured 29-31
+// against 25.7 ms per configs[4] stream, profiles/r03_s22_c5_stream_fanout_ab.txt)
 
 // Resident batches alternate between two lanes whose main streams sit on
 // different hardware queues (lane0, lane1), so runs of two staged batches
 // enqueued back to back overlap: one batch's latency-bound front kernels
 // (prep, scalar stage) and tails share the CUs with the other's point kernel
-// (ES256 +6 %, profiles/r03_s9_altlanes_ab.json).  CAPJWT_BATCH_LANES=1 puts
-// every resident batch on lane0 (A/B).
-int batch_lanes() {
-  static const int n = [] {
-    const char* e = std::getenv("CAPJWT_BATCH_LANES");
-    return e ? std::atoi(e) : 2;
-  }();
-  return n;
-}
-
-bool pipeline_fanout() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPJWT_FANOUT");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
-}
+// (ES256 +6 %, profiles/r03_s9_altlanes_ab.json).
 
 // Class-major zero-copy streams (round 4).  A mixed (class-grouped)
 // submission whose arena lies in memory from jg_host_alloc runs as ONE plan
@@ -1160,18 +1100,10 @@ bool pipeline_fanout() {
 // longer item is cut into equal plans; device scratch grows with it, ~5 KB per
 // job with RSA-4K keys).
 //
-// Where the gathers of a zero-copy plan run.  1 (default): all on one feed
-// stream (the copy stream), the costliest class first, so each gather has the
-// link to itself and the longest arithmetic chain starts earliest; each
-// class's chain waits for its own gather on the lane of its class group.  0:
-// each class's gather heads its own chain on its group lane (A/B).
-bool zc_feed() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPJWT_ZC_FEED");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
+// The gathers of a zero-copy plan all run on one feed stream (the copy
+// stream), the costliest class first, so each gather has the link to itself
+// and the longest arithmetic chain starts earliest; each class's chain waits
+// for its own gather on the lane of its class group.
 
 // Runs of consecutive keys of class c (the plan's key order) whose comb tables
 // have one width: fn(begin, end, w) per run, over padded slots.  All of a
@@ -1262,8 +1194,7 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
   pa.status = (uint8_t*)B->status.p;
   pa.siglen = (uint16_t*)B->siglen.p;
   pa.npad = np;
-  pa.mid = prep_midstate() ? (uint32_t*)B->mid.get(sizeof(uint32_t) * PREP_MID_WORDS * (size_t)std::max<int64_t>(P.nkeys, 1))
-                           : nullptr;
+  pa.mid = (uint32_t*)B->mid.get(sizeof(uint32_t) * PREP_MID_WORDS * (size_t)std::max<int64_t>(P.nkeys, 1));
   uint32_t* rows = (uint32_t*)B->rows.p;
   if (conc) HIPCHK(hipEventRecord(L->ev_start, s0));
   const bool zc = gf && gf->zc, feed = zc && gf->feed;
@@ -1579,10 +1510,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   const uint8_t* hbd = (const uint8_t*)S.h_meta.dp;
   const hipStream_t cs = d->copy;
   if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
-  const bool pre = S.pre && compact && !zc && it.dev_arena && src == S.pre_src && dbase == S.pre_base &&
-                   bytes == S.pre_span;
-  S.pre = false;
-  if (bytes && !zc && !pre) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, cs));
+  if (bytes && !zc) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, cs));
   int nact = 0, jgrp = 0;
   double gcost[3] = {0, 0, 0};
   for (int c = 1; c < NCLS; ++c) {
@@ -1612,7 +1540,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
     gf.gather.kstart = (const int64_t*)(dm + L.zc_off + sizeof(uint64_t) * NB);
     gf.gather.kstride = (const uint64_t*)(dm + L.zc_off + 2 * sizeof(uint64_t) * NB);
     gf.gather.dst = (uint8_t*)S.bufs.arena.p;
-    if (zc_feed()) {
+    {
       gf.feed = cs;                                // the copy stream carries no arena copies now
       for (int c = 1; c < NCLS; ++c) {
         gf.fed[c] = S.ev_fed[c];
@@ -1625,8 +1553,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
     int least = 0;
     for (int g = 1; g < 3; ++g)
       if (d->gload[g] < d->gload[least]) least = g;
-    const int cm = group_ctrl();
-    gf.ctrl = cm == CTRL_COPY ? cs : cm == CTRL_JOIN ? gf.join : d->lanes[least].stream;
+    gf.ctrl = d->lanes[least].stream;
     // queued class cost per group lane, relative (the smallest kept at 0)
     double lo = 1e300;
     for (int g = 0; g < 3; ++g) lo = std::min(lo, d->gload[g] += gcost[g]);
@@ -1656,7 +1583,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
     run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, &gf);
     s = gf.join;                                   // verdicts leave once every class is done
   } else {
-    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, pipeline_fanout());
+    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false);
   }
   if (tr) HIPCHK(hipEventRecord(S.tr_c, s));
   S.h_verdict.get(std::max<size_t>(n, 1));
@@ -1672,53 +1599,9 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   S.inflight = true;
 }
 
-// Early arena DMA: right after chunk c is enqueued, the compact arena span of
-// chunk c + 1 goes on the copy stream into the slot that chunk will use, so it
-// travels while the host plans chunk c + 1 (~4 ms of host work for a 524 k-job
-// chunk) and the copies of a pinned stream run back to back
-// (profiles/r04_s9/stream_trace_*).  Only for spans that enqueue_chunk would
-// DMA as they are (compact, inside the caller's arena); it checks that the
-// span it computes matches and otherwise copies as usual.  Measured neutral on
-// the configs[4] stream (20.9-21.6 vs 21.0-21.2 ms at 262 k chunks,
-// profiles/r04_s12/), so off unless CAPJWT_EARLY_DMA=1.
-bool early_dma() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPJWT_EARLY_DMA");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
-}
-
-void prefetch_arena(Device* d, size_t dslot, Slot& N, const Item& it, size_t lo, size_t hi) {
-  const size_t n = hi - lo;
-  if (n == 0) return;
-  const jg_tok* toks = it.toks + lo;
-  uint64_t amin = UINT64_MAX, amax = 0, need = 0;
-  for (size_t i = 0; i < n; ++i) {
-    const uint64_t e = tok_end(toks[i]);
-    amin = std::min<uint64_t>(amin, toks[i].off);
-    amax = std::max<uint64_t>(amax, e);
-    need += e - toks[i].off;
-  }
-  if (amax > it.arena_len) return;                 // a bad job: enqueue_chunk's checks report it
-  const uint64_t base = amin & ~uint64_t(255), span = amax - base;
-  if (!(span <= 2 * need + 65536 && span < (uint64_t(1) << 32) - ARENA_SLACK)) return;
-  finish_slot(N);                                  // its previous chunk (a ring length ago)
-  const KeyState& K = *it.ks;
-  if (N.reserved != it.chunk || N.reserved_epoch != K.epoch) {
-    double bpj = 0;
-    for (size_t i = 0; i < std::min<size_t>(n, 256); ++i) bpj += (double)(tok_end(toks[i]) - toks[i].off);
-    reserve_slot(K, N, std::max(it.chunk, n), K.keys.size() + 1, bpj / (double)std::min<size_t>(n, 256), false);
-  }
-  N.bufs.arena.get((size_t)span + ARENA_SLACK);
-  HIPCHK(hipMemcpyAsync(N.bufs.arena.p, it.arena + base, (size_t)span, hipMemcpyHostToDevice, d->copy));
-  N.pre = true;
-  N.pre_src = it.arena + base;
-  N.pre_base = base;
-  N.pre_span = span;
-  (void)dslot;
-}
-
+// (Issuing the next chunk's arena DMA right after the current chunk's copies
+// measured neutral on the configs[4] stream, 20.9-21.6 vs 21.0-21.2 ms at
+// 262 k chunks, profiles/r04_s12/; not kept.)
 void process_item(Device* d, size_t dslot, Item& it) {
   size_t enq = 0;
   try {
@@ -1748,11 +1631,6 @@ void process_item(Device* d, size_t dslot, Item& it) {
       finish_slot(S);                 // the slot's previous chunk (a ring length ago)
       const double wait_ms = pipe_trace() ? ms_since(tw) : 0.0;
       enqueue_chunk(d, dslot, S, it, it.toks + lo, hi - lo, it.out + lo);
-      // after chunk c's own copies (the copy stream is in order: issued before
-      // them, chunk c + 1's span delayed chunk c by a whole copy, 22.9 -> 26.4 ms
-      // per configs[4] stream, profiles/r04_s11/)
-      if (!it.zc && it.dev_arena && early_dma() && c + 2 < it.cuts.size())
-        prefetch_arena(d, dslot, d->slots[d->next_slot], it, it.cuts[c + 1], it.cuts[c + 2]);
       S.seq = ++d->slot_seq;
       S.host_ms[0] = wait_ms;
       S.chunk_no = (int)enq;
@@ -1763,7 +1641,6 @@ void process_item(Device* d, size_t dslot, Item& it) {
     it.t->fail(-2, e.what());
     it.t->done_chunks(it.nchunks - enq);
   }
-  for (auto& S : d->slots) S.pre = false;         // an early DMA whose chunk was never enqueued (a bad job)
 }
 
 void worker_loop(Device* d, size_t dslot) {
@@ -2403,7 +2280,7 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
     it.ks = ks;
     it.dev_arena = dview;
     it.chunk = C;
-    it.grouped = class_grouping() && mixed_classes(*ks, toks + it.lo, it.hi - it.lo);
+    it.grouped = mixed_classes(*ks, toks + it.lo, it.hi - it.lo);
     // grouped chunks serialise each class group's launches on one lane, so a
     // long ramp of small chunks would queue latency-bound launches (an
     // RSA-4096 modexp takes ~1.5 ms at any size): start at C / 4
@@ -2652,6 +2529,12 @@ int jg_debug_fail_alloc(jg_ctx* ctx, int n) {
   return 0;
 }
 
+int jg_debug_fail_verify(jg_ctx* ctx, int n) {
+  if (!ctx || n < 0) return -1;
+  ctx->fail_verify.store(n);
+  return 0;
+}
+
 int jg_debug_lifetime_check(int enable, uint64_t* violations, uint64_t* checked) {
   if (enable > 0) g_lifetime_on.store(1);
   else if (enable == 0) g_lifetime_on.store(0);
@@ -2678,6 +2561,18 @@ int jg_submit(jg_ctx* ctx, const uint8_t* arena, size_t arena_len, const jg_tok*
   *out = nullptr;
   if (ntok > (size_t)INT32_MAX / 2) { ctx->set_err("batch too large"); return -1; }
   try {
+    if (ctx->poisoned.load()) {
+      ctx->set_err("context unusable after an injected device failure (jg_debug_fail_verify): recreate it");
+      return -2;
+    }
+    if (ctx->fail_verify.load() > 0 && ctx->fail_verify.fetch_sub(1) == 1) {
+      // the injected failure surfaces where a kernel fault would: in jg_wait
+      ctx->poisoned.store(true);
+      auto t = std::make_shared<Ticket>();
+      t->fail(-2, "injected device failure (jg_debug_fail_verify)");
+      *out = new jg_ticket{std::move(t)};
+      return 0;
+    }
     if (ntok == 0) {                       // nothing to verify
       *out = new jg_ticket{std::make_shared<Ticket>()};
       return 0;
@@ -2743,7 +2638,7 @@ int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t ar
     b->own = std::make_unique<Bufs>();
     b->b = b->own.get();
     std::lock_guard<std::mutex> g(b->dev->mu);
-    b->lane = batch_lanes() > 1 && (b->dev->next_res++ & 1) ? &b->dev->lane1 : &b->dev->lane0;
+    b->lane = (b->dev->next_res++ & 1) ? &b->dev->lane1 : &b->dev->lane0;
     HIPCHK(hipSetDevice(b->dev->id));
     PlanScratch X;
     if (arena_len >= (uint64_t(1) << 32) - ARENA_SLACK) {
@@ -2773,59 +2668,16 @@ namespace {
 // A resident batch runs against the current key state when its key list is
 // the one it was planned for (a comb-width upgrade since staging is fine: the
 // run picks up the wider tables); a reload with another key list invalidates it.
-// CAPJWT_RESIDENT_GROUPS=1 (A/B): untimed resident runs of mixed batches use
-// the pipeline's class groups (cls_group) on the device's three group lanes,
-// as streamed chunks do, instead of one stream per class on the batch's lane.
-bool resident_groups() {
-  static const bool on = [] {
-    const char* e = std::getenv("CAPJWT_RESIDENT_GROUPS");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
-}
-
+// (One stream per class on the batch's lane: running mixed resident batches
+// on the pipeline's three group lanes measured 80.0-80.2 against 81.6-82.3
+// M/s on configs[4], profiles/r04_s14.)
 void run_resident(jg_ctx* ctx, jg_batch* b, bool timed) {
   HIPCHK(hipSetDevice(b->dev->id));
   KeyStateP ks = ctx->state();
   if (b->epoch != ks->epoch) throw std::runtime_error("key table reloaded since this batch was staged");
   b->timing = timed;
   b->marks_used = 0;
-  int nact = 0;
-  double gcost[3] = {0, 0, 0};
-  for (int c = 1; c < NCLS; ++c) {
-    const int64_t m = b->plan.ranges[c].end - b->plan.ranges[c].begin;
-    if (m <= 0) continue;
-    ++nact;
-    gcost[cls_group(c)] += CLS_COST[c] * (double)m;
-  }
-  if (!timed && nact >= 2 && resident_groups()) {
-    Device* d = b->dev;
-    if (b->gev.empty()) {
-      b->gev.resize(3 + NCLS);
-      for (auto& e : b->gev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    int jgrp = 0, least = 0;
-    for (int g = 1; g < 3; ++g) {
-      if (gcost[g] > gcost[jgrp]) jgrp = g;
-      if (d->gload[g] < d->gload[least]) least = g;
-    }
-    double lo = 1e300;
-    for (int g = 0; g < 3; ++g) lo = std::min(lo, d->gload[g] += gcost[g]);
-    for (int g = 0; g < 3; ++g) d->gload[g] -= lo;
-    GroupFan gf;
-    gf.join = d->lanes[jgrp].stream;
-    gf.ctrl = d->lanes[least].stream;
-    for (int c = 1; c < NCLS; ++c) gf.cls[c] = d->lanes[cls_group(c)].stream;
-    gf.start = b->gev[1];
-    for (int c = 0; c < NCLS; ++c) gf.done[c] = b->gev[3 + c];
-    HIPCHK(hipEventRecord(b->gev[0], b->lane->stream));        // after the batch's staging / previous run
-    HIPCHK(hipStreamWaitEvent(gf.ctrl, b->gev[0], 0));
-    run_plan(d, *ks, *ks->dev[b->dslot], b->lane, b->b, b->plan, nullptr, false, &gf);
-    HIPCHK(hipEventRecord(b->gev[2], gf.join));
-    HIPCHK(hipStreamWaitEvent(b->lane->stream, b->gev[2], 0));   // verdict copies and syncs stay on the lane
-  } else {
-    run_plan(b->dev, *ks, *ks->dev[b->dslot], b->lane, b->b, b->plan, b);
-  }
+  run_plan(b->dev, *ks, *ks->dev[b->dslot], b->lane, b->b, b->plan, b);
   if (b->ks_run && b->ks_run != ks) HIPCHK(hipStreamSynchronize(b->lane->stream));   // its kernels may read the old state
   b->ks_run = std::move(ks);
 }
@@ -2921,6 +2773,10 @@ int jg_hash_batch(jg_ctx* ctx, const uint8_t* arena, size_t arena_len,
                   const jg_hjob* jobs, size_t njobs, uint8_t* digest_out) {
   if (!ctx || (njobs > 0 && (!jobs || !digest_out)) || (arena_len > 0 && !arena)) return -1;
   if (njobs == 0) return 0;
+  if (ctx->poisoned.load()) {
+    ctx->set_err("context unusable after an injected device failure (jg_debug_fail_verify): recreate it");
+    return -2;
+  }
   for (size_t i = 0; i < njobs; ++i) {
     const jg_hjob& J = jobs[i];
     if (J.fam < JG_SHA256 || J.fam > JG_SHA512 || J.off > arena_len || J.len > arena_len - J.off) {

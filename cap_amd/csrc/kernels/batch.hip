@@ -189,11 +189,9 @@ void launch_scatter(const int32_t* perm, const uint8_t* verdict_pad, uint8_t* ve
 }
 
 void launch_plan_fill(const PlanFillArgs& a, hipStream_t s) {
-  static const bool blocked = [] {
-    const char* e = std::getenv("CAPJWT_PLAN_FILL");
-    return !(e && std::string(e) == "wave");          // A/B: the one-level kernel
-  }();
-  if (blocked && a.nkeys + 1 <= PF_MAX_BUCKETS) {
+  // two-level fill (LDS bucket counts, one global atomic per block and
+  // bucket); the one-level kernel serves key tables past PF_MAX_BUCKETS
+  if (a.nkeys + 1 <= PF_MAX_BUCKETS) {
     constexpr int64_t per = PF_THREADS * PF_ITEMS;
     if (a.n > 0) hipLaunchKernelGGL(k_plan_fill_blocked, dim3((unsigned)((a.n + per - 1) / per)), dim3(PF_THREADS), 0, s, a);
     const int64_t pads = (int64_t)(a.nkeys + 1) * 64;

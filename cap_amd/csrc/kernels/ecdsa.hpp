@@ -74,11 +74,7 @@ constexpr int ec_comb_w(int cls, bool gen) {
 // top window got 17 = W - 1 bits, and a scalar whose bits 504..520 were all
 // ones with a carry in (probability ~2^-18) lost that carry -- a wrong u2 and
 // a false reject (tests/golden/edge_digit_tokens.json, "p521_w18_top_carry").
-#ifdef JG_AB_OLD_WINDOWS
-constexpr int ec_windows_w(int cls, int w) { return (ec_order_bits(cls) + 1 + w - 1) / w; }   // A/B only: round 3's count
-#else
 constexpr int ec_windows_w(int cls, int w) { return (ec_order_bits(cls) + 2 + w - 1) / w; }
-#endif
 constexpr int ec_entries(int cls, bool gen) { return 1 << (ec_comb_w(cls, gen) - 1); }
 constexpr int ec_windows(int cls, bool gen) { return ec_windows_w(cls, ec_comb_w(cls, gen)); }
 // digit rows of the scalar -> point hand-off: one int32 row per window, the
@@ -104,14 +100,12 @@ constexpr int EC_P384_WQ[4] = {24, 20, 18, 16};
 constexpr int EC_P521_WQ[3] = {20, 18, 16};
 // every tier leaves the top window at most W - 2 bits (see ec_windows_w)
 constexpr bool ec_top_window_ok(int cls, int w) { return ec_order_bits(cls) - w * (ec_windows_w(cls, w) - 1) <= w - 2; }
-#ifndef JG_AB_OLD_WINDOWS
 static_assert(ec_top_window_ok(jgk::CLS_P256, 26) && ec_top_window_ok(jgk::CLS_P256, 24) &&
               ec_top_window_ok(jgk::CLS_P256, 22) && ec_top_window_ok(jgk::CLS_P256, 20) &&
               ec_top_window_ok(jgk::CLS_P384, 24) && ec_top_window_ok(jgk::CLS_P384, 20) &&
               ec_top_window_ok(jgk::CLS_P384, 18) && ec_top_window_ok(jgk::CLS_P384, 16) &&
               ec_top_window_ok(jgk::CLS_P521, 20) && ec_top_window_ok(jgk::CLS_P521, 18) &&
               ec_top_window_ok(jgk::CLS_P521, 16), "comb window count leaves no room for the top carry");
-#endif
 
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);
 // key staging: validate each listed key (plain 28-bit limbs x,y at aux_off:

@@ -536,11 +536,7 @@ __device__ __forceinline__ void add_window(uint32_t* X, uint32_t* Y, uint32_t* Z
   using Fp = typename CV::Fp;
   constexpr int L = Fp::L, STRIDE = ec_stride(CV::CLS), NE = GEN ? ec_entries(CV::CLS, true) : 1 << (CV::WQ - 1);
   if (d == 0) return;
-#ifdef JG_AB_TINY_TABLE
-  const int ad = (((d < 0 ? -d : d) - 1) & 255) + 1;     // A/B only: every gather within 256 entries (wrong verdicts)
-#else
   const int ad = d < 0 ? -d : d;
-#endif
   const uint32_t* ent = tab + ((int64_t)w * NE + (ad - 1)) * STRIDE;
   uint32_t x2[L], y2[L];
   load_entry<CV>(ent, x2, y2);
@@ -977,13 +973,10 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   }
   if (a.exc_reset) (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
   // tokens per thread for the batched inversion: keep >= ~8 waves per CU
-  // (CAPJWT_EC_WAVES_PER_CU: A/B of that target)
+  // (profiles/r04_s3/scalar_occupancy_ab.json: more waves, fewer tokens per
+  // inversion, measured 12-26 % slower)
   const int64_t n = a.end - a.begin;
-  static const int wpc = [] {
-    const char* e = std::getenv("CAPJWT_EC_WAVES_PER_CU");
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 8;
-  }();
+  constexpr int wpc = 8;
   int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * wpc * WAVE)));
   const int64_t S = (n + B - 1) / B;
   constexpr int TPB = WAVE * EC_SCALAR_WPB;

@@ -94,11 +94,7 @@ __device__ void add_full(EPt& R, const EPt& P, const EPt& Q) {
 template <int NE>
 __device__ __forceinline__ void add_window(FPt& P, const uint32_t* __restrict__ tab, int w, int d) {
   if (d == 0) return;
-#ifdef JG_AB_TINY_TABLE
-  const int ad = (((d < 0 ? -d : d) - 1) & 255) + 1;     // A/B only: every gather within 256 entries (wrong verdicts)
-#else
   const int ad = d < 0 ? -d : d;
-#endif
   const uint32_t* ent = tab + ((int64_t)w * NE + (ad - 1)) * ED_STRIDE;
   uint32_t ypx[fe::L], ymx[fe::L], t2d[fe::L];
 #pragma unroll

@@ -67,6 +67,23 @@ class KeySet:
     def VerifySignatureBatch(self, tokens: Sequence, ctx=None):
         return [tuple(r) for r in self._impl.verify_signature_batch(list(tokens))]
 
+    def SetCoalescing(self, max_inflight=2, max_batch=65536, window_us=0):
+        """Batching of concurrent single-token calls (VerifySignature and
+        Validator.Validate): at most `max_inflight` device batches at once, each
+        of at most `max_batch` tokens, collected for at most `window_us`."""
+        self._impl.set_coalescing(int(max_inflight), int(max_batch), int(window_us))
+
+    def CoalescingStats(self):
+        return dict(self._impl.coalescing_stats())
+
+    def DeviceStatus(self) -> str:
+        """"" while the GPU context verifies; else why it is lost (it is
+        recreated after a device error; see DeviceRecoveries)."""
+        return self._impl.device_status()
+
+    def DeviceRecoveries(self) -> int:
+        return self._impl.device_recoveries()
+
 
 def NewStaticKeySet(public_keys: List, devices=()):
     try:

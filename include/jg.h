@@ -120,6 +120,14 @@ int jg_keys_table_widths(jg_ctx* ctx, int* widths, int cap);
  * fails as if hipMalloc ran out of memory; 0 disables.  Returns 0 or -1. */
 int jg_debug_fail_alloc(jg_ctx* ctx, int n);
 
+/* Test hook of the degraded path (SURVEY §5 failure row): the n-th later
+ * jg_submit / jg_verify_batch of this context (counting from 1) fails as a
+ * device fault would -- its jg_wait returns -2 -- and the context is then
+ * unusable, as after a sticky HIP error: every later submission returns -2
+ * until the context is destroyed and recreated (the host layer's Engine does
+ * that, re-staging its key list).  0 disables.  Returns 0 or -1. */
+int jg_debug_fail_verify(jg_ctx* ctx, int n);
+
 /* Test hook: the background upgrader widens at most n more comb tables of
  * this context (-1 = no limit, the default; CAPJWT_DEBUG_MAX_UPGRADES sets
  * the initial value), so a class can be held at mixed widths; raising it

@@ -65,6 +65,17 @@ int main() {
   jr = jw->VerifySignatureBatch({ed_tok});
   check(!jr[0].ok && has(jr[0].err, dev), "jwks: device error again", jr[0].err);
   check(fetches == 1, "jwks: no refetch for a device failure", std::to_string(fetches));
+  // each failed call recreated the context (Engine::recover: new jg_ctx, the
+  // key list re-staged from the key set's own copy, no refetch)
+  check(jw->DeviceRecoveries() >= 2, "jwks: context recreated after each failure",
+        std::to_string(jw->DeviceRecoveries()));
+  check(jw->DeviceStatus().empty(), "jwks: healthy after recovery", jw->DeviceStatus());
+  // a single-token call takes the coalescer and gets the same error
+  Result one = jw->VerifySignature(ed_tok);
+  check(!one.ok && has(one.err, dev), "jwks: coalesced single call", one.err);
+  Result vone = v->Validate(ed_tok, ex);
+  check(!vone.ok && has(vone.err, dev) && has(vone.err, "error verifying token signature: "), "validator: single",
+        vone.err);
   // go-oidc adapter (remoteKeySet.VerifySignature, payload bytes)
   {
     auto rk = NewRemoteKeySet("https://issuer.example/keys", f);

@@ -22,5 +22,20 @@ int jg_verify_batch(jg_ctx* c, const uint8_t*, size_t, const jg_tok*, size_t, ui
   ++c->verify_calls;
   return -2;
 }
+// the host layer submits and waits: the submission is accepted, its wait fails
+struct jg_ticket {
+  int rc;
+};
+int jg_submit(jg_ctx* c, const uint8_t*, size_t, const jg_tok*, size_t, uint8_t*, jg_ticket** t) {
+  ++c->verify_calls;
+  *t = new jg_ticket{-2};
+  return 0;
+}
+int jg_wait(jg_ctx*, jg_ticket* t) {
+  const int rc = t->rc;
+  delete t;
+  return rc;
+}
+int jg_debug_fail_verify(jg_ctx*, int) { return 0; }
 int jg_hash_batch(jg_ctx*, const uint8_t*, size_t, const jg_hjob*, size_t, uint8_t*) { return -2; }
 }

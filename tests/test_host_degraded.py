@@ -26,7 +26,7 @@ def test_device_failure_becomes_per_token_errors(tmp_path):
         pytest.skip("no g++")
     exe = str(tmp_path / "degraded")
     srcs = [os.path.join(HERE, "degraded.cpp"), os.path.join(HERE, "fault_stub.cpp")] + [
-        os.path.join(HOST, f) for f in ("json.cpp", "jose.cpp", "cap_jwt.cpp")]
+        os.path.join(HOST, f) for f in ("hostmem.cpp", "json.cpp", "jose.cpp", "cap_jwt.cpp")]
     b = subprocess.run(["g++", "-O0", "-std=c++17", "-pthread", "-o", exe] + srcs,
                        capture_output=True, text=True, timeout=300)
     assert b.returncode == 0, b.stderr[-3000:]

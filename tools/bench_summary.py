@@ -17,3 +17,10 @@ for k, v in d.get("configs", {}).items():
         if sub in v:
             print(k, sub, {a: b for a, b in v[sub].items() if not isinstance(b, (dict, list, str))})
 print("speedup", d["speedup_vs_cpu"])
+e = d["e2e"]
+print("e2e in-process %.2f M/s (fresh %.2f)" % (e.get("in_bench_process", {}).get("value", 0) / 1e6, e["value"] / 1e6),
+      "flt", {k: v for k, v in e.get("in_bench_process", {}).get("phases_ms_last_pass", {}).items() if "flt" in k})
+if "single" in d:
+    for c, r in d["single"]["by_callers"].items():
+        print("single callers %5s: %.3f M/s p50 %.0f us p99 %.0f us mean batch %.1f %s" % (
+            c, r["value"] / 1e6, r["p50_us"], r["p99_us"], r["mean_batch"], r.get("error", "")))

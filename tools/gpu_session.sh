@@ -2,7 +2,7 @@
 # bench, then optional probes (run via gpurun from the repo root):
 #   bash tools/gpu_session.sh "<first test files>" [probe ...]
 # probes: e2e_ab (tools/e2e_ab.sh), keyload (tools/keyload_trace.py),
-#   ab (tools/ab_r04.sh), pmc_int (tools/gpu_pmc_int.sh), zc (tools/ubench/zc_read); "-" as the first
+#   pmc_int (tools/gpu_pmc_int.sh), zc (tools/ubench/zc_read); "-" as the first
 #   argument skips the tests and the bench
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -20,7 +20,7 @@ python3 tools/bench_summary.py gpurun_out/bench.json || true; }
 for p in "$@"; do
   case $p in
     e2e_ab) bash tools/e2e_ab.sh || exit 1 ;;
-    ab) bash tools/ab_r04.sh || exit 1 ;;
+    boxinfo) bash tools/boxinfo.sh > gpurun_out/boxinfo.txt 2>&1; cat gpurun_out/boxinfo.txt ;;
     pmc_int) bash tools/gpu_pmc_int.sh int || exit 1 ;;
     zc) timeout -k 10 180 ./tools/ubench/zc_read > gpurun_out/zc_read.txt 2>&1 || { echo ZC_FAIL; cat gpurun_out/zc_read.txt; exit 1; }; cat gpurun_out/zc_read.txt ;;
     keyload) timeout -k 10 300 python -u tools/keyload_trace.py > gpurun_out/keyload.log 2>&1 || { echo KEYLOAD_FAIL; tail -20 gpurun_out/keyload.log; exit 1; }; cat gpurun_out/keyload.log ;;

@@ -5,13 +5,20 @@
 // signatures are never checked here, so this binary measures host time only and
 // is never a verifier.  Not part of the product; not loaded by any test.
 //
-//   usage: hostprof TOKENS_FILE JWKS_FILE [reps]      (CAPJWT_TRACE=1 for phases)
+//   usage: hostprof TOKENS_FILE JWKS_FILE [reps [callers]]   (CAPJWT_TRACE=1 for phases)
+//   callers > 0: also time `callers` threads calling Validator::Validate per token
+//   (the coalesced single-token path) over the same tokens
+#include <sys/resource.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <sstream>
 #include <string>
+#include <thread>
+#include <atomic>
+#include <algorithm>
 #include <vector>
 
 #include "../../cap_amd/csrc/host/cap_jwt.hpp"
@@ -60,6 +67,8 @@ int main(int argc, char** argv) {
   double best = 1e30;
   size_t acc = 0;
   for (int r = 0; r < reps; ++r) {
+    rusage ru0, ru1;
+    getrusage(RUSAGE_SELF, &ru0);
     const auto t0 = std::chrono::steady_clock::now();
     auto rs = v->ValidateBatch(toks, e);
     acc = 0;
@@ -67,8 +76,28 @@ int main(int argc, char** argv) {
     release_results(rs);
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     best = std::min(best, dt);
-    std::printf("rep %d: %.1f ms  (%.2f M/s)  accepted %zu/%zu\n", r, dt * 1e3, toks.size() / dt / 1e6, acc, toks.size());
+    getrusage(RUSAGE_SELF, &ru1);
+    const double st = (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) + 1e-6 * (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec);
+    std::printf("rep %d: %.1f ms  (%.2f M/s)  accepted %zu/%zu  minflt %ld  stime %.3f s\n", r, dt * 1e3,
+                toks.size() / dt / 1e6, acc, toks.size(), ru1.ru_minflt - ru0.ru_minflt, st);
   }
   std::printf("best %.1f ms = %.2f M tokens/s on %d host threads\n", best * 1e3, toks.size() / best / 1e6, host_threads());
+  const int callers = argc > 4 ? std::atoi(argv[4]) : 0;
+  if (callers > 0) {
+    std::atomic<size_t> next{0}, ok{0};
+    const size_t total = std::min<size_t>(toks.size(), 200000);
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int c = 0; c < callers; ++c)
+      th.emplace_back([&] {
+        for (size_t i; (i = next.fetch_add(1)) < total;) ok += v->Validate(toks[i], e).ok;
+      });
+    for (auto& t : th) t.join();
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const auto st = ks->CoalescingStats();
+    std::printf("single-token Validate x %d callers: %zu calls in %.1f ms (%.3f M/s), accepted %zu; %llu batches, max %llu\n",
+                callers, total, dt * 1e3, total / dt / 1e6, ok.load(), (unsigned long long)st.batches,
+                (unsigned long long)st.max_batch_seen);
+  }
   return 0;
 }
