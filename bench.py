@@ -54,7 +54,7 @@ P256_WQ = 24          # key comb width of the run (main() sets it from the table
 
 
 def p256_point_mads_per_token(wq=None):
-    """Algorithmic 32x32->64 multiply-accumulates the P-256 comb kernel
+    """Algorithmic multiply-accumulates (v_mad_u64_u32 on 28-bit limbs) the P-256 comb kernel
     (k_ec_point) issues per token: 28-bit limbs, L = 10; a product is L^2 (mul)
     or L(L+1)/2 (sqr) partial products, a Montgomery reduction L * 4 (p + 1 has
     4 non-zero limbs above limb 0, mp.hpp).  Mixed addition = 8 mul + 3 sqr
@@ -1216,8 +1216,10 @@ def main():
                      "achieved": achieved, "peak": MAD_PEAK_T, "unit": "TMAD/s",
                      "frac": achieved / MAD_PEAK_T, "traffic": load_traffic("p256_point"),
                      "trace_window": es_window,
-                     "note": "integer multiply-add roofline (SURVEY §8d): algorithmic 32x32->64 MADs "
-                             f"per token {p256_point_mads_per_token():.0f} x tokens / HIP-event kernel time of the "
+                     "note": "integer multiply-add roofline (SURVEY §8d): algorithmic MADs (v_mad_u64_u32 partial "
+                             f"products of 28-bit limbs) per token {p256_point_mads_per_token():.0f} for the comb "
+                             "algorithm at the run's table widths (not §8(d)'s double-and-add count: the comb tables, "
+                             "built outside the timed region, replace the doublings) x tokens / HIP-event kernel time of the "
                              "synchronous runs (trace_window: their CLOCK_BOOTTIME span; the timed steps overlap two "
                              "batches, so their launches share the CUs); peak = measured v_mad_u64_u32 rate; "
                              "traffic = HBM bytes per launch, 2 x FETCH_SIZE + WRITE_SIZE of the rocprofv3 --pmc "

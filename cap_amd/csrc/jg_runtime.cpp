@@ -394,8 +394,26 @@ struct UseLog {
     if (c >= 0) std::snprintf(buf, sizeof buf, "%s of class %d (stream %p)", role, c, (void*)s);
     else std::snprintf(buf, sizeof buf, "%s (stream %p)", role, (void*)s);
     std::lock_guard<std::mutex> g(mu);
+    // only pending uses matter: once the log has grown past the last prune,
+    // completed events are counted and dropped (a long stream against a
+    // stable key set would otherwise keep one event per chunk for ever)
+    if (ev.size() >= prune_at) {
+      size_t k = 0;
+      for (auto& x : ev) {
+        if (hipEventQuery(x.first) == hipSuccess) {
+          g_lifetime_checked.fetch_add(1, std::memory_order_relaxed);
+          (void)hipEventDestroy(x.first);
+        } else {
+          (void)hipGetLastError();
+          ev[k++] = std::move(x);
+        }
+      }
+      ev.resize(k);
+      prune_at = std::max<size_t>(64, 2 * k);
+    }
     ev.emplace_back(e, buf);
   }
+  size_t prune_at = 64;
   ~UseLog() {
     for (auto& x : ev) {
       const hipError_t q = hipEventQuery(x.first);
@@ -592,11 +610,6 @@ struct Device {
   uint32_t* gtab[NCLS] = {};
   uint32_t* btab = nullptr;
   std::shared_ptr<SharedTable> tab_ref[NCLS];   // keeps gtab / btab alive
-  // comb tables by (key content id, width), shared by every generation that
-  // uses them: a reload (JWKS refresh) reuses the tables of keys it already had
-  // (no copy, no build) and builds only new keys' tables
-  std::mutex tmu;
-  std::map<std::string, std::weak_ptr<DevBuf>> tcache;
   std::mutex mu;                  // lane0 + slots
   // streaming pipeline: H2D copies of every chunk back to back on one copy
   // stream (full link bandwidth, no sharing between slots), each slot's
@@ -1267,18 +1280,21 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
       // A k_ec_exact launch needs a SIMD with ~290 VGPRs free even when it has
       // no work; behind the RSA modexps (256 VGPRs, 2 waves per SIMD) it waited
       // 0.8-1.4 ms for one, and every later class of the EC group's lane (and
-      // the next chunk's) waited behind it (profiles/r04_s3/zc_trace)
-      ea.part = gf ? EC_FAST : EC_ALL;
+      // the next chunk's) waited behind it (profiles/r04_s3/zc_trace).
+      // One exact launch per class, after all of its width runs: k_ec_exact
+      // walks the class's whole exception list (every run appends to it)
+      ea.part = EC_FAST;
       width_runs(K, G, P, c, [&](int64_t b, int64_t e, int w) {
         ea.begin = b; ea.end = e; ea.wq = w;
         launch_ec(c, ea, s, marker(marks, c));
-        if (gf) {
-          EcArgs x = ea;
-          x.part = EC_EXACT;
-          exact_later.push_back({c, x});
-        }
         ea.exc_reset = 0;          // later runs of the class append to its exception list
       });
+      EcArgs x = ea;
+      x.begin = r.begin;
+      x.end = r.end;
+      x.part = EC_EXACT;
+      if (gf) exact_later.push_back({c, x});
+      else launch_ec(c, x, s, marker(marks, c));
     } else {
       if (!d->btab) throw std::runtime_error("Ed25519 base table missing");
       EdArgs ea{};
@@ -1886,6 +1902,69 @@ std::shared_ptr<SharedTable> shared_table(Device* d, int cls, size_t bytes, hipS
   return t;
 }
 
+// Key comb tables by (key content id, width), per physical device: shared by
+// every generation, context slot and context on that device.  A reload (JWKS
+// refresh) reuses the tables of keys it already had (no copy, no build) and
+// builds only new keys' tables; a second slot on the same GPU (Context([0, 0]))
+// or a context recreated after a device error finds them built.
+struct PhysTables {
+  std::mutex mu;
+  std::map<std::string, std::weak_ptr<DevBuf>> cache;
+};
+PhysTables& phys_tables(int dev) {
+  static std::mutex m;
+  static auto* all = new std::map<int, std::unique_ptr<PhysTables>>();   // never destroyed (static teardown)
+  std::lock_guard<std::mutex> g(m);
+  auto& p = (*all)[dev];
+  if (!p) p = std::make_unique<PhysTables>();
+  return *p;
+}
+DevBufP cached_table(int dev, const std::string& key) {
+  PhysTables& T = phys_tables(dev);
+  std::lock_guard<std::mutex> g(T.mu);
+  auto it = T.cache.find(key);
+  return it == T.cache.end() ? nullptr : it->second.lock();
+}
+void cache_table(int dev, const std::string& key, const DevBufP& t) {
+  PhysTables& T = phys_tables(dev);
+  std::lock_guard<std::mutex> g(T.mu);
+  for (auto it = T.cache.begin(); it != T.cache.end();)
+    it = it->second.expired() ? T.cache.erase(it) : std::next(it);
+  T.cache[key] = t;
+}
+
+// fn(i) for every device slot i of ctx (§8(e): key loads and table widening on
+// all GPUs at once, not one after another): one thread per physical device,
+// the slots of one physical device in order on its thread (the second finds the
+// first one's tables in phys_tables).  The first exception is re-thrown after
+// every thread has finished.
+template <class Fn>
+void per_device(jg_ctx* ctx, Fn&& fn) {
+  std::map<int, std::vector<size_t>> by_id;
+  for (size_t i = 0; i < ctx->devs.size(); ++i) by_id[ctx->devs[i]->id].push_back(i);
+  if (by_id.size() <= 1) {
+    for (const auto& kv : by_id)
+      for (size_t i : kv.second) fn(i);
+    return;
+  }
+  std::vector<std::exception_ptr> err(by_id.size());
+  std::vector<std::thread> th;
+  size_t k = 0;
+  for (const auto& kv : by_id) {
+    th.emplace_back([&fn, &err, k, slots = kv.second] {
+      try {
+        for (size_t i : slots) fn(i);
+      } catch (...) {
+        err[k] = std::current_exception();
+      }
+    });
+    ++k;
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+
 void ensure_tables(Device* d, const StagedKeys& S) {
   HIPCHK(hipSetDevice(d->id));
   const hipStream_t s = d->kstream;
@@ -2012,11 +2091,7 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   std::map<std::string, Req> fresh;               // new tables by id + width
   std::vector<std::pair<size_t, std::string>> use;   // key -> id + width of its table
   {
-    std::lock_guard<std::mutex> tg(d->tmu);
-    auto cached = [&](const std::string& id, int w) -> DevBufP {
-      auto it = d->tcache.find(id + (char)w);
-      return it == d->tcache.end() ? nullptr : it->second.lock();
-    };
+    auto cached = [&](const std::string& id, int w) -> DevBufP { return cached_table(d->id, id + (char)w); };
     for (size_t i = 0; i < nk; ++i) {
       if (S.tab_id[i].empty() || !g->mirror[i].valid) continue;
       const int c = S.dk[i].cls, wt = S.want_w[i];
@@ -2080,16 +2155,12 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   if (nk) HIPCHK(hipMemcpyAsync(dk, g->mirror.data(), sizeof(DevKey) * nk, hipMemcpyHostToDevice, s));
   build_tables(groups, dk, blob, di, s);          // synchronises s
   pc.lap("new comb tables (kernels)");
-  {
-    std::lock_guard<std::mutex> tg(d->tmu);
-    for (auto it = d->tcache.begin(); it != d->tcache.end();)
-      it = it->second.expired() ? d->tcache.erase(it) : std::next(it);
-    for (const auto& f : fresh) d->tcache[f.second.id + (char)f.second.w] = f.second.buf;   // at its final width
-  }
+  for (const auto& f : fresh) cache_table(d->id, f.second.id + (char)f.second.w, f.second.buf);   // at its final width
   return g;
 }
 
 void upload_cls(jg_ctx* ctx, Device* d, DevGen& g, const std::vector<uint8_t>& cls_tab) {
+  HIPCHK(hipSetDevice(d->id));
   g.dcls = dev_alloc(d->id, std::max<size_t>(cls_tab.size(), 16), &ctx->fail_alloc);
   if (!cls_tab.empty())
     HIPCHK(hipMemcpyAsync(g.dcls->p, cls_tab.data(), cls_tab.size(), hipMemcpyHostToDevice, d->kstream));
@@ -2129,21 +2200,21 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
   const std::string key = cur->tab_id[k] + (char)cur->want_w[k];
   const int cls = cur->keys[k].cls, w = cur->want_w[k];
   std::vector<DevBufP> built(ctx->devs.size());
-  for (size_t i = 0; i < ctx->devs.size(); ++i) {
+  std::mutex nofit_mu;
+  std::string nofit;              // a device where the wide table does not fit free HBM
+  per_device(ctx, [&](size_t i) {
     Device* d = ctx->devs[i].get();
+    if ((built[i] = cached_table(d->id, key))) return;
     {
-      std::lock_guard<std::mutex> tg(d->tmu);
-      auto it = d->tcache.find(key);
-      if (it != d->tcache.end()) built[i] = it->second.lock();
+      std::lock_guard<std::mutex> g(nofit_mu);
+      if (!nofit.empty()) return;
     }
-    if (built[i]) continue;
     if (table_bytes(cls, w) + HBM_RESERVE > free_hbm(d->id)) {
-      skip.insert(key);
-      std::lock_guard<std::mutex> g(ctx->up_mu);
-      ctx->up_warn = "a " + std::to_string(table_bytes(cls, w) >> 20) + " MiB comb table (W = " + std::to_string(w) +
-                     ") does not fit free HBM on device " + std::to_string(d->id) + "; key " + std::to_string(k) +
-                     " keeps its narrower table";
-      return true;
+      std::lock_guard<std::mutex> g(nofit_mu);
+      nofit = "a " + std::to_string(table_bytes(cls, w) >> 20) + " MiB comb table (W = " + std::to_string(w) +
+              ") does not fit free HBM on device " + std::to_string(d->id) + "; key " + std::to_string(k) +
+              " keeps its narrower table";
+      return;
     }
     HIPCHK(hipSetDevice(d->id));
     const DevGen& G = *cur->dev[i];
@@ -2162,7 +2233,14 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
     // sliced: the upgrade stream may share a hardware queue with a verify
     // lane, which then waits at most one slice behind it (tables.hpp)
     build_tables(groups, tmp->as<DevKey>(), G.keyblob(), (int32_t*)((char*)tmp->p + sizeof(DevKey)), d->ustream, true);
+    cache_table(d->id, key, t);
     built[i] = t;
+  });
+  if (!nofit.empty()) {
+    skip.insert(key);
+    std::lock_guard<std::mutex> g(ctx->up_mu);
+    ctx->up_warn = nofit;
+    return true;
   }
   // publish against whatever state is current now (a load may have replaced
   // the one the build started from: every key with this content gets the table)
@@ -2180,10 +2258,6 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
       g->mirror[j].tab_w = w;
       g->kw[j] = (uint8_t)w;
       hit = true;
-    }
-    {
-      std::lock_guard<std::mutex> tg(d->tmu);
-      d->tcache[key] = built[i];
     }
     if (!hit) continue;
     any = true;
@@ -2448,13 +2522,13 @@ int jg_keys_load(jg_ctx* ctx, const jg_key* keys, int nkeys) {
     pc.lap("host key staging");
     // stage on every device beside running work; any failure throws and
     // leaves the published table (and what verifies against it) untouched
-    std::vector<std::shared_ptr<DevGen>> gens;
-    for (auto& d : ctx->devs) gens.push_back(stage_device(ctx, d.get(), S, !tables_sync()));
+    std::vector<std::shared_ptr<DevGen>> gens(ctx->devs.size());
+    per_device(ctx, [&](size_t i) { gens[i] = stage_device(ctx, ctx->devs[i].get(), S, !tables_sync()); });
     pc.lap("device staging (all devices)");
     // device-side validity (on-curve, Ed25519 decoding) back into the host view
     for (size_t i = 0; i < ns->keys.size(); ++i) ns->keys[i].valid = ns->keys[i].valid && gens[0]->mirror[i].valid;
     rebuild_class_tables(*ns);
-    for (size_t i = 0; i < gens.size(); ++i) upload_cls(ctx, ctx->devs[i].get(), *gens[i], ns->cls_tab);
+    per_device(ctx, [&](size_t i) { upload_cls(ctx, ctx->devs[i].get(), *gens[i], ns->cls_tab); });
     pc.lap("class tables");
     ns->tab_id = std::move(S.tab_id);
     ns->want_w = std::move(S.want_w);

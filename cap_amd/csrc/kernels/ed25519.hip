@@ -52,13 +52,16 @@ struct FPt { uint32_t X[fe::L], Y[fe::L], Z[fe::L], T[fe::L]; };
 // 7 products.  fe::mul's second operand carries the factor 19 and must be the
 // smaller one: the point side for A, B, C, then E and G (tools/fe25519_bounds.py)
 __device__ __forceinline__ void add_niels(FPt& P, const uint32_t* ypx, const uint32_t* ymx, const uint32_t* t2d) {
-  uint32_t t[fe::L], A[fe::L], B[fe::L], C[fe::L], D[fe::L], E[fe::L], F[fe::L], G[fe::L], H[fe::L];
+  uint32_t t[fe::L], A[fe::L], B[fe::L], C[fe::L], E[fe::L], F[fe::L], G[fe::L], H[fe::L];
+  // ordered so that each input dies as early as it can (P.T and 2dxy first):
+  // the live set stays near 4 field elements + one product's columns
+  fe::mul(C, t2d, P.T);
+  fe::add(t, P.Z, P.Z);                                   // D
+  fe::sub(F, t, C); fe::add(G, t, C);
   fe::sub(t, P.Y, P.X); fe::mul(A, ymx, t);
   fe::add(t, P.Y, P.X); fe::mul(B, ypx, t);
-  fe::mul(C, t2d, P.T);
-  fe::add(D, P.Z, P.Z);
-  fe::sub(E, B, A); fe::sub(F, D, C); fe::add(G, D, C); fe::add(H, B, A);
-  fe::mul(P.X, F, E); fe::mul(P.Y, H, G); fe::mul(P.T, H, E); fe::mul(P.Z, F, G);
+  fe::sub(E, B, A); fe::add(H, B, A);
+  fe::mul(P.X, F, E); fe::mul(P.T, H, E); fe::mul(P.Y, H, G); fe::mul(P.Z, F, G);
 }
 
 // radix-2^25.5 limbs (limbs < 2^31) -> ED25519P Montgomery form
@@ -114,9 +117,10 @@ __device__ __forceinline__ void add_window(FPt& P, const uint32_t* __restrict__ 
   add_niels(P, a1, a2, t2d);
 }
 
-// signed W-bit digits d_w in [-2^(W-1), 2^(W-1)], s = sum d_w 2^(W w)
+// signed W-bit digits d_w in [-2^(W-1), 2^(W-1)], s = sum d_w 2^(W w);
+// digit w goes to dg[w * stride] (k_ed_point: the wave's LDS digit rows)
 template <int W, int NWIN>
-__device__ __forceinline__ void recode(int* dg, const uint32_t* s) {
+__device__ __forceinline__ void recode(int* dg, const uint32_t* s, int stride = 1) {
   constexpr uint32_t DM = (1u << W) - 1u;
   int c = 0;
 #pragma unroll
@@ -126,7 +130,7 @@ __device__ __forceinline__ void recode(int* dg, const uint32_t* s) {
     if (sh > MP_W - W && q + 1 < L) b |= s[q + 1] << (MP_W - sh);
     int v = (int)(b & DM) + c;
     c = v > (1 << (W - 1));
-    dg[w] = v - (c << W);
+    dg[w * stride] = v - (c << W);
   }
 }
 
@@ -174,19 +178,21 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
     mp::csub<Fl>(k);
   }
   constexpr int NB = ed_windows(true), NA = ed_windows_w(WA), NW = NB > NA ? NB : NA;
-  int d1[NB], d2[NA];
-  recode<ed_comb_w(true), NB>(d1, s);
-  recode<WA, NA>(d2, k);
+  // the signed digits of S (B windows) and k (-A windows) wait in LDS, one row
+  // per window, lane-contiguous (conflict-free): held in registers they took
+  // NB + NA VGPRs through the whole loop and the kernel three waves per SIMD
+  __shared__ int dg[(NB + NA) * WAVE];
+  const int lane = (int)threadIdx.x;
+  recode<ed_comb_w(true), NB>(dg + lane, s, WAVE);
+  recode<WA, NA>(dg + NB * WAVE + lane, k, WAVE);
   FPt P;                                      // the neutral element (0, 1, 1, 0)
   fe::set_small(P.X, 0u); fe::set_small(P.Y, 1u); fe::set_small(P.Z, 1u); fe::set_small(P.T, 0u);
   const uint32_t* __restrict__ atab = key_table(K);
 #pragma unroll 1
   for (int w = 0; w < NW; ++w) {
-    int e1 = 0, e2 = 0;                       // uniform select: no dynamic register indexing
-#pragma unroll
-    for (int i = 0; i < NB; ++i) if (i == w) e1 = d1[i];
-#pragma unroll
-    for (int i = 0; i < NA; ++i) if (i == w) e2 = d2[i];
+    // each lane reads back only its own digits: no barrier needed
+    const int e1 = w < NB ? dg[w * WAVE + lane] : 0;
+    const int e2 = w < NA ? dg[(NB + w) * WAVE + lane] : 0;
     add_window<ed_entries(true)>(P, a.btab, w, e1);
     add_window<(1 << (WA - 1))>(P, atab, w, e2);
   }

@@ -39,6 +39,16 @@ def oracle_jwks(tok, okeys):
         return None, str(e)
 
 
+def same(got, want):
+    """got == the oracle's (claims, err); the oracle's "oidc: malformed jwt"
+    stands for the whole go-jose parse error after it (the parse error text
+    itself is pinned by tests/test_host_cpu.py)"""
+    got, want = tuple(got), tuple(want)
+    if want[1] and want[1].endswith("oidc: malformed jwt"):
+        return got[0] is None and got[1] is not None and got[1].startswith(want[1] + ": ")
+    return got == want
+
+
 def test_concurrent_single_calls_equal_batch_and_oracle(c5):
     from cap_amd import jwt
     meta, pool, okeys = c5
@@ -53,8 +63,8 @@ def test_concurrent_single_calls_equal_batch_and_oracle(c5):
         assert single == batch
     st = ks.CoalescingStats()
     assert st["calls"] == 2 * len(pool) and st["batches"] <= st["calls"]
-    for tok, (claims, gerr) in zip(pool, batch):
-        assert (claims, gerr) == oracle_jwks(tok, okeys)
+    for tok, g in zip(pool, batch):
+        assert same(g, oracle_jwks(tok, okeys)), (tok, g)
     # Validator.Validate from many threads == ValidateBatch == the oracle
     v, _ = jwt.NewValidator(ks)
     algs = sorted({m[1] for m in meta})
@@ -67,7 +77,7 @@ def test_concurrent_single_calls_equal_batch_and_oracle(c5):
     now_ns = (1611699344 + 60) * jws.SECOND
     exp = dict(SigningAlgorithms=algs, Issuer="https://example.com/", Audiences=["www.example.com"])
     for tok, g in zip(pool, vb):
-        assert tuple(g) == tuple(jws.validate(tok, lambda t: jws.jwks_keyset_verify(t, okeys), exp, now_ns))
+        assert same(g, jws.validate(tok, lambda t: jws.jwks_keyset_verify(t, okeys), exp, now_ns)), (tok, g)
     assert fetch.calls == 1
 
 
@@ -116,11 +126,11 @@ def test_device_failure_then_recovery_jwks(c5, single):
     assert got[-1][0] is None and got[-1][1].startswith("oidc: malformed jwt: ")
     for i, g in enumerate(got[:-1]):
         if i not in failed:
-            assert g == oracle_jwks(toks[i], okeys)
+            assert same(g, oracle_jwks(toks[i], okeys))
     assert fetch.calls == calls0
     # recovered: a new context with the same key list, verdicts exact again
     assert ks.DeviceRecoveries() == 1 and ks.DeviceStatus() == ""
-    assert ks.VerifySignatureBatch(pool) == [oracle_jwks(t, okeys) for t in pool]
+    assert all(same(g, oracle_jwks(t, okeys)) for t, g in zip(pool, ks.VerifySignatureBatch(pool)))
     assert [ks.VerifySignature(t) for t in good[:8]] == [oracle_jwks(t, okeys) for t in good[:8]]
     assert fetch.calls == calls0 + 1                # the pool's tampered tokens miss: one refresh (max_age 0)
 

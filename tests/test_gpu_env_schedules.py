@@ -11,6 +11,7 @@ child process started with that environment, before any GPU call of its own:
   CAPJWT_CHUNK                 pipeline chunk size (an odd size: ragged chunks)
 """
 import os
+import re
 import subprocess
 import sys
 
@@ -35,4 +36,4 @@ def test_config5_under_env(case):
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, f"{case}: child failed\n{tail}"
-    assert " 2 passed" in r.stdout, tail
+    assert re.search(r"\b2 passed", r.stdout), tail

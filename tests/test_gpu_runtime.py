@@ -187,8 +187,10 @@ def _pinned_copy(arena, tail=0):
 
 def test_zero_copy_class_major_plans():
     """Mixed batches from jg_host_alloc memory run as class-major zero-copy
-    plans (prep kernels read the pinned arena over PCIe; jg_set_zero_copy):
-    verdicts equal the oracle's and the chunked DMA path's -- whole-item plans,
+    plans (jg_set_zero_copy: per class, k_zc_gather copies the class's token
+    bytes from the pinned arena over PCIe into a per-key strided device arena,
+    then the class's prep and arithmetic run on it): verdicts equal the
+    oracle's and the chunked DMA path's -- whole-item plans,
     items cut into several plans, several submissions in flight across both
     zero-copy slots, the last token ending exactly at the block's end, and a
     two-slot context whose items each read their own share in place."""
@@ -253,4 +255,48 @@ def test_zero_copy_only_inside_host_alloc_blocks():
     out3 = (ctypes.c_uint8 * n)()
     assert L.jg_verify_batch(ctx.h, bytes(arena.buf), len(arena.buf), ta, n, out3) == 0
     assert list(out3) == want
+    ctx.close()
+
+
+def test_zero_copy_gather_layout_edges():
+    """k_zc_gather's layout edges: an arena base that is 16-byte
+    but not 256-byte aligned inside a jg_host_alloc block, and the tokens of
+    one key with different lengths, so that key's longest span sets its
+    device stride -- the short tokens' slots carry slack, the long ones fill
+    them exactly.  Verdicts == the oracle's and the chunked path's."""
+    from cap_amd import _lib
+    from oracle import jws
+    keys, toks = H.golden()
+    okeys = [jws.Key.from_fixture(k) for k in keys]
+    L = _lib.lib()
+    arena = _lib.Arena()
+    want = []
+    for t in toks:
+        p = jws.parse_jws(t["token"])
+        if p is None or not p.crit_ok:
+            continue
+        sig_b64 = jws.b64url_encode(p.signature).encode()
+        for ki, k in enumerate(okeys):
+            # each token twice: as signed, and with one more signing-input
+            # byte (a reject) -- every key sees several span lengths
+            arena.add(p.signing_input, sig_b64, p.alg, ki)
+            want.append(int(jws.verify_sig(p, k)))
+            arena.add(p.signing_input + b"A", sig_b64, p.alg, ki)
+            want.append(0)
+    lens = {}
+    for off, si, rel, sb, ki, alg in arena.toks:
+        lens.setdefault(ki, set()).add(rel + sb)
+    assert any(len(v) > 2 for v in lens.values())        # mixed lengths on one key
+    n = len(arena.toks)
+    ta = arena.tok_array()
+    ctx = _lib.Context()
+    ctx.load_keys([H.abi_key(k) for k in keys])
+    big = _lib.PinnedBuffer(len(arena.buf) + 16 + 512)
+    ctypes.memmove(big.ptr + 16, bytes(arena.buf), len(arena.buf))     # base == 16 (mod 256)
+    for zc in (True, False):
+        ctx.set_zero_copy(zc, 1 << 21)
+        out = (ctypes.c_uint8 * n)()
+        assert L.jg_verify_batch(ctx.h, big.ptr + 16, len(arena.buf), ta, n, out) == 0
+        assert list(out) == want, zc
+    big.free()
     ctx.close()

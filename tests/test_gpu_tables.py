@@ -59,11 +59,13 @@ def test_background_widening_matches_sync_build():
     a.wait_tables()
     da = [a.table_digest(i) for i in range(len(keys))]
     wa = a.table_widths()
+    # closed first: key tables are shared per physical device between live
+    # contexts (jg_runtime.cpp phys_tables), and B must build its own
+    a.close()
     b = _lib.Context()
     b.load_keys([H.abi_key(k) for k in keys])
     db = [b.table_digest(i) for i in range(len(keys))]
     assert wa == b.table_widths()
-    a.close()
     b.close()
     assert any(da)
     assert da == db
