@@ -15,7 +15,10 @@
 //      do not depend on which key verified).
 #include "cap_jwt.hpp"
 
+#include <linux/futex.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <sys/resource.h>
 
 #include <algorithm>
@@ -1101,12 +1104,33 @@ Coalescer::Stats Coalescer::stats() {
   return st_;
 }
 
+namespace {
+// A caller of the coalescer sleeps on its own request's state word (Linux
+// futex, process-private): the leader wakes it without the queue lock, so
+// hundreds of waiting callers do not convoy on that lock (a condition
+// variable waits by re-acquiring it: two context switches or more per call).
+void futex_wait(std::atomic<int>* w, int expect) {
+  syscall(SYS_futex, reinterpret_cast<int*>(w), FUTEX_WAIT_PRIVATE, expect, nullptr, nullptr, 0);
+}
+void futex_wake(std::atomic<int>* w) {
+  syscall(SYS_futex, reinterpret_cast<int*>(w), FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
+}  // namespace
+
+// Wake position i of a finished batch's wake-up list (its leader is not in it)
+void Coalescer::release(const std::vector<Req*>& wake, size_t i) {
+  if (i >= wake.size()) return;
+  Req* x = wake[i];
+  x->state.store(Req::DONE, std::memory_order_release);
+  futex_wake(&x->state);                         // x may be touched no more after this (its owner returns)
+}
+
 void Coalescer::run(Req* r) {
   std::unique_lock<std::mutex> lk(m_);
   q_.push_back(r);
   ++st_.calls;
   window_cv_.notify_one();                       // a leader collecting a window may want it
-  while (!r->done) {
+  while (true) {
     if (leaders_ < cfg_.max_inflight && !q_.empty()) {
       // lead one batch: everything queued (FIFO), up to max_batch
       ++leaders_;
@@ -1131,20 +1155,52 @@ void Coalescer::run(Req* r) {
       } catch (...) {
         ex = std::current_exception();
       }
-      lk.lock();
+      // the batch's other callers wake as a binary tree: this leader wakes
+      // the first, each woken caller wakes its own two -- log2(batch) rounds of
+      // wake-ups instead of one leader issuing every one in turn
+      bool mine = false;
+      auto wake = std::make_shared<std::vector<Req*>>();
+      wake->reserve(batch.size());
       for (size_t i = 0; i < batch.size(); ++i) {
         Req* x = batch[i];
         x->batch = V;
         x->idx = i;
         x->ex = ex;                              // a host-side bug in the batch reaches every caller in it
-        x->done = true;
-        if (x != r) x->cv.notify_one();
+        if (x == r) {
+          mine = true;
+          continue;
+        }
+        x->wpos = wake->size();
+        wake->push_back(x);
       }
+      for (Req* x : *wake) x->peers = wake;
+      release(*wake, 0);
+      lk.lock();
       --leaders_;
       // hand the lead to the oldest waiting caller, if any
-      if (!q_.empty()) q_.front()->cv.notify_one();
+      if (!q_.empty()) {
+        Req* f = q_.front();
+        int w = Req::WAITING;
+        if (f->state.compare_exchange_strong(w, Req::LEAD, std::memory_order_acq_rel)) futex_wake(&f->state);
+      }
+      if (mine) break;
     } else {
-      r->cv.wait(lk);
+      // sleep until a leader carries r (DONE) or hands r the lead (LEAD)
+      lk.unlock();
+      int st;
+      while ((st = r->state.load(std::memory_order_acquire)) == Req::WAITING) futex_wait(&r->state, Req::WAITING);
+      if (st != Req::DONE) {                     // LEAD: take the lead if it is still free
+        int lead = Req::LEAD;
+        r->state.compare_exchange_strong(lead, Req::WAITING, std::memory_order_acq_rel);
+        lk.lock();
+        if (r->state.load(std::memory_order_acquire) != Req::DONE) continue;
+        lk.unlock();
+      }
+      // carried by a batch: wake this caller's two children in its wake-up tree
+      auto peers = std::move(r->peers);
+      release(*peers, 2 * r->wpos + 1);
+      release(*peers, 2 * r->wpos + 2);
+      break;
     }
   }
   if (r->ex) std::rethrow_exception(r->ex);

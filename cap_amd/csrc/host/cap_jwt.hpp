@@ -273,9 +273,11 @@ class Coalescer {
     std::string_view tok;
     std::shared_ptr<const Verified> batch;   // the verified batch that carried this token ...
     size_t idx = 0;                          // ... and its index there
-    bool done = false;
     std::exception_ptr ex;        // the batch threw (a host-side bug): re-thrown to every caller in it
-    std::condition_variable cv;
+    std::shared_ptr<std::vector<Req*>> peers;   // the batch's callers to wake (a binary tree) ...
+    size_t wpos = 0;                            // ... and this one's position there
+    enum { WAITING = 0, DONE = 1, LEAD = 2 };
+    std::atomic<int> state{WAITING};   // futex word: set by the leader that carried it / handed it the lead
   };
   // parse + verify a batch of tokens (KeySet::verify_raw)
   using Exec = std::function<std::shared_ptr<const Verified>(const std::vector<std::string_view>&)>;
@@ -286,6 +288,7 @@ class Coalescer {
   struct Stats { uint64_t calls = 0, batches = 0, max_batch_seen = 0; };
   Stats stats();
  private:
+  static void release(const std::vector<Req*>& wake, size_t i);
   Exec exec_;
   std::mutex m_;
   std::condition_variable window_cv_;

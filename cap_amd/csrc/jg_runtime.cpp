@@ -579,7 +579,7 @@ struct Slot {
   uint64_t seq = 0;                // enqueue order across both slot rings (oldest completes first)
   size_t reserved = 0;             // chunk capacity (jobs) the buffers were sized for
   uint64_t reserved_epoch = ~0ull; // key table they were sized against
-  bool inflight = false;
+  bool inflight = false;            // enqueued, not yet completed (Device::cmu)
   std::shared_ptr<Ticket> ticket;
   KeyStateP ks;                    // key state of the chunk in flight (kept alive until it completes)
   uint8_t* out = nullptr;
@@ -621,11 +621,15 @@ struct Device {
   double gload[3] = {0, 0, 0};    // class-grouped chunks: class cost queued per group lane (relative)
   uint64_t slot_seq = 0;
   int next_res = 0;                // resident batches staged (CAPJWT_BATCH_LANES)
-  std::thread worker;
+  std::thread worker, completer;
   std::mutex qmu;
-  std::condition_variable qcv, idle_cv;
+  std::condition_variable qcv;
   std::deque<Item> q;
-  bool stop = false, busy = false;
+  bool stop = false;
+  std::mutex cmu;                  // slots in flight (Slot::inflight, cq)
+  std::condition_variable ccv, scv; // completer: a chunk enqueued / worker: a slot freed
+  std::deque<Slot*> cq;            // in-flight chunks, enqueue order
+  bool cstop = false;
   PlanScratch plan;               // worker scratch of the host plan
 };
 
@@ -1213,6 +1217,17 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
   const bool zc = gf && gf->zc, feed = zc && gf->feed;
   int order[NCLS - 1];
   for (int i = 0; i < NCLS - 1; ++i) order[i] = i + 1;
+#ifndef JG_RESIDENT_COST_ORDER
+#define JG_RESIDENT_COST_ORDER 0
+#endif
+  if (JG_RESIDENT_COST_ORDER && conc) {
+    // a mixed resident batch's class chains, costliest first: the critical
+    // chain (RSA-4K+ in configs[4]) takes the CUs first, the short EC chains
+    // fill in beside it
+    double cost[NCLS] = {};
+    for (int c = 1; c < NCLS; ++c) cost[c] = CLS_COST[c] * (double)(P.ranges[c].end - P.ranges[c].begin);
+    std::stable_sort(order, order + NCLS - 1, [&](int x, int y) { return cost[x] > cost[y]; });
+  }
   if (feed) {
     std::stable_sort(order, order + NCLS - 1, [&](int x, int y) { return gf->cost[x] > gf->cost[y]; });
     if (gf->feed != gf->ctrl) HIPCHK(hipStreamWaitEvent(gf->feed, gf->start, 0));
@@ -1348,8 +1363,9 @@ void collect_times(jg_batch* b) {
 // ---------------------------------------------------------------- streaming pipeline
 // Complete the chunk held by slot S (its verdicts were copied to pinned
 // staging): hand the verdicts to the caller and count the chunk off its ticket.
+// Runs on the device's completer thread (completer_loop), S.inflight still
+// set: the worker does not touch S until the completer clears it.
 void finish_slot(Slot& S) {
-  if (!S.inflight) return;
   const hipError_t e = hipEventSynchronize(S.done);
   if (e != hipSuccess) S.ticket->fail(-2, std::string("verify chunk: ") + hipGetErrorString(e));
   else if (S.n) std::memcpy(S.out, S.h_verdict.p, S.n);
@@ -1362,7 +1378,6 @@ void finish_slot(Slot& S) {
     std::fprintf(stderr, "[pipe] chunk %3d n=%7zu host wait %.3f plan %.3f enq %.3f (h2d calls %.3f, sizing %.3f, grows %d) | gpu h2d %.3f-%.3f kern-end %.3f done %.3f ms\n",
                  S.chunk_no, S.n, S.host_ms[0], S.host_ms[1], S.host_ms[2], S.host_ms[3], S.host_ms[4], S.grows, a, b, c, dn);
   }
-  S.inflight = false;
   auto t = std::move(S.ticket);
   S.ticket.reset();
   S.ks.reset();                    // may free a replaced key state (after this chunk completed)
@@ -1411,14 +1426,98 @@ void reserve_slot(const KeyState& K, Slot& S, size_t C, size_t nbuckets, double 
   S.reserved_epoch = K.epoch;
 }
 
-void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_tok* toks, size_t n, uint8_t* out) {
+// A job outside the key table or the arena, found by scan_chunk (jg_wait -> -1)
+struct BadJob : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// enqueue_chunk's one host pass over a chunk's jobs: validate each (key_idx in
+// the table, spans inside the arena: check_jobs' rule), count the plan's
+// buckets and the (class, alg) pairs, find the arena span, and copy the jobs
+// into the pinned plan block (ht).  Chunks of 64 k jobs and more are cut over
+// four host threads (per-thread counts, merged): a 524 k-job chunk's pass held
+// the device worker ~4 ms, during which the next chunk's copy could not start
+// (profiles/r04_s9/stream_trace_timeline.txt, the gaps between chunks).
+struct ChunkScan {
+  uint64_t amin = UINT64_MAX, amax = 0, need = 0, seen[2] = {0, 0};
+};
+void scan_chunk(const KeyState& K, const jg_tok* toks, size_t n, size_t arena_len, size_t base, jg_tok* ht, bool zc,
+                PlanScratch& X, ChunkScan& out) {
+  const size_t nk = K.keys.size(), NB = nk + 1, RB = nk;
+  const uint8_t* ctab = K.cls_tab.data();
+  const int nt = n >= 65536 ? 4 : 1;
+  std::vector<std::vector<int64_t>> tot(nt, std::vector<int64_t>(NB, 0));
+  std::vector<std::vector<uint64_t>> kmax(zc ? nt : 0, std::vector<uint64_t>(NB, 0));
+  std::vector<ChunkScan> part(nt);
+  std::vector<size_t> bad(nt, SIZE_MAX);
+  auto run = [&](int t) {
+    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    int64_t* tt = tot[t].data();
+    ChunkScan& r = part[t];
+    uint64_t sl = 0, sh = 0;
+    for (size_t i = lo; i < hi; ++i) {
+      const jg_tok& tk = toks[i];
+      if (tk.key_idx >= nk || tk.off > arena_len || tk.sig_in_len > arena_len - tk.off ||
+          (uint64_t)tk.sig_rel_off + tk.sig_b64_len > arena_len - tk.off) {
+        bad[t] = i;
+        break;
+      }
+      const uint64_t e = tok_end(tk);
+      r.amin = std::min<uint64_t>(r.amin, tk.off);
+      r.amax = std::max<uint64_t>(r.amax, e);
+      r.need += e - tk.off;
+      ht[i] = tk;
+      const unsigned alg = tk.alg;
+      const unsigned c = alg < NALG ? ctab[(size_t)tk.key_idx * NALG + alg] : CLS_REJECT;
+      const unsigned combo = c * 16 + (alg & 15u);
+      if (combo < 64) sl |= 1ull << combo;
+      else sh |= 1ull << (combo - 64);
+      tt[c == CLS_REJECT ? RB : tk.key_idx]++;
+      if (zc && c != CLS_REJECT) kmax[t][tk.key_idx] = std::max<uint64_t>(kmax[t][tk.key_idx], e - tk.off);
+    }
+    r.seen[0] = sl;
+    r.seen[1] = sh;
+  };
+  if (nt == 1) {
+    run(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(run, t);
+    run(0);
+    for (auto& t : th) t.join();
+  }
+  for (int t = 0; t < nt; ++t)
+    if (bad[t] != SIZE_MAX) {
+      std::string err;
+      check_jobs(K, arena_len, toks + bad[t], 1, &err, base + bad[t]);
+      throw BadJob(err);
+    }
+  X.total.assign(NB, 0);
+  if (zc) X.kmax.assign(NB, 0);
+  for (int t = 0; t < nt; ++t) {
+    for (size_t b = 0; b < NB; ++b) X.total[b] += tot[t][b];
+    if (zc)
+      for (size_t b = 0; b < NB; ++b) X.kmax[b] = std::max(X.kmax[b], kmax[t][b]);
+    out.amin = std::min(out.amin, part[t].amin);
+    out.amax = std::max(out.amax, part[t].amax);
+    out.need += part[t].need;
+    out.seen[0] |= part[t].seen[0];
+    out.seen[1] |= part[t].seen[1];
+  }
+}
+
+void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_tok* toks, size_t n, uint8_t* out,
+                   size_t job_base) {
   const auto t_start = std::chrono::steady_clock::now();
   const int grows0 = g_grows.load(std::memory_order_relaxed);
   const KeyState& K = *it.ks;
   const DevGen& G = *K.dev[dslot];
   if (S.reserved != it.chunk || S.reserved_epoch != K.epoch) {
+    // bytes per job from a sample (jobs are validated by scan_chunk below:
+    // a bad span must not size the buffers)
     double bpj = 0;
-    for (size_t i = 0; i < std::min<size_t>(n, 256); ++i) bpj += (double)(tok_end(toks[i]) - toks[i].off);
+    for (size_t i = 0; i < std::min<size_t>(n, 256); ++i)
+      bpj += (double)std::min<uint64_t>(tok_end(toks[i]) - toks[i].off, it.arena_len);
     reserve_slot(K, S, std::max(it.chunk, n), K.keys.size() + 1, n ? bpj / (double)std::min<size_t>(n, 256) : 512.0,
                  it.zc);
   }
@@ -1430,18 +1529,10 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   const PlanBlock L(NB, n);
   uint8_t* hb = (uint8_t*)S.h_meta.get(L.bytes);
   jg_tok* ht = (jg_tok*)(hb + L.toks_off);
-  uint64_t amin = UINT64_MAX, amax = 0, need = 0, seen[2];
+  ChunkScan scan;
+  scan_chunk(K, toks, n, it.arena_len, job_base, ht, it.zc, d->plan, scan);
+  uint64_t amin = scan.amin, amax = scan.amax, need = scan.need, seen[2] = {scan.seen[0], scan.seen[1]};
   std::vector<uint64_t>& kmax = d->plan.kmax;
-  if (it.zc) kmax.assign(NB, 0);
-  plan_count(K, toks, n, d->plan, false, seen, [&](size_t i) {
-    const jg_tok& t = toks[i];
-    const uint64_t e = tok_end(t);
-    amin = std::min<uint64_t>(amin, t.off);
-    amax = std::max<uint64_t>(amax, e);
-    need += e - t.off;
-    ht[i] = t;
-    if (it.zc && classify(K, t) != CLS_REJECT) kmax[t.key_idx] = std::max<uint64_t>(kmax[t.key_idx], e - t.off);
-  });
   if (n == 0) amin = amax = 0;
   const uint64_t base = amin & ~uint64_t(255);
   const uint64_t span = amax - base;
@@ -1612,7 +1703,6 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   S.ks = it.ks;
   S.out = out;
   S.n = n;
-  S.inflight = true;
 }
 
 // (Issuing the next chunk's arena DMA right after the current chunk's copies
@@ -1629,11 +1719,6 @@ void process_item(Device* d, size_t dslot, Item& it) {
     }
     for (size_t c = 0; c + 1 < it.cuts.size(); ++c) {
       const size_t lo = it.cuts[c], hi = it.cuts[c + 1];
-      std::string bad;
-      if (!check_jobs(*it.ks, it.arena_len, it.toks + lo, hi - lo, &bad, lo)) {
-        it.t->fail(-1, bad);
-        break;
-      }
       Slot* Sp;
       if (it.zc) {
         Sp = &d->slots[NSLOT + d->next_zslot];
@@ -1644,9 +1729,23 @@ void process_item(Device* d, size_t dslot, Item& it) {
       }
       Slot& S = *Sp;
       const auto tw = std::chrono::steady_clock::now();
-      finish_slot(S);                 // the slot's previous chunk (a ring length ago)
+      {                               // the slot's previous chunk (a ring length ago) completed
+        std::unique_lock<std::mutex> lk(d->cmu);
+        d->scv.wait(lk, [&] { return !S.inflight; });
+      }
       const double wait_ms = pipe_trace() ? ms_since(tw) : 0.0;
-      enqueue_chunk(d, dslot, S, it, it.toks + lo, hi - lo, it.out + lo);
+      try {
+        enqueue_chunk(d, dslot, S, it, it.toks + lo, hi - lo, it.out + lo, lo);
+      } catch (const BadJob& e) {                 // nothing of this chunk was enqueued
+        it.t->fail(-1, e.what());
+        break;
+      }
+      {
+        std::lock_guard<std::mutex> lk(d->cmu);
+        S.inflight = true;
+        d->cq.push_back(&S);
+      }
+      d->ccv.notify_one();
       S.seq = ++d->slot_seq;
       S.host_ms[0] = wait_ms;
       S.chunk_no = (int)enq;
@@ -1659,6 +1758,11 @@ void process_item(Device* d, size_t dslot, Item& it) {
   }
 }
 
+// The device's submission thread: plans and enqueues each queued item's
+// chunks.  Completion runs on a thread of its own (completer_loop), so a
+// submission arriving while earlier chunks are on the device is enqueued at
+// once rather than after the oldest chunk's event fires (small coalesced
+// batches: the device works on several at a time).
 void worker_loop(Device* d, size_t dslot) {
   (void)hipSetDevice(d->id);
   std::unique_lock<std::mutex> lk(d->qmu);
@@ -1666,34 +1770,31 @@ void worker_loop(Device* d, size_t dslot) {
     if (!d->q.empty()) {
       Item it = std::move(d->q.front());
       d->q.pop_front();
-      d->busy = true;
       lk.unlock();
       process_item(d, dslot, it);
       lk.lock();
       continue;
     }
-    // queue empty: complete the in-flight chunks oldest first (blocking on
-    // each; a submission arriving meanwhile is picked up after that chunk)
-    bool any = false;
+    if (d->stop) break;
+    d->qcv.wait(lk, [&] { return d->stop || !d->q.empty(); });
+  }
+}
+
+// Completes the device's in-flight chunks in enqueue order (both slot rings):
+// waits for each chunk's verdict copy, hands the verdicts over, frees the slot.
+void completer_loop(Device* d) {
+  (void)hipSetDevice(d->id);
+  std::unique_lock<std::mutex> lk(d->cmu);
+  while (true) {
+    d->ccv.wait(lk, [&] { return d->cstop || !d->cq.empty(); });
+    if (d->cq.empty()) break;                    // stopping, nothing in flight
+    Slot* S = d->cq.front();
     lk.unlock();
-    {
-      std::lock_guard<std::mutex> g(d->mu);
-      Slot* oldest = nullptr;
-      for (auto& S : d->slots)
-        if (S.inflight && (!oldest || S.seq < oldest->seq)) oldest = &S;
-      if (oldest) {
-        finish_slot(*oldest);
-        any = true;
-      }
-    }
+    finish_slot(*S);
     lk.lock();
-    if (any) continue;
-    if (d->q.empty()) {
-      d->busy = false;
-      d->idle_cv.notify_all();
-      if (d->stop) break;
-      d->qcv.wait(lk, [&] { return d->stop || !d->q.empty(); });
-    }
+    d->cq.pop_front();
+    S->inflight = false;
+    d->scv.notify_all();
   }
 }
 
@@ -2435,7 +2536,10 @@ jg_ctx* jg_create(const int* devices, int ndev) {
     for (size_t i = 0; i < ctx->devs.size(); ++i) ks->dev.push_back(std::make_shared<DevGen>());
     ctx->ks = ks;
     jg_ctx* c = ctx.release();
-    for (size_t i = 0; i < c->devs.size(); ++i) c->devs[i]->worker = std::thread(worker_loop, c->devs[i].get(), i);
+    for (size_t i = 0; i < c->devs.size(); ++i) {
+      c->devs[i]->worker = std::thread(worker_loop, c->devs[i].get(), i);
+      c->devs[i]->completer = std::thread(completer_loop, c->devs[i].get());
+    }
     c->upgrader = std::thread(upgrade_loop, c);
     return c;
   } catch (const std::exception& e) {
@@ -2459,6 +2563,12 @@ void jg_destroy(jg_ctx* ctx) {
     }
     d->qcv.notify_all();
     if (d->worker.joinable()) d->worker.join();
+    {
+      std::lock_guard<std::mutex> g(d->cmu);
+      d->cstop = true;
+    }
+    d->ccv.notify_all();
+    if (d->completer.joinable()) d->completer.join();
   }
   ctx->publish(nullptr);                           // key generations: handed to the reaper
   reaper().drain();                                // ... and freed before jg_destroy returns

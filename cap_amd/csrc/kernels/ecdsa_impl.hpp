@@ -465,9 +465,9 @@ __device__ __forceinline__ void madd(uint32_t* X, uint32_t* Y, uint32_t* Z, cons
   mp::norm_for_mulf<Fp>(h);                  // P-384: h, r are squared (mulf precondition)
   mp::norm_for_mulf<Fp>(r);
   mp::sqrf<Fp>(hh, h);
+  mp::mulf<Fp>(Z, Z, h);                     // Z3 before hhh and v: h dies at hhh, hh at v
   mp::mulf<Fp>(hhh, h, hh);
   mp::mulf<Fp>(v, X, hh);
-  mp::mulf<Fp>(Z, Z, h);
   uint32_t y1[L];
   mp::copy<Fp>(y1, Y);
   x3_from<Fp>(X, r, hhh, v);

@@ -26,6 +26,9 @@
 #define MP_W 28
 #define MP_MASK 0x0fffffffu
 #define MPD __device__ __forceinline__
+#ifndef JG_P384_COLS
+#define JG_P384_COLS 1
+#endif
 
 namespace mp {
 
@@ -295,15 +298,68 @@ MPD void mont_reduce_p384(uint32_t* r, uint64_t* t) {
   }
 }
 
+// The same product and reduction column by column (product scanning): column
+// k gets its partial products, the reduction terms of the rows that reach it
+// (q_{k-1} 2^4, q_{k-3} (-2^12), q_{k-4} (-2^16), q_{k-13} 2^20) and the carry
+// of column k-1, then yields q_k (k < L) or output limb k - L.  Every term
+// lands in the same column as in mont_reduce_p384's row order, so the value and
+// the column bounds are the same; but only the current column, the 13 pending
+// q's and the output are live instead of 2L 64-bit columns (P-384 point kernel:
+// the register pressure that held it at three waves per SIMD).
+template <bool SQR>
+MPD void mont_mul_p384_cols(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  constexpr int L = P384P::L;
+  const int32_t c4 = opaque_sgpr(16), c12 = opaque_sgpr(-4096), c16 = opaque_sgpr(-65536),
+                c20 = opaque_sgpr(1048576);
+  uint32_t a2[L];
+  if constexpr (SQR) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) a2[i] = a[i] << 1;
+  }
+  int32_t q[L];
+  int64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * L - 1; ++k) {
+    uint64_t col = 0;
+    bool first = true;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int j = k - i;
+      if (j < 0 || j >= L) continue;
+      if constexpr (SQR) {
+        if (j < i) continue;
+        const uint32_t x = i == j ? a[i] : a2[i];
+        if (first) mul64c(col, x, a[j]); else mad64c(col, x, a[j]);
+      } else {
+        if (first) mul64c(col, a[i], b[j]); else mad64c(col, a[i], b[j]);
+      }
+      first = false;
+    }
+    int64_t s = (int64_t)col + carry;
+    if (k >= 1 && k - 1 < L) s += (int64_t)q[k - 1] * (int64_t)c4;
+    if (k >= 3 && k - 3 < L) s += (int64_t)q[k - 3] * (int64_t)c12;
+    if (k >= 4 && k - 4 < L) s += (int64_t)q[k - 4] * (int64_t)c16;
+    if (k >= 13 && k - 13 < L) s += (int64_t)q[k - 13] * (int64_t)c20;
+    if (k < L) q[k] = (int32_t)((uint32_t)s & MP_MASK);
+    else r[k - L] = (uint32_t)s & MP_MASK;
+    carry = s >> MP_W;
+  }
+  r[L - 1] = (uint32_t)carry & MP_MASK;    // column 2L-1: no products, only the carries
+}
+
 // Products for the point-addition hot loop: the field's special-form
 // reduction where it has one (P-384), else mul / sqr.  Precondition (P-384):
 // at least one operand has limbs < 2^28 (squares: the operand itself).
 template <class F>
 MPD void mulf(uint32_t* r, const uint32_t* a, const uint32_t* b) {
   if constexpr (std::is_same<F, P384P>::value) {
+#if JG_P384_COLS
+    mont_mul_p384_cols<false>(r, a, b);
+#else
     uint64_t t[2 * F::L];
     prod<F>(t, a, b);
     mont_reduce_p384(r, t);
+#endif
   } else {
     mul<F>(r, a, b);
   }
@@ -311,9 +367,13 @@ MPD void mulf(uint32_t* r, const uint32_t* a, const uint32_t* b) {
 template <class F>
 MPD void sqrf(uint32_t* r, const uint32_t* a) {
   if constexpr (std::is_same<F, P384P>::value) {
+#if JG_P384_COLS
+    mont_mul_p384_cols<true>(r, a, a);
+#else
     uint64_t t[2 * F::L];
     sqprod<F>(t, a);
     mont_reduce_p384(r, t);
+#endif
   } else {
     sqr<F>(r, a);
   }

@@ -86,6 +86,8 @@ int main(int argc, char** argv) {
   if (callers > 0) {
     std::atomic<size_t> next{0}, ok{0};
     const size_t total = std::min<size_t>(toks.size(), 200000);
+    rusage r0, r1;
+    getrusage(RUSAGE_SELF, &r0);
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int c = 0; c < callers; ++c)
@@ -94,6 +96,10 @@ int main(int argc, char** argv) {
       });
     for (auto& t : th) t.join();
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    getrusage(RUSAGE_SELF, &r1);
+    auto secs = [](const timeval& a, const timeval& b) { return (b.tv_sec - a.tv_sec) + 1e-6 * (b.tv_usec - a.tv_usec); };
+    std::printf("  cpu: user %.2f s sys %.2f s, vol cs %ld invol cs %ld\n", secs(r0.ru_utime, r1.ru_utime),
+                secs(r0.ru_stime, r1.ru_stime), r1.ru_nvcsw - r0.ru_nvcsw, r1.ru_nivcsw - r0.ru_nivcsw);
     const auto st = ks->CoalescingStats();
     std::printf("single-token Validate x %d callers: %zu calls in %.1f ms (%.3f M/s), accepted %zu; %llu batches, max %llu\n",
                 callers, total, dt * 1e3, total / dt / 1e6, ok.load(), (unsigned long long)st.batches,

@@ -4,6 +4,8 @@
 // linked into the product or any test.
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
+#include <thread>
 
 #include "../../include/jg.h"
 
@@ -32,8 +34,15 @@ int jg_submit(jg_ctx*, const uint8_t*, size_t, const jg_tok*, size_t n, uint8_t*
   *t = new jg_ticket{0};
   return 0;
 }
+// HOSTPROF_DEVICE_US: simulated device latency of every submission (the
+// coalescer's behaviour under many concurrent single-token callers)
 int jg_wait(jg_ctx*, jg_ticket* t) {
   delete t;
+  static const long us = [] {
+    const char* e = std::getenv("HOSTPROF_DEVICE_US");
+    return e ? std::atol(e) : 0L;
+  }();
+  if (us > 0) std::this_thread::sleep_for(std::chrono::microseconds(us));
   return 0;
 }
 int jg_debug_fail_verify(jg_ctx*, int) { return 0; }

@@ -1,0 +1,56 @@
+"""The coalesced single-token path (bench.py `single`) under several
+coalescer settings: Validator.Validate per token from N C++ threads on the
+configs[1] pool, per (max_inflight, window_us) and N.
+usage: python tools/single_probe.py [out.json] [inflight,window ...]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    out = sys.argv[1] if len(sys.argv) > 1 else None
+    settings = [tuple(int(x) for x in s.split(",")) for s in sys.argv[2:]] or [(4, 0), (2, 0), (8, 0), (4, 100)]
+    from cap_amd import jwt
+    cpu = bench.cpu_info()
+    kids = ["p256-a", "p256-b", "p256-c", "p256-d"]
+    pool = bench.gen_tokens("ES256", 1 << 16, bench.golden_keypaths(kids), cpu["cores_used"], "single")
+    jwk = [{"kty": "EC", "kid": f"kid-{i:02d}", "crv": "P-256", **xy} for i, xy in enumerate(bench.p256_jwk_xy(kids))]
+    jwks = json.dumps({"keys": jwk}).encode()
+    ks, err = jwt.NewJSONWebKeySet(None, "https://bench.example/jwks", "",
+                                   lambda url, ca: {"status": 200, "body": jwks, "max_age": 3600})
+    v, _ = jwt.NewValidator(ks)
+    e = jwt.Expected(Issuer="https://example.com/", Audiences=["www.example.com"], SigningAlgorithms=["ES256"],
+                     Now=lambda: 1611699344 + 60)
+    blob = b"\n".join(pool)
+    v.ValidateBlob(blob, e)
+    ks.WaitTables()
+    res = {"cpu": cpu, "runs": []}
+    for inflight, window in settings:
+        ks.SetCoalescing(max_inflight=inflight, window_us=window)
+        for c in (cpu["cores_used"], 64, 256, 1024):
+            v._impl._concurrent_validate(blob, e._native(), c, 1 << 14)
+            s0 = ks.CoalescingStats()
+            h0 = bench.host_snapshot()
+            r = dict(v._impl._concurrent_validate(blob, e._native(), c, 1 << 17))
+            hd = bench.host_delta(h0, bench.host_snapshot())
+            s1 = ks.CoalescingStats()
+            r["host"] = {k: hd[k] for k in ("utime", "stime", "nvcsw", "nivcsw", "cg_nr_throttled", "cg_throttled_usec",
+                                           "cpu_by_thread_name")}
+            r.update(inflight=inflight, window_us=window, callers=c, value=r["calls"] / r["wall_s"],
+                     mean_batch=r["calls"] / max(1, s1["batches"] - s0["batches"]))
+            res["runs"].append(r)
+            print(f"inflight {inflight} window {window} callers {c}: {r['value'] / 1e6:.3f} M/s p50 {r['p50_us']:.0f} "
+                  f"p99 {r['p99_us']:.0f} us, mean batch {r['mean_batch']:.1f}, accepted {r['accepted']}/{r['calls']}; "
+                  f"cpu {r['host']['utime']:.2f}u {r['host']['stime']:.2f}s throttled {r['host']['cg_throttled_usec'] / 1e3:.0f} ms "
+                  f"top {list(r['host']['cpu_by_thread_name'].items())[:3]}",
+                  flush=True)
+    if out:
+        json.dump(res, open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
