@@ -33,6 +33,7 @@
 #include <stdexcept>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <vector>
 
 #include "jose.hpp"
@@ -276,12 +277,14 @@ class Coalescer {
     std::exception_ptr ex;        // the batch threw (a host-side bug): re-thrown to every caller in it
     std::shared_ptr<std::vector<Req*>> peers;   // the batch's callers to wake (a binary tree) ...
     size_t wpos = 0;                            // ... and this one's position there
-    enum { WAITING = 0, DONE = 1, LEAD = 2 };
-    std::atomic<int> state{WAITING};   // futex word: set by the leader that carried it / handed it the lead
+    Req* next = nullptr;          // the submission stack's link
+    enum { WAITING = 0, DONE = 1 };
+    std::atomic<int> state{WAITING};   // futex word: DONE once a dispatcher has carried it
   };
   // parse + verify a batch of tokens (KeySet::verify_raw)
   using Exec = std::function<std::shared_ptr<const Verified>(const std::vector<std::string_view>&)>;
   explicit Coalescer(Exec exec) : exec_(std::move(exec)) {}
+  ~Coalescer();
   void run(Req* r);               // blocks until r->batch is set (exceptions of the batch re-thrown)
   void configure(const CoalesceConfig& c);
   CoalesceConfig config();
@@ -289,13 +292,21 @@ class Coalescer {
   Stats stats();
  private:
   static void release(const std::vector<Req*>& wake, size_t i);
+  void dispatch_loop();
+  void carry(std::vector<Req*>& batch);
+  void start_locked();            // spawn the dispatchers (threads_mu_ held)
+  void stop_locked();             // stop and join them (threads_mu_ held)
   Exec exec_;
-  std::mutex m_;
-  std::condition_variable window_cv_;
-  std::deque<Req*> q_;
-  int leaders_ = 0;
-  CoalesceConfig cfg_;
-  Stats st_;
+  std::atomic<Req*> head_{nullptr};        // submissions not yet taken (LIFO, lock-free)
+  std::atomic<uint32_t> seq_{0};           // futex word of idle dispatchers: bumped on a push to an empty stack
+  std::atomic<bool> stop_{false};
+  std::atomic<bool> started_{false};
+  std::mutex threads_mu_;
+  std::vector<std::thread> threads_;
+  CoalesceConfig cfg_;                      // threads_mu_
+  std::atomic<size_t> max_batch_{65536};
+  std::atomic<int64_t> window_us_{0};
+  std::atomic<uint64_t> calls_{0}, batches_{0}, max_seen_{0};
 };
 
 class KeySet {

@@ -479,6 +479,20 @@ auto& g_tabs = *new std::map<std::pair<int, int>, std::shared_ptr<SharedTable>>(
 // One in-order stream plus per-class fan-out streams: a mixed batch's classes
 // are each too small to fill 256 CUs alone, so untimed runs put every class's
 // kernel chain on its own stream, joined back before the scatter.
+inline void make_stream(hipStream_t* s, int prio) {
+  if (prio > 0) {
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPCHK(hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest));
+  } else {
+    HIPCHK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+  }
+}
+
+#ifndef JG_LANE_PRIO
+#define JG_LANE_PRIO 0
+#endif
+
 struct Lane {
   hipStream_t stream = nullptr;
   hipStream_t cstream[NCLS] = {};
@@ -487,10 +501,11 @@ struct Lane {
   // creation order (GPU_MAX_HW_QUEUES, 4 by default): the device creates
   // every lane's main stream first so the pipeline slots land on distinct
   // queues and really overlap, then the per-class fan-out streams.
-  void create_main() { HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); }
-  void create_fanout() {
+  // prio: 0 normal, > 0 the device's highest stream priority (A/B: JG_LANE_PRIO)
+  void create_main(int prio = 0) { make_stream(&stream, prio); }
+  void create_fanout(const int* cls_prio = nullptr) {
     for (int c = 1; c < NCLS; ++c) {
-      HIPCHK(hipStreamCreateWithFlags(&cstream[c], hipStreamNonBlocking));
+      make_stream(&cstream[c], cls_prio ? cls_prio[c] : 0);
       HIPCHK(hipEventCreateWithFlags(&ev_done[c], hipEventDisableTiming));
     }
     HIPCHK(hipEventCreateWithFlags(&ev_start, hipEventDisableTiming));
@@ -573,12 +588,12 @@ struct Slot {
   hipEvent_t tr_a = nullptr, tr_b = nullptr, tr_c = nullptr;   // CAPJWT_PIPE_TRACE: H2D start / end, kernels end
   hipEvent_t ev_planned = nullptr, ev_cls[NCLS] = {};            // class-grouped chunks (GroupFan)
   hipEvent_t ev_fed[NCLS] = {};                                  // zero-copy plans: class gathered (GroupFan::fed)
-  double host_ms[5] = {};                                       // wait, plan, enqueue, of which H2D calls, of which sizing
+  double host_ms[7] = {};         // wait, plan, enqueue; of enqueue: H2D calls, sizing, before run_plan, run_plan
   int grows = 0;                                                // buffer reallocations while enqueuing (trace)
   int chunk_no = 0;
-  uint64_t seq = 0;                // enqueue order across both slot rings (oldest completes first)
   size_t reserved = 0;             // chunk capacity (jobs) the buffers were sized for
   uint64_t reserved_epoch = ~0ull; // key table they were sized against
+  PlanScratch plan;                // host plan scratch of the chunk being planned into this slot
   bool inflight = false;            // enqueued, not yet completed (Device::cmu)
   std::shared_ptr<Ticket> ticket;
   KeyStateP ks;                    // key state of the chunk in flight (kept alive until it completes)
@@ -597,8 +612,55 @@ struct Item {                     // one device's share of a submission
   const uint8_t* dev_arena = nullptr;   // device view of a page-locked arena (kernels read it over PCIe)
   size_t chunk = 0, nchunks = 0;
   std::vector<size_t> cuts;       // chunk boundaries (chunk_cuts)
-  bool grouped = false;           // mixed classes: chunks run class-grouped (enqueue_chunk)
+  bool grouped = false;           // mixed classes: chunks run class-grouped (plan_chunk / issue_chunk)
   bool zc = false;                // class-major zero-copy plans (zc_enabled): no arena copy
+};
+
+// A thread that runs one job at a time for its owner (the device worker's
+// planner: run() hands over a job, wait() returns once it has finished).
+class Helper {
+ public:
+  explicit Helper(int device) : th_([this, device] { loop(device); }) {}
+  ~Helper() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void run(std::function<void()> f) {
+    std::lock_guard<std::mutex> g(m_);
+    job_ = std::move(f);
+    busy_ = true;
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    cv_.wait(lk, [&] { return !busy_; });
+  }
+
+ private:
+  void loop(int device) {
+    (void)hipSetDevice(device);
+    std::unique_lock<std::mutex> lk(m_);
+    while (true) {
+      cv_.wait(lk, [&] { return stop_ || job_; });
+      if (!job_) break;                            // stopping
+      auto f = std::move(job_);
+      job_ = nullptr;
+      lk.unlock();
+      f();
+      lk.lock();
+      busy_ = false;
+      cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::function<void()> job_;
+  bool busy_ = false, stop_ = false;
+  std::thread th_;
 };
 
 struct Device {
@@ -619,9 +681,9 @@ struct Device {
   Slot slots[NSLOT + NZSLOT];      // the chunk ring, then the zero-copy plans' ring
   int next_slot = 0, next_lane = 0, next_zslot = 0;
   double gload[3] = {0, 0, 0};    // class-grouped chunks: class cost queued per group lane (relative)
-  uint64_t slot_seq = 0;
   int next_res = 0;                // resident batches staged (CAPJWT_BATCH_LANES)
   std::thread worker, completer;
+  std::unique_ptr<Helper> planner;  // plans a pipeline item's next chunk (process_item)
   std::mutex qmu;
   std::condition_variable qcv;
   std::deque<Item> q;
@@ -630,7 +692,6 @@ struct Device {
   std::condition_variable ccv, scv; // completer: a chunk enqueued / worker: a slot freed
   std::deque<Slot*> cq;            // in-flight chunks, enqueue order
   bool cstop = false;
-  PlanScratch plan;               // worker scratch of the host plan
 };
 
 }  // namespace
@@ -1171,7 +1232,7 @@ void check_device_records(const DevGen& G) {
                                ") differs from the host mirror (tab_w " + std::to_string(G.mirror[k].tab_w) + ")");
 }
 
-// Explicit streams of a class-grouped pipeline chunk (enqueue_chunk): the
+// Explicit streams of a class-grouped pipeline chunk (plan_chunk / issue_chunk): the
 // chunk's control work on `ctrl`, each class chain on cls[c], the verdict
 // scatter on `join` once every class's `done` event has fired.
 struct GroupFan {
@@ -1343,7 +1404,7 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
   mark(marks, "scatter");
   HIPCHK(hipGetLastError());
   // the class streams logged their uses above; the chunk's control stream
-  // logged its plan fill (enqueue_chunk, before `start`); the zero-copy feed's
+  // logged its plan fill (issue_chunk, before `start`); the zero-copy feed's
   // gathers read no key memory
   G.uses.record(s0, gf ? "join lane" : "lane");
 }
@@ -1375,8 +1436,8 @@ void finish_slot(Slot& S) {
     (void)hipEventElapsedTime(&b, g_trace_ref, S.tr_b);
     (void)hipEventElapsedTime(&c, g_trace_ref, S.tr_c);
     (void)hipEventElapsedTime(&dn, g_trace_ref, S.done);
-    std::fprintf(stderr, "[pipe] chunk %3d n=%7zu host wait %.3f plan %.3f enq %.3f (h2d calls %.3f, sizing %.3f, grows %d) | gpu h2d %.3f-%.3f kern-end %.3f done %.3f ms\n",
-                 S.chunk_no, S.n, S.host_ms[0], S.host_ms[1], S.host_ms[2], S.host_ms[3], S.host_ms[4], S.grows, a, b, c, dn);
+    std::fprintf(stderr, "[pipe] chunk %3d n=%7zu host wait %.3f plan %.3f enq %.3f (h2d calls %.3f, sizing %.3f, pre-launch %.3f, launches %.3f, grows %d) | gpu h2d %.3f-%.3f kern-end %.3f done %.3f ms\n",
+                 S.chunk_no, S.n, S.host_ms[0], S.host_ms[1], S.host_ms[2], S.host_ms[3], S.host_ms[4], S.host_ms[5], S.host_ms[6], S.grows, a, b, c, dn);
   }
   auto t = std::move(S.ticket);
   S.ticket.reset();
@@ -1431,7 +1492,7 @@ struct BadJob : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
-// enqueue_chunk's one host pass over a chunk's jobs: validate each (key_idx in
+// plan_chunk's one host pass over a chunk's jobs: validate each (key_idx in
 // the table, spans inside the arena: check_jobs' rule), count the plan's
 // buckets and the (class, alg) pairs, find the arena span, and copy the jobs
 // into the pinned plan block (ht).  Chunks of 64 k jobs and more are cut over
@@ -1506,12 +1567,27 @@ void scan_chunk(const KeyState& K, const jg_tok* toks, size_t n, size_t arena_le
   }
 }
 
-void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_tok* toks, size_t n, uint8_t* out,
-                   size_t job_base) {
-  const auto t_start = std::chrono::steady_clock::now();
-  const int grows0 = g_grows.load(std::memory_order_relaxed);
+// A chunk planned on the host (plan_chunk), ready for issue_chunk.
+struct ChunkPlan {
+  Plan P;
+  size_t n = 0, bytes = 0;
+  const uint8_t* src = nullptr;    // arena bytes to DMA (nullptr: none)
+  uint64_t base = 0, dbase = 0;
+  bool zc = false;
+  std::chrono::steady_clock::time_point t_start;
+};
+
+// The host half of a chunk: buffers sized, jobs validated and copied into the
+// slot's pinned plan block, the arena span staged, the plan laid out.  Touches
+// only slot S (free: its previous chunk completed) and read-only key state, so
+// the device worker runs it for the next chunk on its planner thread while it
+// issues the current one (process_item).
+void plan_chunk(Slot& S, const Item& it, const jg_tok* toks, size_t n, size_t job_base, ChunkPlan& CP) {
+  CP = ChunkPlan{};
+  CP.n = n;
+  CP.t_start = std::chrono::steady_clock::now();
+  const auto t_start = CP.t_start;
   const KeyState& K = *it.ks;
-  const DevGen& G = *K.dev[dslot];
   if (S.reserved != it.chunk || S.reserved_epoch != K.epoch) {
     // bytes per job from a sample (jobs are validated by scan_chunk below:
     // a bad span must not size the buffers)
@@ -1530,9 +1606,9 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   uint8_t* hb = (uint8_t*)S.h_meta.get(L.bytes);
   jg_tok* ht = (jg_tok*)(hb + L.toks_off);
   ChunkScan scan;
-  scan_chunk(K, toks, n, it.arena_len, job_base, ht, it.zc, d->plan, scan);
+  scan_chunk(K, toks, n, it.arena_len, job_base, ht, it.zc, S.plan, scan);
   uint64_t amin = scan.amin, amax = scan.amax, need = scan.need, seen[2] = {scan.seen[0], scan.seen[1]};
-  std::vector<uint64_t>& kmax = d->plan.kmax;
+  std::vector<uint64_t>& kmax = S.plan.kmax;
   if (n == 0) amin = amax = 0;
   const uint64_t base = amin & ~uint64_t(255);
   const uint64_t span = amax - base;
@@ -1549,7 +1625,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
   uint64_t zbytes = 0;
   uint64_t* zc_tab = (uint64_t*)(hb + L.zc_off);   // [NB] base | [NB] first slot | [NB] stride
   if (zc) {
-    const int64_t* tot = d->plan.total.data();
+    const int64_t* tot = S.plan.total.data();
     for (size_t k = 0; k < NB; ++k) {
       const uint64_t slots = k + 1 < NB ? (uint64_t)(tot[k] + WAVE - 1) / WAVE * WAVE : 0;   // the reject bucket is never prepped
       const uint64_t stride = slots ? (kmax[k] + 30 + 15) & ~uint64_t(15) : 0;
@@ -1587,22 +1663,42 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
     dbase = 0;
     src = h;
   }
-  Plan P;
-  plan_layout(K, ht, n, P, d->plan, false, seen);
+  Plan& P = CP.P;
+  plan_layout(K, ht, n, P, S.plan, false, seen);
   uint64_t* cur = (uint64_t*)(hb + L.cur_off);
   int64_t* pad = (int64_t*)(hb + L.pad_off);
   for (size_t k = 0; k < NB; ++k) {
-    const auto r = pad_range(d->plan, k, P, NB - 1);
-    cur[k] = (uint64_t)d->plan.start[k];
+    const auto r = pad_range(S.plan, k, P, NB - 1);
+    cur[k] = (uint64_t)S.plan.start[k];
     pad[2 * k] = r.first;
     pad[2 * k + 1] = r.second;
-    if (zc) zc_tab[NB + k] = (uint64_t)d->plan.start[k];
+    if (zc) zc_tab[NB + k] = (uint64_t)S.plan.start[k];
   }
+  CP.bytes = bytes;
+  CP.src = src;
+  CP.base = base;
+  CP.dbase = dbase;
+  CP.zc = zc;
+  if (pipe_trace()) S.host_ms[1] = ms_since(t_start);
+}
+
+// The device half of a chunk planned by plan_chunk: arena DMA, plan fill,
+// the class launches and the verdict copy (device worker thread only).
+void issue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const ChunkPlan& CP, uint8_t* out) {
+  const int grows0 = g_grows.load(std::memory_order_relaxed);
+  const KeyState& K = *it.ks;
+  const DevGen& G = *K.dev[dslot];
+  const Plan& P = CP.P;
+  const size_t n = CP.n, NB = K.keys.size() + 1, bytes = CP.bytes;
+  const PlanBlock L(NB, n);
+  uint8_t* hb = (uint8_t*)S.h_meta.p;
+  const uint8_t* src = CP.src;
+  const uint64_t base = CP.base, dbase = CP.dbase;
+  const bool zc = CP.zc;
   Lane& LN = d->lanes[d->next_lane];
   d->next_lane = (d->next_lane + 1) % NLANE;
   hipStream_t s = LN.stream;
   const bool tr = pipe_trace();
-  S.host_ms[1] = tr ? ms_since(t_start) : 0.0;
   const auto t_enq = std::chrono::steady_clock::now();
   // The arena span goes over PCIe on the copy stream's DMA engine (spans of
   // consecutive chunks back to back); the rest of the chunk runs on a compute
@@ -1686,12 +1782,15 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
     launch_plan_fill(fa, fs);
     G.uses.record(fs, "plan fill");                // reads the generation's class table
   }
+  const auto t_run = std::chrono::steady_clock::now();
+  if (tr) S.host_ms[5] = ms_since(t_enq);
   if (grouped) {
     run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, &gf);
     s = gf.join;                                   // verdicts leave once every class is done
   } else {
     run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false);
   }
+  if (tr) S.host_ms[6] = ms_since(t_run);
   if (tr) HIPCHK(hipEventRecord(S.tr_c, s));
   S.h_verdict.get(std::max<size_t>(n, 1));
   launch_copy(S.bufs.verdict.p, S.h_verdict.dp, n, s);
@@ -1710,6 +1809,7 @@ void enqueue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const jg_to
 // 262 k chunks, profiles/r04_s12/; not kept.)
 void process_item(Device* d, size_t dslot, Item& it) {
   size_t enq = 0;
+  const size_t nch = it.cuts.size() - 1;
   try {
     std::lock_guard<std::mutex> g(d->mu);
     HIPCHK(hipSetDevice(d->id));
@@ -1717,8 +1817,7 @@ void process_item(Device* d, size_t dslot, Item& it) {
       if (!g_trace_ref) HIPCHK(hipEventCreate(&g_trace_ref));
       HIPCHK(hipEventRecord(g_trace_ref, d->copy));
     }
-    for (size_t c = 0; c + 1 < it.cuts.size(); ++c) {
-      const size_t lo = it.cuts[c], hi = it.cuts[c + 1];
+    auto take_slot = [&]() -> Slot* {
       Slot* Sp;
       if (it.zc) {
         Sp = &d->slots[NSLOT + d->next_zslot];
@@ -1727,34 +1826,82 @@ void process_item(Device* d, size_t dslot, Item& it) {
         Sp = &d->slots[d->next_slot];
         d->next_slot = (d->next_slot + 1) % NSLOT;
       }
-      Slot& S = *Sp;
       const auto tw = std::chrono::steady_clock::now();
       {                               // the slot's previous chunk (a ring length ago) completed
         std::unique_lock<std::mutex> lk(d->cmu);
-        d->scv.wait(lk, [&] { return !S.inflight; });
+        d->scv.wait(lk, [&] { return !Sp->inflight; });
       }
-      const double wait_ms = pipe_trace() ? ms_since(tw) : 0.0;
+      Sp->host_ms[0] = pipe_trace() ? ms_since(tw) : 0.0;
+      return Sp;
+    };
+    auto plan = [&](Slot* S, size_t c, ChunkPlan& cp) {
+      const size_t lo = it.cuts[c], hi = it.cuts[c + 1];
+      plan_chunk(*S, it, it.toks + lo, hi - lo, lo, cp);
+    };
+    // Chunk c is issued on this thread while chunk c + 1 is planned on the
+    // planner thread (its own slot): the host's per-chunk work is the longer
+    // of the two rather than their sum (configs[4] stream: planning ~1.2 ms
+    // and issuing ~2 ms per 262 k-job chunk, against ~3.2 ms of device work).
+    ChunkPlan cp[2];
+    int ci = 0;
+    Slot* cur = take_slot();
+    bool ok = true;
+    try {
+      plan(cur, 0, cp[0]);
+    } catch (const BadJob& e) {                   // nothing of this chunk was enqueued
+      it.t->fail(-1, e.what());
+      ok = false;
+    }
+    for (size_t c = 0; ok && c < nch; ++c) {
+      Slot* nxt = nullptr;
+      std::exception_ptr nerr;
+#ifndef JG_NO_PLANNER
+#define JG_NO_PLANNER 0
+#endif
+      auto plan_next = [&, c] {
+        try {
+          plan(nxt, c + 1, cp[ci ^ 1]);
+        } catch (...) {
+          nerr = std::current_exception();
+        }
+      };
+      if (c + 1 < nch) {
+        nxt = take_slot();
+        if (!JG_NO_PLANNER) d->planner->run(plan_next);
+      }
       try {
-        enqueue_chunk(d, dslot, S, it, it.toks + lo, hi - lo, it.out + lo, lo);
-      } catch (const BadJob& e) {                 // nothing of this chunk was enqueued
-        it.t->fail(-1, e.what());
-        break;
+        issue_chunk(d, dslot, *cur, it, cp[ci], it.out + it.cuts[c]);
+      } catch (...) {
+        if (nxt) d->planner->wait();
+        throw;
       }
+      cur->chunk_no = (int)enq;
       {
         std::lock_guard<std::mutex> lk(d->cmu);
-        S.inflight = true;
-        d->cq.push_back(&S);
+        cur->inflight = true;
+        d->cq.push_back(cur);
       }
       d->ccv.notify_one();
-      S.seq = ++d->slot_seq;
-      S.host_ms[0] = wait_ms;
-      S.chunk_no = (int)enq;
       ++enq;
+      if (nxt) {
+        if (JG_NO_PLANNER) plan_next();
+        d->planner->wait();
+        if (nerr) {
+          try {
+            std::rethrow_exception(nerr);
+          } catch (const BadJob& e) {             // chunk c + 1 and later: not enqueued
+            it.t->fail(-1, e.what());
+            ok = false;
+          }
+        }
+        cur = nxt;
+        ci ^= 1;
+      }
     }
-    if (enq < it.nchunks) it.t->done_chunks(it.nchunks - enq);
+    if (enq < nch) it.t->done_chunks(nch - enq);
   } catch (const std::exception& e) {
     it.t->fail(-2, e.what());
-    it.t->done_chunks(it.nchunks - enq);
+    it.t->done_chunks(nch - enq);
   }
 }
 
@@ -2512,12 +2659,16 @@ jg_ctx* jg_create(const int* devices, int ndev) {
       d->id = id;
       HIPCHK(hipSetDevice(id));
       HIPCHK(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
-      for (auto& l : d->lanes) l.create_main();
+      // JG_LANE_PRIO (A/B): the EC / Ed25519 class group's pipeline lane and
+      // the resident batches' EC / Ed25519 class streams at high priority
+      for (int l = 0; l < NLANE; ++l) d->lanes[l].create_main(JG_LANE_PRIO && l == 2 ? 1 : 0);
       d->lane0.create_main();
       d->lane1.create_main();
+      int cprio[NCLS] = {};
+      for (int c = CLS_P256; c < NCLS; ++c) cprio[c] = JG_LANE_PRIO ? 1 : 0;
       for (auto& l : d->lanes) l.create_fanout();
-      d->lane0.create_fanout();
-      d->lane1.create_fanout();
+      d->lane0.create_fanout(cprio);
+      d->lane1.create_fanout(cprio);
       for (auto& s : d->slots) {
         HIPCHK(hipEventCreateWithFlags(&s.done, pipe_trace() ? hipEventDefault : hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
@@ -2537,6 +2688,7 @@ jg_ctx* jg_create(const int* devices, int ndev) {
     ctx->ks = ks;
     jg_ctx* c = ctx.release();
     for (size_t i = 0; i < c->devs.size(); ++i) {
+      c->devs[i]->planner = std::make_unique<Helper>(c->devs[i]->id);
       c->devs[i]->worker = std::thread(worker_loop, c->devs[i].get(), i);
       c->devs[i]->completer = std::thread(completer_loop, c->devs[i].get());
     }
@@ -2569,6 +2721,7 @@ void jg_destroy(jg_ctx* ctx) {
     }
     d->ccv.notify_all();
     if (d->completer.joinable()) d->completer.join();
+    d->planner.reset();
   }
   ctx->publish(nullptr);                           // key generations: handed to the reaper
   reaper().drain();                                // ... and freed before jg_destroy returns

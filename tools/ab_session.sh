@@ -2,13 +2,15 @@
 # step under its own time limit; results under gpurun_out/ab/.
 #   bash tools/ab_session.sh STEP ...
 # steps:
-#   cfg3:NAME[:LIB]      tools/config_probe.py eddsa_es384 (LIB: a cap_amd/ab_*.so)
+#   cfg3:NAME[:LIB]      tools/config_probe.py eddsa_es384 (LIB: a cap_amd/ab_*.so, or VAR=VALUE)
 #   cfg2:NAME[:LIB]      tools/config_probe.py ps512
 #   c5:NAME[:LIB]        bench.py --configs-only (configs[2..4] lines, no refresh / e2e)
 #   es256:NAME[:LIB]     bench.py ES256 line only
 #   small:THREADS        tools/small_batch_probe.py
 #   single[:S+S...]      tools/single_probe.py (S = inflight,window_us)
 #   ktrace               tools/small_batch_trace.sh (small-batch kernel trace)
+#   valu                 tools/microbench/valu_rates (VALU instruction issue rates)
+#   sys                  tools/single_sys_probe.sh (single-token path at many callers)
 #   trace:CHUNK          tools/gpu_zctrace.sh (configs[4] stream kernel trace)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -17,7 +19,11 @@ mkdir -p $O
 for step in "$@"; do
   IFS=: read -r kind name lib <<< "$step"
   envs=()
-  [ -n "$lib" ] && envs=(CAPJWT_LIB="$GRAFT_REPO_ROOT/cap_amd/$lib")
+  case "$lib" in
+    "") ;;
+    *=*) envs=("$lib") ;;                        # an environment assignment
+    *) envs=(CAPJWT_LIB="$GRAFT_REPO_ROOT/cap_amd/$lib") ;;
+  esac
   echo "== $step $(date +%T)"
   case $kind in
     cfg3) env "${envs[@]}" timeout -k 10 300 python3 -u tools/config_probe.py eddsa_es384 > $O/cfg3_$name.json 2> $O/cfg3_$name.err || { echo FAIL; tail -5 $O/cfg3_$name.err; exit 1; }; cat $O/cfg3_$name.json ;;
@@ -27,6 +33,8 @@ for step in "$@"; do
     small) timeout -k 10 300 python3 -u tools/small_batch_probe.py $O/small_$name.json $name > $O/small_$name.txt 2>&1 || { echo FAIL; tail -5 $O/small_$name.txt; exit 1; }; cat $O/small_$name.txt ;;
     single) timeout -k 10 400 python3 -u tools/single_probe.py $O/single.json ${name//+/ } > $O/single.txt 2>&1 || { echo FAIL; tail -5 $O/single.txt; exit 1; }; cat $O/single.txt ;;
     ktrace) bash tools/small_batch_trace.sh || exit 1 ;;
+    valu) timeout -k 10 120 tools/microbench/valu_rates > $O/valu.txt 2>&1 || { echo FAIL; cat $O/valu.txt; exit 1; }; cat $O/valu.txt ;;
+    sys) bash tools/single_sys_probe.sh || exit 1 ;;
     trace) bash tools/gpu_zctrace.sh ab/trace_$name $name || exit 1 ;;
   esac
 done

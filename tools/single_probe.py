@@ -31,21 +31,23 @@ def main():
     res = {"cpu": cpu, "runs": []}
     for inflight, window in settings:
         ks.SetCoalescing(max_inflight=inflight, window_us=window)
-        for c in (cpu["cores_used"], 64, 256, 1024):
+        callers = os.environ.get("PROBE_CALLERS")
+        for c in ([int(x) for x in callers.split(",")] if callers else (cpu["cores_used"], 64, 256, 1024)):
             v._impl._concurrent_validate(blob, e._native(), c, 1 << 14)
             s0 = ks.CoalescingStats()
             h0 = bench.host_snapshot()
             r = dict(v._impl._concurrent_validate(blob, e._native(), c, 1 << 17))
             hd = bench.host_delta(h0, bench.host_snapshot())
             s1 = ks.CoalescingStats()
-            r["host"] = {k: hd[k] for k in ("utime", "stime", "nvcsw", "nivcsw", "cg_nr_throttled", "cg_throttled_usec",
+            r["host"] = {k: hd[k] for k in ("utime", "stime", "minflt", "nvcsw", "nivcsw", "cg_nr_throttled", "cg_throttled_usec",
                                            "cpu_by_thread_name")}
             r.update(inflight=inflight, window_us=window, callers=c, value=r["calls"] / r["wall_s"],
                      mean_batch=r["calls"] / max(1, s1["batches"] - s0["batches"]))
             res["runs"].append(r)
             print(f"inflight {inflight} window {window} callers {c}: {r['value'] / 1e6:.3f} M/s p50 {r['p50_us']:.0f} "
                   f"p99 {r['p99_us']:.0f} us, mean batch {r['mean_batch']:.1f}, accepted {r['accepted']}/{r['calls']}; "
-                  f"cpu {r['host']['utime']:.2f}u {r['host']['stime']:.2f}s throttled {r['host']['cg_throttled_usec'] / 1e3:.0f} ms "
+                  f"cpu {r['host']['utime']:.2f}u {r['host']['stime']:.2f}s throttled {r['host']['cg_throttled_usec'] / 1e3:.0f} ms minflt {r['host']['minflt']} "
+                  f"cs {r['host']['nvcsw']}/{r['host']['nivcsw']} "
                   f"top {list(r['host']['cpu_by_thread_name'].items())[:3]}",
                   flush=True)
     if out:
