@@ -539,9 +539,15 @@ def measure_single(pool, kids_jwk, threads, callers_list=None, total=1 << 18):
     for c in callers_list or (threads, 256, 1024):
         v._impl._concurrent_validate(blob, e._native(), c, min(total, 1 << 15))      # warm the callers' path
         st0 = ks.CoalescingStats()
+        h0 = host_snapshot()
         r = dict(v._impl._concurrent_validate(blob, e._native(), c, total))
+        hd = host_delta(h0, host_snapshot())
         st1 = ks.CoalescingStats()
         batches = st1["batches"] - st0["batches"]
+        # CPU the process spent per call, and whether the cgroup quota throttled it
+        r["host"] = {"cpu_us_per_call": (hd["utime"] + hd["stime"]) / max(1, r["calls"]) * 1e6,
+                     "stime_s": hd["stime"], "cg_throttled_ms": hd["cg_throttled_usec"] / 1e3,
+                     "voluntary_cs": hd["nvcsw"]}
         r["value"] = r["calls"] / r["wall_s"]
         r["mean_batch"] = r["calls"] / max(1, batches)
         if r["accepted"] != r["calls"]:
@@ -552,7 +558,8 @@ def measure_single(pool, kids_jwk, threads, callers_list=None, total=1 << 18):
             "p99_us": head["p99_us"], "by_callers": out,
             "note": "Validator.Validate per token from N concurrent host threads (one call per token, as Go callers "
                     "do), coalesced into device batches by the key set; value/p50/p99 at N = host_threads; "
-                    "by_callers: the same at more concurrent requests. Not the headline."}
+                    "by_callers: the same at more concurrent requests (host: CPU per call, cgroup throttling; "
+                    "the process sees every CPU of the box under a 16-CPU quota). Not the headline."}
 
 
 E2E_KIDS = ["p256-a", "p256-b", "p256-c", "p256-d"]
@@ -992,7 +999,7 @@ def run_configs(ctx, args, threads, rank, world, dist):
     # plan, kernels, verdicts back), chunks overlapping
     share = 10_000_000 // 8
     arena, toks = pack(pool, algs, keyidx, share)
-    st = measure_pcie(ctx, arena, toks, iters=4, chunks=("zc", 262144, 524288), warm=3)
+    st = measure_pcie(ctx, arena, toks, iters=4, chunks=("zc", 196608, 262144, 524288), warm=3)
     st["workload"] = f"{share} tokens per GPU (10M / 8) streamed with H2D"
     line["stream"] = st
     del arena, toks

@@ -16,6 +16,7 @@
 #include "cap_jwt.hpp"
 
 #include <linux/futex.h>
+#include <pthread.h>
 #include <sched.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -1192,6 +1193,7 @@ void Coalescer::run(Req* r) {
 }
 
 void Coalescer::dispatch_loop() {
+  pthread_setname_np(pthread_self(), "capjwt-batch");
   std::vector<Req*> all, batch;
   while (!stop_.load()) {
     const uint32_t s = seq_.load(std::memory_order_seq_cst);

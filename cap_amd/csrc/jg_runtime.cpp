@@ -19,6 +19,7 @@
 // each chunk's kernels run on one of NLANE compute streams (+ per-class
 // fan-out streams) once its copy event fires, overlapping the next copies.  One worker thread per device drains a FIFO of submitted
 // work, so chunks of consecutive submissions overlap as well.
+#include <pthread.h>
 #include <hip/hip_runtime.h>
 #include <sched.h>
 
@@ -155,6 +156,11 @@ std::vector<size_t> chunk_cuts(size_t lo, size_t hi, size_t C, size_t first = 40
   const size_t tail = C / 4;
   if (tail_chunk && cut.size() > 2 && tail >= 1024 && cut.back() - cut[cut.size() - 2] > tail)
     cut.insert(cut.end() - 1, cut.back() - tail);
+  else if (!tail_chunk && cut.size() > 2 && cut.back() - cut[cut.size() - 2] < C / 8)
+    // a remainder of a few thousand jobs would end the item with a whole
+    // latency-bound kernel chain of its own (configs[4] stream: 4.8 k jobs,
+    // +1.5 ms after the last full chunk): the last full chunk takes it
+    cut.erase(cut.end() - 2);
   return cut;
 }
 
@@ -479,46 +485,37 @@ auto& g_tabs = *new std::map<std::pair<int, int>, std::shared_ptr<SharedTable>>(
 // One in-order stream plus per-class fan-out streams: a mixed batch's classes
 // are each too small to fill 256 CUs alone, so untimed runs put every class's
 // kernel chain on its own stream, joined back before the scatter.
-inline void make_stream(hipStream_t* s, int prio) {
-  if (prio > 0) {
-    int least = 0, greatest = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HIPCHK(hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest));
-  } else {
-    HIPCHK(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-  }
-}
-
-#ifndef JG_LANE_PRIO
-#define JG_LANE_PRIO 0
-#endif
-
 struct Lane {
   hipStream_t stream = nullptr;
-  hipStream_t cstream[NCLS] = {};
+  hipStream_t cstream[NCLS] = {};   // fan-out stream of each class (resident batches; may alias)
+  std::vector<hipStream_t> fan;     // the fan-out streams themselves
   hipEvent_t ev_start = nullptr, ev_done[NCLS] = {};
   // Streams are bound to the process's hardware queues round-robin in
   // creation order (GPU_MAX_HW_QUEUES, 4 by default): the device creates
   // every lane's main stream first so the pipeline slots land on distinct
-  // queues and really overlap, then the per-class fan-out streams.
-  // prio: 0 normal, > 0 the device's highest stream priority (A/B: JG_LANE_PRIO)
-  void create_main(int prio = 0) { make_stream(&stream, prio); }
-  void create_fanout(const int* cls_prio = nullptr) {
+  // queues and really overlap, then the resident lanes' fan-out streams, each
+  // lane's back to back (distinct queues while there are no more than the
+  // process has).
+  void create_main() { HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)); }
+  // group[c]: class c's fan-out stream (0 .. ngroups-1)
+  void create_fanout(const int* group, int ngroups) {
+    fan.assign((size_t)ngroups, nullptr);
+    for (auto& f : fan) HIPCHK(hipStreamCreateWithFlags(&f, hipStreamNonBlocking));
     for (int c = 1; c < NCLS; ++c) {
-      make_stream(&cstream[c], cls_prio ? cls_prio[c] : 0);
+      cstream[c] = fan[(size_t)group[c]];
       HIPCHK(hipEventCreateWithFlags(&ev_done[c], hipEventDisableTiming));
     }
     HIPCHK(hipEventCreateWithFlags(&ev_start, hipEventDisableTiming));
   }
   void sync() {
     if (stream) (void)hipStreamSynchronize(stream);
-    for (int c = 1; c < NCLS; ++c)
-      if (cstream[c]) (void)hipStreamSynchronize(cstream[c]);
+    for (hipStream_t f : fan) (void)hipStreamSynchronize(f);
   }
   void destroy() {
     sync();
+    for (hipStream_t f : fan) (void)hipStreamDestroy(f);
+    fan.clear();
     for (int c = 1; c < NCLS; ++c) {
-      if (cstream[c]) (void)hipStreamDestroy(cstream[c]);
       if (ev_done[c]) (void)hipEventDestroy(ev_done[c]);
       cstream[c] = nullptr;
       ev_done[c] = nullptr;
@@ -529,6 +526,14 @@ struct Lane {
     stream = nullptr;
   }
 };
+
+// Resident batches: one fan-out stream per class.  Sharing one stream among
+// the EC / Ed25519 classes (one per RSA class + one for the rest: no class
+// chain behind an RSA chain on a shared hardware queue) measured 75.9 vs
+// 83.3 M/s on configs[4]: the short, GPU-underfilling EC launches gain more
+// from running beside each other (profiles/r05_s2/session_f.log).
+constexpr int RES_GROUP[NCLS] = {0, 0, 1, 2, 3, 4, 5, 6};
+constexpr int RES_NGROUPS = 7;
 
 struct Bufs {
   // jobs: the plan's padded JobDev array; perm (resident batches only): padded
@@ -642,6 +647,7 @@ class Helper {
 
  private:
   void loop(int device) {
+    pthread_setname_np(pthread_self(), "capjwt-plan");
     (void)hipSetDevice(device);
     std::unique_lock<std::mutex> lk(m_);
     while (true) {
@@ -1250,8 +1256,9 @@ struct GroupFan {
   ZcGatherArgs gather{};          // begin / end set per class
 };
 
+// vpad_zeroed: the device plan fill zeroed every padded slot's verdict (pipeline chunks)
 void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, const Plan& P, jg_batch* marks,
-              bool fanout = true, const GroupFan* gf = nullptr) {
+              bool fanout = true, const GroupFan* gf = nullptr, bool vpad_zeroed = false) {
   if (check_keys_env()) check_device_records(G);
   const bool timed = marks && marks->timing;
   int nact = 0;
@@ -1260,7 +1267,7 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
   const int64_t np = P.npad;
   const hipStream_t s0 = gf ? gf->join : L->stream;
   mark(marks, "begin");
-  HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, gf ? gf->ctrl : s0));
+  if (!vpad_zeroed) HIPCHK(hipMemsetAsync(B->vpad.p, 0, np, gf ? gf->ctrl : s0));
   if (gf) HIPCHK(hipEventRecord(gf->start, gf->ctrl));
   PrepArgs pa{};
   pa.arena = (const uint8_t*)B->arena.p;
@@ -1588,7 +1595,7 @@ void plan_chunk(Slot& S, const Item& it, const jg_tok* toks, size_t n, size_t jo
   CP.t_start = std::chrono::steady_clock::now();
   const auto t_start = CP.t_start;
   const KeyState& K = *it.ks;
-  if (S.reserved != it.chunk || S.reserved_epoch != K.epoch) {
+  if (S.reserved < std::max(it.chunk, n) || S.reserved_epoch != K.epoch) {
     // bytes per job from a sample (jobs are validated by scan_chunk below:
     // a bad span must not size the buffers)
     double bpj = 0;
@@ -1779,16 +1786,17 @@ void issue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const ChunkPl
     fa.pad = (const int64_t*)(dm + L.pad_off);
     fa.jobs = (JobDev*)S.bufs.jobs.p;
     fa.perm = (int32_t*)S.bufs.perm.p;
+    fa.vpad = (uint8_t*)S.bufs.vpad.p;
     launch_plan_fill(fa, fs);
     G.uses.record(fs, "plan fill");                // reads the generation's class table
   }
   const auto t_run = std::chrono::steady_clock::now();
   if (tr) S.host_ms[5] = ms_since(t_enq);
   if (grouped) {
-    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, &gf);
+    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, &gf, true);
     s = gf.join;                                   // verdicts leave once every class is done
   } else {
-    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false);
+    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, nullptr, true);
   }
   if (tr) S.host_ms[6] = ms_since(t_run);
   if (tr) HIPCHK(hipEventRecord(S.tr_c, s));
@@ -1911,6 +1919,7 @@ void process_item(Device* d, size_t dslot, Item& it) {
 // once rather than after the oldest chunk's event fires (small coalesced
 // batches: the device works on several at a time).
 void worker_loop(Device* d, size_t dslot) {
+  pthread_setname_np(pthread_self(), "capjwt-submit");
   (void)hipSetDevice(d->id);
   std::unique_lock<std::mutex> lk(d->qmu);
   while (true) {
@@ -1930,6 +1939,7 @@ void worker_loop(Device* d, size_t dslot) {
 // Completes the device's in-flight chunks in enqueue order (both slot rings):
 // waits for each chunk's verdict copy, hands the verdicts over, frees the slot.
 void completer_loop(Device* d) {
+  pthread_setname_np(pthread_self(), "capjwt-done");
   (void)hipSetDevice(d->id);
   std::unique_lock<std::mutex> lk(d->cmu);
   while (true) {
@@ -2522,6 +2532,7 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
 }
 
 void upgrade_loop(jg_ctx* ctx) {
+  pthread_setname_np(pthread_self(), "capjwt-widen");
   std::set<std::string> skip;     // tables that did not fit (retried after the next key load)
   std::unique_lock<std::mutex> lk(ctx->up_mu);
   while (true) {
@@ -2614,6 +2625,8 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
       for (size_t k = 0; k <= parts; ++k) it.cuts.push_back(it.lo + n * k / parts);
       it.chunk = (n + parts - 1) / parts;
     } else {
+      // (a ramp from C / 2 or from C itself measured slower on the configs[4]
+      // stream: 58.4 / 56.7 vs 62-63 M/s, profiles/r05_s2/session_g.log)
       it.cuts = chunk_cuts(it.lo, it.hi, C, it.grouped ? std::max<size_t>(4096, C / 4) : 4096, !it.grouped);
     }
     it.nchunks = it.cuts.size() - 1;
@@ -2659,16 +2672,12 @@ jg_ctx* jg_create(const int* devices, int ndev) {
       d->id = id;
       HIPCHK(hipSetDevice(id));
       HIPCHK(hipStreamCreateWithFlags(&d->copy, hipStreamNonBlocking));
-      // JG_LANE_PRIO (A/B): the EC / Ed25519 class group's pipeline lane and
-      // the resident batches' EC / Ed25519 class streams at high priority
-      for (int l = 0; l < NLANE; ++l) d->lanes[l].create_main(JG_LANE_PRIO && l == 2 ? 1 : 0);
+      for (auto& l : d->lanes) l.create_main();
       d->lane0.create_main();
       d->lane1.create_main();
-      int cprio[NCLS] = {};
-      for (int c = CLS_P256; c < NCLS; ++c) cprio[c] = JG_LANE_PRIO ? 1 : 0;
-      for (auto& l : d->lanes) l.create_fanout();
-      d->lane0.create_fanout(cprio);
-      d->lane1.create_fanout(cprio);
+      // (pipeline lanes run class-grouped on the lanes themselves: no fan-out)
+      d->lane0.create_fanout(RES_GROUP, RES_NGROUPS);
+      d->lane1.create_fanout(RES_GROUP, RES_NGROUPS);
       for (auto& s : d->slots) {
         HIPCHK(hipEventCreateWithFlags(&s.done, pipe_trace() ? hipEventDefault : hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));

@@ -48,6 +48,7 @@ __global__ void __launch_bounds__(256) k_plan_fill(PlanFillArgs a) {
     a.jobs[p] = JobDev{(uint32_t)o, t.sig_in_len, (uint32_t)(o + t.sig_rel_off),
                        job_pack(c == 0 ? 0u : t.key_idx, (uint32_t)alg, t.sig_b64_len)};
     a.perm[p] = (int32_t)j;
+    a.vpad[p] = 0;
   } else {
     const int64_t k = j - a.n;
     const int64_t b = k >> 6;
@@ -56,6 +57,7 @@ __global__ void __launch_bounds__(256) k_plan_fill(PlanFillArgs a) {
     if (p >= a.pad[2 * b + 1]) return;
     a.jobs[p] = JobDev{0, 0, 0, job_pack(b == a.nkeys ? 0u : (uint32_t)b, JOB_PAD, 0)};
     a.perm[p] = -1;
+    a.vpad[p] = 0;
   }
 }
 
@@ -102,6 +104,7 @@ __global__ void __launch_bounds__(PF_THREADS) k_plan_fill_blocked(PlanFillArgs a
     a.jobs[p] = JobDev{(uint32_t)o, t.sig_in_len, (uint32_t)(o + t.sig_rel_off),
                        job_pack(bk[it] == a.nkeys ? 0u : t.key_idx, (uint32_t)t.alg, t.sig_b64_len)};
     a.perm[p] = (int32_t)j;
+    a.vpad[p] = 0;
   }
 }
 
@@ -114,6 +117,7 @@ __global__ void __launch_bounds__(256) k_plan_pad(PlanFillArgs a) {
   if (p >= a.pad[2 * b + 1]) return;
   a.jobs[p] = JobDev{0, 0, 0, job_pack(b == a.nkeys ? 0u : (uint32_t)b, JOB_PAD, 0)};
   a.perm[p] = -1;
+  a.vpad[p] = 0;
 }
 
 __global__ void __launch_bounds__(256) k_copy16(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16,

@@ -22,6 +22,7 @@ struct PlanFillArgs {
   const int64_t* pad;               // [nkeys + 1][2]: padding lanes [lo, hi) of each bucket
   jgk::JobDev* jobs;
   int32_t* perm;
+  uint8_t* vpad;                    // [npad] verdict per padded slot: zeroed for every slot filled
 };
 void launch_plan_fill(const PlanFillArgs& a, hipStream_t s);
 

@@ -265,6 +265,10 @@ __global__ void __launch_bounds__(64 * EC_SCALAR_WPB) JG_EC_SCALAR_ATTR k_ec_sca
   const int64_t n = a.end - a.begin;
   const int64_t S = (n + B - 1) / B;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the class's first width run empties its exception list (k_ec_point appends
+  // to it after this kernel; a separate memset would be one more dependent
+  // launch on the lane, waiting for a free wave slot behind the modexps)
+  if (a.exc_reset && i == 0) *a.exc_count = 0u;
   if (EC_SCALAR_WPB == 1 && i >= S) return;        // (blocks of several waves keep every thread for the barriers)
   uint32_t acc[L];
   mp::set_const<Fn>(acc, Fn::ONE);
@@ -971,7 +975,6 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
     mk("exact");
     return;
   }
-  if (a.exc_reset) (void)hipMemsetAsync(a.exc_count, 0, sizeof(uint32_t), s);
   // tokens per thread for the batched inversion: keep >= ~8 waves per CU
   // (profiles/r04_s3/scalar_occupancy_ab.json: more waves, fewer tokens per
   // inversion, measured 12-26 % slower)
