@@ -536,7 +536,7 @@ def measure_single(pool, kids_jwk, threads, callers_list=None, total=1 << 18):
     v.ValidateBlob(blob[:1 << 20], e)                # first fetch + key staging
     ks.WaitTables()
     out = {}
-    for c in callers_list or (threads, 256, 1024):
+    for c in callers_list or (threads, 64, 256, 1024):
         v._impl._concurrent_validate(blob, e._native(), c, min(total, 1 << 15))      # warm the callers' path
         st0 = ks.CoalescingStats()
         h0 = host_snapshot()

@@ -194,8 +194,10 @@ void launch_scatter(const int32_t* perm, const uint8_t* verdict_pad, uint8_t* ve
 
 void launch_plan_fill(const PlanFillArgs& a, hipStream_t s) {
   // two-level fill (LDS bucket counts, one global atomic per block and
-  // bucket); the one-level kernel serves key tables past PF_MAX_BUCKETS
-  if (a.nkeys + 1 <= PF_MAX_BUCKETS) {
+  // bucket); the one-level kernel serves key tables past PF_MAX_BUCKETS and
+  // small chunks (jobs and padding in one launch: one dependent launch fewer
+  // on a coalesced single-token batch's chain)
+  if (a.nkeys + 1 <= PF_MAX_BUCKETS && a.n > 4096) {
     constexpr int64_t per = PF_THREADS * PF_ITEMS;
     if (a.n > 0) hipLaunchKernelGGL(k_plan_fill_blocked, dim3((unsigned)((a.n + per - 1) / per)), dim3(PF_THREADS), 0, s, a);
     const int64_t pads = (int64_t)(a.nkeys + 1) * 64;
