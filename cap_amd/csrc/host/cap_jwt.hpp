@@ -293,12 +293,16 @@ class Coalescer {
  private:
   static void release(const std::vector<Req*>& wake, size_t i);
   void dispatch_loop();
+  void serve_stack(std::vector<Req*>& all, std::vector<Req*>& batch);   // one exchange of the stack, carried
   void carry(std::vector<Req*>& batch);
+  void kick();                    // wake one idle dispatcher
   void start_locked();            // spawn the dispatchers (threads_mu_ held)
   void stop_locked();             // stop and join them (threads_mu_ held)
   Exec exec_;
   std::atomic<Req*> head_{nullptr};        // submissions not yet taken (LIFO, lock-free)
-  std::atomic<uint32_t> seq_{0};           // futex word of idle dispatchers: bumped on a push to an empty stack
+  std::atomic<uint32_t> seq_{0};           // futex word of idle dispatchers (kick)
+  std::atomic<int> active_{0};             // batches being carried (callers leading + dispatchers)
+  std::atomic<int> max_inflight_{4};
   std::atomic<bool> stop_{false};
   std::atomic<bool> started_{false};
   std::mutex threads_mu_;

@@ -31,6 +31,42 @@ Arena::~Arena() {
   for (void* b : big_) ::operator delete(b);
 }
 
+void Str::assign_in(Arena* a, const char* p, size_t n) {
+  if (n > 0xFFFFFFF0u) throw std::bad_alloc();
+  if (n <= kInline) {
+    char tmp[kInline + 1];
+    std::memcpy(tmp, p, n);                        // p may point into this string
+    release();
+    std::memcpy(s_, tmp, n);
+    s_[n] = 0;
+    n_ = (uint32_t)n;
+    return;
+  }
+  char* q = static_cast<char*>(a ? a->alloc(n + 1) : ::operator new(n + 1));
+  std::memcpy(q, p, n);
+  q[n] = 0;
+  release();
+  p_ = q;
+  n_ = (uint32_t)n;
+  arena_ = a != nullptr;
+}
+
+void Str::take(Str& o) {
+  if (o.n_ <= kInline) {
+    std::memcpy(s_, o.s_, o.n_ + 1);
+    n_ = o.n_;
+  } else if (o.arena_ && !current_arena()) {       // leaving the batch: to the heap
+    assign_in(nullptr, o.p_, o.n_);
+  } else {
+    p_ = o.p_;
+    n_ = o.n_;
+    arena_ = o.arena_;
+    o.n_ = 0;
+    o.arena_ = false;
+  }
+  o.release();
+}
+
 void* Arena::alloc(size_t bytes) {
   bytes = (bytes + 15) & ~size_t(15);
   used_ += bytes;
@@ -112,6 +148,7 @@ struct Reader {
   const unsigned char* end;
   const unsigned char* begin;
   std::string err;
+  Arena* arena = nullptr;          // the tree's containers and texts go here (parse under an ArenaScope)
 
   bool fail(const char* what) {
     if (err.empty()) {
@@ -148,17 +185,38 @@ struct Reader {
     return true;
   }
 
-  bool string(std::string* out) {
+  bool string(Str* out) {
     // at the opening quote
     ++p;
     const unsigned char* run = p;
     // fast scan: plain ASCII without escapes
     while (p < end && *p != '"' && *p != '\\' && *p >= 0x20 && *p < 0x80) ++p;
     if (p < end && *p == '"') {
+      out->assign_in(arena, (const char*)run, (size_t)(p - run));
+      ++p;
+      return true;
+    }
+    thread_local std::string scratch;
+    if (!string_slow(&scratch, run)) return false;
+    out->assign_in(arena, scratch.data(), scratch.size());
+    return true;
+  }
+
+  bool string(std::string* out) {
+    ++p;
+    const unsigned char* run = p;
+    while (p < end && *p != '"' && *p != '\\' && *p >= 0x20 && *p < 0x80) ++p;
+    if (p < end && *p == '"') {
       out->assign((const char*)run, (size_t)(p - run));
       ++p;
       return true;
     }
+    return string_slow(out, run);
+  }
+
+  // the rest of a string with escapes or non-ASCII bytes: p is past the plain
+  // prefix that starts at `run`
+  bool string_slow(std::string* out, const unsigned char* run) {
     out->assign((const char*)run, (size_t)(p - run));
     while (true) {
       if (p >= end) return fail("");
@@ -240,7 +298,7 @@ struct Reader {
     if (ndig <= 15 && (p >= end || (*p != '.' && *p != 'e' && *p != 'E'))) {
       // an integer below 10^15 is exact in float64: ParseFloat's result without strtod
       v->kind = Value::Number;
-      v->str.assign((const char*)s, (size_t)(p - s));
+      v->str.assign_in(arena, (const char*)s, (size_t)(p - s));
       v->num = neg ? -(double)iv : (double)iv;
       v->num_range_err = false;
       return true;
@@ -257,7 +315,7 @@ struct Reader {
       while (p < end && *p >= '0' && *p <= '9') ++p;
     }
     v->kind = Value::Number;
-    v->str.assign((const char*)s, (size_t)(p - s));
+    v->str.assign_in(arena, (const char*)s, (size_t)(p - s));
     // strconv.ParseFloat: correctly rounded; overflow -> ErrRange, underflow -> 0
     errno = 0;
     const double d = std::strtod(v->str.c_str(), nullptr);
@@ -356,7 +414,7 @@ struct Reader {
   }
 };
 
-void escape_string(std::string& o, const std::string& s) {
+void escape_string(std::string& o, std::string_view s) {
   static const char* hexd = "0123456789abcdef";
   o.push_back('"');
   const unsigned char* p = (const unsigned char*)s.data();
@@ -435,6 +493,7 @@ void marshal_into(std::string& o, const Value& v) {
 
 bool parse(std::string_view text, Value* out, std::string* err) {
   Reader r;
+  r.arena = current_arena();
   r.begin = r.p = (const unsigned char*)text.data();
   r.end = r.p + text.size();
   *out = Value();

@@ -158,6 +158,56 @@ class Vec {
   }
 };
 
+// The text of a String / Number Value: up to 15 bytes inline, longer text on
+// the heap -- or, for text the parser reads into a tree built under an arena
+// scope (json::parse), in that arena.  Always NUL-terminated.  Moves follow
+// Vec's rule: arena text leaving its batch (a move with no arena in scope) is
+// copied to the heap.  A 1M-token batch's claim strings (issuer URLs,
+// subjects) were ~1-3 mallocs and frees per token as std::string.
+class Str {
+ public:
+  Str() { s_[0] = 0; }
+  ~Str() { release(); }
+  Str(const Str& o) : Str() { assign(o.data(), o.size()); }
+  Str(Str&& o) noexcept : Str() { take(o); }
+  explicit Str(std::string_view v) : Str() { assign(v.data(), v.size()); }
+  Str& operator=(const Str& o) {
+    if (this != &o) assign(o.data(), o.size());
+    return *this;
+  }
+  Str& operator=(Str&& o) noexcept {
+    if (this != &o) { release(); take(o); }
+    return *this;
+  }
+  Str& operator=(std::string_view v) { assign(v.data(), v.size()); return *this; }
+  void assign(const char* p, size_t n) { assign_in(nullptr, p, n); }
+  void assign_in(Arena* a, const char* p, size_t n);   // a == nullptr: heap
+  const char* data() const { return n_ <= kInline ? s_ : p_; }
+  const char* c_str() const { return data(); }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  std::string_view view() const { return {data(), n_}; }
+  operator std::string_view() const { return view(); }
+  friend bool operator==(const Str& a, std::string_view b) { return a.view() == b; }
+  friend bool operator!=(const Str& a, std::string_view b) { return a.view() != b; }
+
+ private:
+  static constexpr uint32_t kInline = 15;
+  union {
+    char s_[kInline + 1];
+    char* p_;
+  };
+  uint32_t n_ = 0;
+  bool arena_ = false;
+  void release() {
+    if (n_ > kInline && !arena_) ::operator delete(p_);
+    n_ = 0;
+    arena_ = false;
+    s_[0] = 0;
+  }
+  void take(Str& o);
+};
+
 struct Value;
 using Member = std::pair<std::string, Value>;
 
@@ -167,7 +217,7 @@ struct Value {
   bool b = false;
   bool num_range_err = false;    // the literal overflows float64
   double num = 0;                // Number: float64 value (Go interface{} decoding)
-  std::string str;               // String: decoded text; Number: the literal as written
+  Str str;                       // String: decoded text; Number: the literal as written
   Vec<Value> arr;
   Vec<Member> obj;               // insertion order of first occurrence, last value wins
 

@@ -27,7 +27,7 @@ py::object to_py(const json::Value& v) {
     case json::Value::Null: return py::none();
     case json::Value::Bool: return py::bool_(v.b);
     case json::Value::Number: return py::float_(v.num);
-    case json::Value::String: return py::str(v.str);
+    case json::Value::String: return py::str(v.str.data(), v.str.size());
     case json::Value::Array: {
       py::list l;
       for (const auto& e : v.arr) l.append(to_py(e));
