@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <stdexcept>
 #include <thread>
 #include <unordered_map>
@@ -80,6 +81,98 @@ int host_threads() {
 
 namespace {
 
+// The batch passes' worker threads, started once per process (host_threads()
+// - 1 of them; the calling thread takes part too).  A ValidateBatch call runs
+// ~8 parallel passes; creating 15 threads for each cost the caller a few
+// hundred microseconds per pass.  A pass started from inside a pass (a nested
+// call) gets threads of its own, as before.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool(host_threads() - 1);   // never destroyed: threads live as long as the process
+    return *p;
+  }
+  static bool inside() { return tl_inside_; }
+  // task(i) for i in [0, nt), on the pool's threads and the caller's
+  void run(size_t nt, const std::function<void(size_t)>& task) {
+    Job j;
+    j.fn = &task;
+    j.nt = nt;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(&j);
+    }
+    cv_.notify_all();
+    size_t i;
+    while ((i = take(&j)) < nt) {
+      task(i);
+      finish(&j);
+    }
+    std::unique_lock<std::mutex> lk(j.m);
+    j.cv.wait(lk, [&] { return j.done == nt; });
+  }
+
+ private:
+  struct Job {
+    const std::function<void(size_t)>* fn = nullptr;
+    size_t nt = 0, next = 0;        // next: under the pool's m_
+    size_t done = 0;                // under m
+    std::mutex m;
+    std::condition_variable cv;
+  };
+  explicit HostPool(int n) {
+    for (int t = 0; t < n; ++t) th_.emplace_back([this] { worker(); });
+    for (auto& t : th_) t.detach();
+  }
+  // the next index of j (nt when none is left; the job leaves the queue with its last index)
+  size_t take(Job* j) {
+    std::lock_guard<std::mutex> g(m_);
+    if (j->next >= j->nt) return j->nt;
+    const size_t i = j->next++;
+    if (j->next == j->nt) q_.erase(std::find(q_.begin(), q_.end(), j));
+    return i;
+  }
+  static void finish(Job* j) {
+    std::lock_guard<std::mutex> g(j->m);     // the owner destroys j only after taking this lock
+    if (++j->done == j->nt) j->cv.notify_all();
+  }
+  void worker() {
+    pthread_setname_np(pthread_self(), "capjwt-host");
+    tl_inside_ = true;
+    std::unique_lock<std::mutex> lk(m_);
+    while (true) {
+      cv_.wait(lk, [&] { return !q_.empty(); });
+      Job* j = q_.front();
+      const size_t i = j->next++;
+      if (j->next == j->nt) q_.pop_front();
+      lk.unlock();
+      (*j->fn)(i);
+      finish(j);
+      lk.lock();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<Job*> q_;
+  std::vector<std::thread> th_;
+  static thread_local bool tl_inside_;
+};
+thread_local bool HostPool::tl_inside_ = false;
+
+// fn(i) for i in [0, nt) on nt threads (the pool's, or new ones for a nested call)
+template <class F>
+void run_parallel(size_t nt, F&& fn) {
+  if (!HostPool::inside() && nt <= (size_t)host_threads()) {
+    const std::function<void(size_t)> task = [&fn](size_t i) { fn(i); };
+    HostPool::get().run(nt, task);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (size_t t = 0; t < nt; ++t) th.emplace_back([&fn, t] { fn(t); });
+  for (auto& t : th) t.join();
+}
+
 template <class F>
 void parallel_for(size_t n, int threads, F&& fn) {
   // fn(begin, end): contiguous chunks; small batches stay on the caller's thread
@@ -89,13 +182,7 @@ void parallel_for(size_t n, int threads, F&& fn) {
     if (n) fn((size_t)0, n);
     return;
   }
-  std::vector<std::thread> th;
-  th.reserve(nt);
-  for (size_t t = 0; t < nt; ++t) {
-    const size_t lo = n * t / nt, hi = n * (t + 1) / nt;
-    th.emplace_back([&fn, lo, hi] { fn(lo, hi); });
-  }
-  for (auto& t : th) t.join();
+  run_parallel(nt, [&](size_t t) { fn(n * t / nt, n * (t + 1) / nt); });
 }
 
 // A fixed cut of [0, n) into per-thread ranges, so that several passes over a
@@ -120,10 +207,7 @@ void run_chunks(const Chunks& c, F&& fn) {
     fn((size_t)0, c.b[0], c.b[1]);
     return;
   }
-  std::vector<std::thread> th;
-  th.reserve(c.count());
-  for (size_t t = 0; t < c.count(); ++t) th.emplace_back([&fn, &c, t] { fn(t, c.b[t], c.b[t + 1]); });
-  for (auto& t : th) t.join();
+  run_parallel(c.count(), [&](size_t t) { fn(t, c.b[t], c.b[t + 1]); });
 }
 
 }  // namespace
