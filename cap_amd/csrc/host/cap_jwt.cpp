@@ -608,7 +608,8 @@ namespace {
 
 template <class Cand>
 void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verified* V, Cand&& cand,
-                const std::vector<size_t>* subset = nullptr, std::shared_lock<std::shared_mutex>* keys_lock = nullptr) {
+                const std::vector<size_t>* subset = nullptr, std::shared_lock<std::shared_mutex>* keys_lock = nullptr,
+                const KeySet::Overlap* overlap = nullptr) {
   const size_t n = subset ? subset->size() : tokens.size();
   auto tok_index = [&](size_t i) { return subset ? (*subset)[i] : i; };
   auto release_keys = [&] {
@@ -688,7 +689,13 @@ void gpu_verify(Engine& eng, const std::vector<std::string_view>& tokens, Verifi
   });
   pt.lap("pack");
   try {
-    eng.verify(arena.get(), arena_len, jobs.get(), total_jobs, verdict.get(), release_keys);
+    eng.verify(arena.get(), arena_len, jobs.get(), total_jobs, verdict.get(), [&] {
+      release_keys();
+      if (overlap) {
+        (*overlap)(*V);
+        pt.lap("overlap");
+      }
+    });
   } catch (const DeviceError& e) {
     release_keys();
     V->dev_err = std::string("capjwt: signature verification unavailable: ") + e.what();
@@ -730,7 +737,8 @@ class StaticKeySet final : public KeySet {
   int DeviceRecoveries() override { return eng_.recoveries(); }
   int DebugFailVerify(int n) override { return eng_.debug_fail_verify(n); }
   // The key list never changes: no lock; concurrent calls pipeline on the device.
-  std::shared_ptr<Verified> verify_raw(const std::vector<std::string_view>& tokens) override {
+  std::shared_ptr<Verified> verify_raw(const std::vector<std::string_view>& tokens,
+                                       const Overlap* overlap = nullptr) override {
     auto V = std::make_shared<Verified>();
     gpu_verify(eng_, tokens, V.get(), [&](const Tok& t, std::vector<uint16_t>& out) {
       // staticKeySet: every key in order (jwt/keyset.go:162-168); a key of
@@ -738,7 +746,7 @@ class StaticKeySet final : public KeySet {
       const int fam = alg_key_kind(t.alg);
       for (size_t k = 0; k < keys_.size(); ++k)
         if (fam_[k] == fam) out.push_back((uint16_t)k);
-    });
+    }, nullptr, nullptr, overlap);
     recover_after(eng_, *V);
     return V;
   }
@@ -758,6 +766,18 @@ class StaticKeySet final : public KeySet {
         r.claims = json::Value();
         r.err = "no known key successfully validated the token signature";
       }
+    }
+  }
+  void finish_pre(const Verified& V, size_t i, Result& r, bool json_ok) override {
+    if (V.failed[i]) {
+      r.claims = json::Value();
+      r.err = V.dev_err;
+    } else if (V.any[i] && json_ok) {
+      r.err.clear();
+      r.ok = true;
+    } else {
+      r.claims = json::Value();
+      r.err = "no known key successfully validated the token signature";
     }
   }
   const char* trace_name() const override { return "static"; }
@@ -800,9 +820,10 @@ class JSONWebKeySet final : public KeySet {
   std::string DeviceStatus() override { return eng_.status(); }
   int DeviceRecoveries() override { return eng_.recoveries(); }
   int DebugFailVerify(int n) override { return eng_.debug_fail_verify(n); }
-  std::shared_ptr<Verified> verify_raw(const std::vector<std::string_view>& tokens) override {
+  std::shared_ptr<Verified> verify_raw(const std::vector<std::string_view>& tokens,
+                                       const Overlap* overlap = nullptr) override {
     auto V = std::make_shared<Verified>();
-    remote_verify(tokens, V.get(), &V->miss_err);
+    remote_verify(tokens, V.get(), &V->miss_err, overlap);
     return V;
   }
   void finish(const Verified& V, size_t i, Result& r) override {
@@ -817,6 +838,20 @@ class JSONWebKeySet final : public KeySet {
       std::string jerr;       // jsonWebKeySet.VerifySignature: json.Unmarshal(payload)
       if (claims_map(t.payload, &r.claims, &jerr)) r.ok = true;
       else { r.claims = json::Value(); r.err = jerr; }
+    }
+  }
+  void finish_pre(const Verified& V, size_t i, Result& r, bool json_ok) override {
+    if (V.failed[i]) {
+      r.claims = json::Value();
+      r.err = V.dev_err;
+    } else if (!V.any[i]) {
+      r.claims = json::Value();
+      r.err = V.miss_err;
+    } else if (json_ok) {
+      r.err.clear();
+      r.ok = true;
+    } else {
+      r.claims = json::Value();                  // r.err: the JSON error
     }
   }
   const char* trace_name() const override { return "jwks"; }
@@ -853,7 +888,8 @@ class JSONWebKeySet final : public KeySet {
   // one it read with the cached keys; a call that needs remote keys while
   // another call's refresh completed since its read takes that refresh's
   // outcome (go-oidc's keysFromRemote shares an in-flight request the same way).
-  void remote_verify(const std::vector<std::string_view>& tokens, Verified* V, std::string* miss_err) {
+  void remote_verify(const std::vector<std::string_view>& tokens, Verified* V, std::string* miss_err,
+                     const Overlap* overlap) {
     auto cand = [&](const Tok& t, std::vector<uint16_t>& out) {
       // remoteKeySet.verify: keyID == "" || key.KeyID == keyID   [R31, R34]
       const int fam = alg_key_kind(t.alg);
@@ -868,8 +904,8 @@ class JSONWebKeySet final : public KeySet {
       seen_refreshes = refreshes_;
       seen_expiry = expiry_ns_;
       seen_have = have_keys_;
-      if (have_keys_) gpu_verify(eng_, tokens, V, cand, nullptr, &lk);
-      else gpu_verify(eng_, tokens, V, [](const Tok&, std::vector<uint16_t>&) {}, nullptr, &lk);
+      if (have_keys_) gpu_verify(eng_, tokens, V, cand, nullptr, &lk, overlap);
+      else gpu_verify(eng_, tokens, V, [](const Tok&, std::vector<uint16_t>&) {}, nullptr, &lk, overlap);
     }
     recover_after(eng_, *V);
     // tokens that parsed but did not verify: refresh once if the cache has
@@ -1367,16 +1403,55 @@ KeySet::KeySet()
       }) {}
 
 Results KeySet::verify_batch(const std::vector<std::string_view>& tokens, const PostFn* post) {
-  std::shared_ptr<Verified> V = verify_raw(tokens);
   const int th = host_threads();
   Results res(tokens.size(), th);
+  // Claims maps are read -- and, with a post step (Validator's claim checks),
+  // checked -- while the device verifies (Overlap): a parsed token's payload
+  // is JSON-decoded before its verdict is known, and the result of a token no
+  // key verifies is replaced afterwards.  pre[i]: 0 not read (finish reads
+  // it), 1 read, 2 JSON error (the message in res[i].err), 3 read and post-
+  // processed as if verified (kept iff it was).
+  std::vector<uint8_t> pre(tokens.size(), 0);
+  const Overlap overlap = [&](const Verified& V) {
+    parallel_for(tokens.size(), th, [&](size_t lo, size_t hi) {
+      auto arena = std::make_unique<json::Arena>();   // this range's claims trees (owned by res)
+      json::ArenaScope scope(arena.get());
+      res.adopt(std::move(arena));
+      std::string jerr;
+      for (size_t i = lo; i < hi; ++i) {
+        const Tok& t = V.toks[i];
+        if (!t.parsed) continue;
+        if (claims_map(t.payload, &res[i].claims, &jerr)) {
+          pre[i] = 1;
+          if (post) {
+            res[i].ok = true;
+            (*post)(i, res[i], t.view());
+            pre[i] = 3;
+          }
+        } else {
+          res[i].claims = json::Value();
+          res[i].err = jerr;
+          pre[i] = 2;
+        }
+      }
+    });
+  };
+  std::shared_ptr<Verified> V = verify_raw(tokens, &overlap);
   PhaseTimer pt(trace_name());
   parallel_for(tokens.size(), th, [&](size_t lo, size_t hi) {
     auto arena = std::make_unique<json::Arena>();   // this range's claims trees (owned by res)
     json::ArenaScope scope(arena.get());
     res.adopt(std::move(arena));
     for (size_t i = lo; i < hi; ++i) {
-      finish(*V, i, res[i]);
+      if (pre[i] == 3) {
+        if (!V->failed[i] && V->any[i]) continue;            // verified: the checked result stands
+        res[i] = Result();
+        finish_pre(*V, i, res[i], true);
+      } else if (pre[i]) {
+        finish_pre(*V, i, res[i], pre[i] == 1);
+      } else {
+        finish(*V, i, res[i]);
+      }
       if (post) (*post)(i, res[i], V->toks[i].view());
     }
   });

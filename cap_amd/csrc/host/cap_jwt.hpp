@@ -328,8 +328,15 @@ class KeySet {
   Result verify_one(std::string_view token, TokenInfo* info);
   // the two halves of a batch: parse + device verification, then token i's
   // (claims, error) -- the key set's own error strings and JSON rules
-  virtual std::shared_ptr<Verified> verify_raw(const std::vector<std::string_view>& tokens) = 0;
+  // overlap (may be null): run while the batch's device call is in flight
+  // (after parse, before the verdicts) -- verify_batch parses the claims then
+  using Overlap = std::function<void(const Verified&)>;
+  virtual std::shared_ptr<Verified> verify_raw(const std::vector<std::string_view>& tokens,
+                                               const Overlap* overlap = nullptr) = 0;
   virtual void finish(const Verified& V, size_t i, Result& r) = 0;
+  // finish() for a parsed token whose claims map was already read into r
+  // (json_ok; else r.err holds the JSON error) while the device verified
+  virtual void finish_pre(const Verified& V, size_t i, Result& r, bool json_ok) = 0;
   virtual const char* trace_name() const = 0;
   // block until background comb-table widening of the last key load is done
   // (keys verify before that, on narrower tables; a measurement hook)
