@@ -2679,13 +2679,9 @@ jg_ctx* jg_create(const int* devices, int ndev) {
       d->lane0.create_fanout(RES_GROUP, RES_NGROUPS);
       d->lane1.create_fanout(RES_GROUP, RES_NGROUPS);
       for (auto& s : d->slots) {
-#ifndef JG_DONE_BLOCKING
-#define JG_DONE_BLOCKING 0
-#endif
-        // JG_DONE_BLOCKING (A/B): the completer sleeps in hipEventSynchronize
-        // until the chunk's interrupt instead of polling
-        HIPCHK(hipEventCreateWithFlags(&s.done, (pipe_trace() ? hipEventDefault : hipEventDisableTiming) |
-                                                    (JG_DONE_BLOCKING ? hipEventBlockingSync : 0)));
+        // (hipEventBlockingSync here left the completer thread's CPU time and
+        // a small batch's round trip unchanged, profiles/r05_s2/session_k.log)
+        HIPCHK(hipEventCreateWithFlags(&s.done, pipe_trace() ? hipEventDefault : hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
         HIPCHK(hipEventCreate(&s.tr_a));
         HIPCHK(hipEventCreate(&s.tr_b));
