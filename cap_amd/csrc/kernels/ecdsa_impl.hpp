@@ -844,6 +844,100 @@ __global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ split point (small launches)
+// k_ec_point with S lanes per token, for launches that fill the GPU poorly
+// (a coalesced single-token batch, a mixed batch's small EC classes): lane s
+// of a token sums the comb windows w = s, s + S, ... of both scalars into its
+// own Jacobian partial (the fast madd chain; a partial with Z == 0 is
+// exceptional, as in k_ec_point), and the partials are combined pairwise
+// across lanes with the exact addition (jadd: doubling and infinity handled).
+// S partial chains of NWIN / S additions run side by side, so a token's
+// latency is ~1/S of k_ec_point's plus log2(S) additions; the work per token
+// grows by those additions and the conversions to normalized form.
+template <class CV, int S>
+__global__ void __launch_bounds__(64) k_ec_point_split(EcArgs a) {
+  using Fp = typename CV::Fp;
+  using Fn = typename CV::Fn;
+  constexpr int L = Fp::L;
+  constexpr int NG = ec_windows(CV::CLS, true), NQ = ec_windows_w(CV::CLS, CV::WQ);
+  constexpr int NWIN = NG > NQ ? NG : NQ;
+  const int lane = threadIdx.x, sub = lane % S;
+  const int64_t p = a.begin + (int64_t)blockIdx.x * (WAVE / S) + lane / S;
+  const int64_t np = a.npad;
+  bool live = p < a.end;
+  JobDev jb{};
+  if (live) jb = a.jobs[p];
+  live = live && job_live(jb);
+  const bool ok_status = live && a.status[p] == ST_OK;
+  if (live && !ok_status && sub == 0) a.verdict_pad[p] = 0;
+  const bool run = ok_status;                     // the S lanes of a token agree
+  // (every lane stays for the cross-lane exchanges below; idle lanes compute nothing)
+  JPt<Fp> P;
+  bool exc = false;
+  P.inf = true;
+  if (run) {
+    const int kidx = job_key(jb);
+    const uint32_t* __restrict__ qtab = key_table(a.keys[kidx]);
+    const uint32_t* __restrict__ gtab = a.gtab;
+    uint32_t X[L], Y[L], Z[L];
+    bool empty = true;
+    for (int w = sub; w < NWIN; w += S) {
+      if (w < NG) add_window<CV, true>(X, Y, Z, empty, gtab, w, (int)a.digs[(int64_t)w * np + p]);
+      if (w < NQ) add_window<CV, false>(X, Y, Z, empty, qtab, w, (int)a.digs[(int64_t)(NG + w) * np + p]);
+    }
+    if (!empty) {
+      mp::canon<Fp>(X); mp::canon<Fp>(Y); mp::canon<Fp>(Z);
+      exc = mp::is_zero_canon<Fp>(Z);            // an exceptional step in this lane's chain
+      mp::copy<Fp>(P.X, X); mp::copy<Fp>(P.Y, Y); mp::copy<Fp>(P.Z, Z);
+      P.inf = false;
+    }
+  }
+#pragma unroll 1
+  for (int off = 1; off < S; off <<= 1) {
+    JPt<Fp> Q;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      Q.X[j] = __shfl_xor(P.X[j], off);
+      Q.Y[j] = __shfl_xor(P.Y[j], off);
+      Q.Z[j] = __shfl_xor(P.Z[j], off);
+    }
+    Q.inf = __shfl_xor((int)P.inf, off) != 0;
+    exc = exc || __shfl_xor((int)exc, off) != 0;
+    if (run && (sub & off) == 0 && !exc) jadd<CV>(P, P, Q);
+  }
+  if (!run || sub != 0) return;
+  if (exc) {                                      // exact recompute (k_ec_exact)
+    const uint32_t idx = atomicAdd(a.exc_count, 1u);
+    a.exc_list[idx] = (int32_t)p;
+    a.status[p] = ST_EXCEPTIONAL;
+    return;
+  }
+  if (P.inf) { a.verdict_pad[p] = 0; return; }    // R = infinity: rejected
+  // x(R) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2)
+  constexpr int CW = ec_sig_words(CV::CLS);
+  uint32_t rw[CW], r[L];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) rw[q] = a.sigw[(int64_t)q * np + p];
+  mp::words_to_limbs<L, CW>(r, rw);
+  uint32_t zz[L], rm[L], tt[L];
+  mp::sqr<Fp>(zz, P.Z);
+  mp::to_mont<Fp>(rm, r);
+  mp::mul<Fp>(tt, rm, zz);
+  bool ok = mp::eq_mod<Fp>(P.X, tt);
+  if (!ok) {
+    uint32_t rn[L], pl[L];
+    mp::add<Fp>(rn, r, Fn::M);
+    mp::norm<Fp>(rn);
+    mp::set_const<Fp>(pl, Fp::M);
+    if (lt_limbs<L>(rn, pl)) {
+      mp::to_mont<Fp>(rm, rn);
+      mp::mul<Fp>(tt, rm, zz);
+      ok = mp::eq_mod<Fp>(P.X, tt);
+    }
+  }
+  a.verdict_pad[p] = ok;
+}
+
 // ------------------------------------------------------------------ staging
 // thread per key: validate (coordinates < p, on the curve) and convert to Montgomery
 template <class CV>
@@ -966,6 +1060,22 @@ __global__ void k_ec_table_g(uint32_t* tab) {
   table_entry<CV, W>(tab + (int64_t)e * STRIDE, tab + (int64_t)(e / NE) * NE * STRIDE, e % NE + 1);
 }
 
+// Launches of up to EC_SPLIT_MAX_TOKENS padded tokens run k_ec_point_split
+// with EC_SPLIT lanes per token.  Measured (profiles/r05_s2/split_ab/): a lone
+// ES256 batch of 1 ... 4096 tokens 238 -> 183 us (4 lanes; 2 lanes: 198 us),
+// 16 coalesced single-token callers 45 k -> 60 k calls/s; but the configs[4]
+// classes (62.5 k tokens per launch) ran slower split (P-256 point 0.31 ->
+// 0.26 of the MAD roofline at 4 lanes, P-384 0.40 -> 0.31; 2 lanes: P-256 0.34,
+// P-384 0.38, the batch 82.1 -> 81.2 M/s), so only small launches split.
+#ifndef JG_EC_SPLIT
+#define JG_EC_SPLIT 4
+#endif
+#ifndef JG_EC_SPLIT_MAX
+#define JG_EC_SPLIT_MAX 16384
+#endif
+constexpr int EC_SPLIT = JG_EC_SPLIT;                    // lanes per token of k_ec_point_split
+constexpr int64_t EC_SPLIT_MAX_TOKENS = JG_EC_SPLIT_MAX;  // launches up to this many padded tokens use it
+
 template <class CV>
 void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
@@ -985,7 +1095,14 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   constexpr int TPB = WAVE * EC_SCALAR_WPB;
   hipLaunchKernelGGL(k_ec_scalar_batch<CV>, dim3((unsigned)((S + TPB - 1) / TPB)), dim3(TPB), 0, s, a, B);
   mk("scalar");
-  hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
+  // a launch of fewer waves than ~2 per SIMD runs its tokens S lanes each
+  // (k_ec_point_split): one wave per SIMD leaves the madd chain's latency bare
+  if (n <= EC_SPLIT_MAX_TOKENS) {
+    hipLaunchKernelGGL((k_ec_point_split<CV, EC_SPLIT>), dim3((unsigned)((n * EC_SPLIT + WAVE - 1) / WAVE)), b, 0, s,
+                       a);
+  } else {
+    hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
+  }
   mk("point");
   if (a.part == EC_FAST) return;
   hipLaunchKernelGGL(k_ec_exact<CV>, dim3(64), b, 0, s, a);

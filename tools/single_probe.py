@@ -26,6 +26,19 @@ def main():
     e = jwt.Expected(Issuer="https://example.com/", Audiences=["www.example.com"], SigningAlgorithms=["ES256"],
                      Now=lambda: 1611699344 + 60)
     blob = b"\n".join(pool)
+    pre = os.environ.get("PROBE_PRE")        # "e2e": a 1M-token ValidateBatch on another key set first (the bench's order)
+    keep = None
+    if pre == "e2e":
+        ks2, _ = jwt.NewJSONWebKeySet(None, "https://bench.example/jwks", "",
+                                      lambda url, ca: {"status": 200, "body": jwks, "max_age": 3600})
+        v2, _ = jwt.NewValidator(ks2)
+        big = b"\n".join((pool * 16)[:1 << 20])
+        v2.ValidateBlob(big[:1 << 20], e)
+        ks2.WaitTables()
+        for _ in range(2):
+            v2.ValidateBlob(big, e)
+        keep = (ks2, v2) if os.environ.get("PROBE_PRE_KEEP") else None
+        del big, v2, ks2
     v.ValidateBlob(blob, e)
     ks.WaitTables()
     res = {"cpu": cpu, "runs": []}
