@@ -10,6 +10,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -435,7 +437,7 @@ PYBIND11_MODULE(_capjwt_host, m) {
         return py::bytes(ok);
       })
       .def("_concurrent_validate", [](PyValidator& s, py::bytes blob, const Expected& e, int callers,
-                                      int64_t total) {
+                                      int64_t total, int pin_cpus) {
         // Measurement helper (bench.py `single`): `callers` host threads, each
         // calling Validator::Validate once per token -- the goroutine-per-
         // request pattern of an unchanged cap caller -- over `total` tokens
@@ -454,9 +456,23 @@ PYBIND11_MODULE(_capjwt_host, m) {
           if (toks.empty()) throw std::runtime_error("empty token pool");
           std::atomic<int64_t> next{0};
           std::vector<std::thread> th;
+          // pin_cpus > 0: every caller thread runs on the first pin_cpus CPUs the
+          // process may use (a Go service's goroutines on GOMAXPROCS threads)
+          cpu_set_t pin;
+          CPU_ZERO(&pin);
+          if (pin_cpus > 0) {
+            cpu_set_t all;
+            CPU_ZERO(&all);
+            if (sched_getaffinity(0, sizeof all, &all) == 0) {
+              int k = 0;
+              for (int c = 0; c < CPU_SETSIZE && k < pin_cpus; ++c)
+                if (CPU_ISSET(c, &all)) { CPU_SET(c, &pin); ++k; }
+            }
+          }
           const auto t0 = std::chrono::steady_clock::now();
           for (int c = 0; c < callers; ++c)
             th.emplace_back([&, c] {
+              if (pin_cpus > 0 && CPU_COUNT(&pin) > 0) (void)sched_setaffinity(0, sizeof pin, &pin);
               lat[c].reserve((size_t)(total / callers + 16));
               while (true) {
                 const int64_t i = next.fetch_add(1);
@@ -487,7 +503,7 @@ PYBIND11_MODULE(_capjwt_host, m) {
         d["p999_us"] = pct(0.999);
         d["max_us"] = all.empty() ? 0.0 : (double)all.back() / 1e3;
         return d;
-      }, py::arg("blob"), py::arg("expected"), py::arg("callers"), py::arg("total"));
+      }, py::arg("blob"), py::arg("expected"), py::arg("callers"), py::arg("total"), py::arg("pin_cpus") = 0);
 
   // ---- go-oidc oidc.KeySet adapter (NewRemoteKeySet): payload bytes out
   struct PyRemoteKeySet {
