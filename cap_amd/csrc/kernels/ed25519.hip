@@ -64,6 +64,24 @@ __device__ __forceinline__ void add_niels(FPt& P, const uint32_t* ypx, const uin
   fe::mul(P.X, F, E); fe::mul(P.T, H, E); fe::mul(P.Y, H, G); fe::mul(P.Z, F, G);
 }
 
+// extended + extended in radix 2^25.5 (complete, a = -1; add-2008-hwcd-3 with
+// k = 2d): 9 products, the operand shapes of add_niels (tools/fe25519_bounds.py)
+__device__ __forceinline__ void add_ext(FPt& R, const FPt& P, const FPt& Q) {
+  // 2d mod p, canonical radix-2^25.5 limbs
+  constexpr uint32_t D2[fe::L] = {0x2b2f159u, 0x1a6e509u, 0x22add7au, 0x0d4141du, 0x0038052u,
+                                  0x0f3d130u, 0x3407977u, 0x19ce331u, 0x1c56dffu, 0x0901b67u};
+  uint32_t t[fe::L], u[fe::L], A[fe::L], B[fe::L], C[fe::L], E[fe::L], F[fe::L], G[fe::L], H[fe::L];
+  fe::mul(t, Q.T, D2);                                    // 2d T2
+  fe::mul(C, t, P.T);
+  fe::mul(t, P.Z, Q.Z);
+  fe::add(t, t, t);                                       // D
+  fe::sub(F, t, C); fe::add(G, t, C);
+  fe::sub(t, P.Y, P.X); fe::sub(u, Q.Y, Q.X); fe::mul(A, u, t);
+  fe::add(t, P.Y, P.X); fe::add(u, Q.Y, Q.X); fe::mul(B, u, t);
+  fe::sub(E, B, A); fe::add(H, B, A);
+  fe::mul(R.X, F, E); fe::mul(R.T, H, E); fe::mul(R.Y, H, G); fe::mul(R.Z, F, G);
+}
+
 // radix-2^25.5 limbs (limbs < 2^31) -> ED25519P Montgomery form
 __device__ void fe_to_mont(uint32_t* m, const uint32_t* f) {
   uint32_t c[fe::L], w[8], pl[L];
@@ -203,6 +221,106 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
     a.xyz[(int64_t)(2 * L + j) * np + p] = P.Z[j];
   }
   if (!ok) a.status[p] = ST_REJECT;
+}
+
+// k_ed_point with two lanes per token, for launches that fill the GPU poorly
+// (a coalesced single-token batch, a mixed batch's Ed25519 class): lane 0 sums
+// the [S]B windows, lane 1 the [k](-A) windows, each into its own extended
+// point, and lane 0 adds the two with the complete law (add_ext).  Each lane
+// runs the additions of one scalar: a token's latency about halves for one
+// extra addition.  Lane 0 checks S, lane 1 derives k = H mod L.
+template <int WA>
+__global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point_split(EdArgs a) {
+  const int lane = (int)threadIdx.x, sub = lane & 1;
+  const int64_t p = a.begin + (int64_t)blockIdx.x * (WAVE / 2) + (lane >> 1);
+  const int64_t np = a.npad;
+  bool live = p < a.end;
+  JobDev jb{};
+  if (live) jb = a.jobs[p];
+  live = live && job_live(jb);
+  // (every lane stays for the exchange below; dead tokens compute on key 0)
+  const int kidx = live ? job_key(jb) : 0;
+  const DevKey& K = a.keys[kidx];
+  bool ok = live && a.status[p] == ST_OK && K.valid && a.siglen[p] == 64;
+  constexpr int NB = ed_windows(true), NA = ed_windows_w(WA), NW = NB > NA ? NB : NA;
+  __shared__ int dg[NW * WAVE];
+  uint32_t sc[L];                               // lane 0: S, lane 1: k
+  if (sub == 0) {
+    // S: canonical, and sig[63] & 0xE0 == 0
+    uint32_t sw[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sw[q] = live ? a.sigw[(int64_t)(8 + q) * np + p] : 0u;
+    ok = ok && (sw[7] & 0xE0000000u) == 0;
+    mp::words_to_limbs<L, 8>(sc, sw);
+    uint32_t lord[L];
+    mp::set_const<Fl>(lord, Fl::M);
+    ok = ok && lt_limbs(sc, lord);
+    recode<ed_comb_w(true), NB>(dg + lane, sc, WAVE);
+    for (int w = NB; w < NW; ++w) dg[w * WAVE + lane] = 0;
+  } else {
+    // k = H mod L  (H little-endian, 512 bits)
+    uint32_t hw[16], hl[2 * L];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t x = live ? a.dig[(int64_t)q * np + p] : 0u;
+      hw[q] = (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+    }
+    mp::words_to_limbs<2 * L, 16>(hl, hw);
+    uint64_t tt[2 * L];
+#pragma unroll
+    for (int j = 0; j < 2 * L; ++j) tt[j] = hl[j];
+    uint32_t kr[L], rr[L];
+    mp::mont_reduce<Fl>(kr, tt);
+    mp::set_const<Fl>(rr, Fl::RR);
+    mp::mul<Fl>(sc, kr, rr);
+    mp::csub<Fl>(sc);
+    recode<WA, NA>(dg + lane, sc, WAVE);
+    for (int w = NA; w < NW; ++w) dg[w * WAVE + lane] = 0;
+  }
+  FPt P;                                        // the neutral element (0, 1, 1, 0)
+  fe::set_small(P.X, 0u); fe::set_small(P.Y, 1u); fe::set_small(P.Z, 1u); fe::set_small(P.T, 0u);
+  if (live) {
+    const uint32_t* __restrict__ tab = sub ? key_table(K) : a.btab;
+    const int ne = sub ? (1 << (WA - 1)) : ed_entries(true);
+#pragma unroll 1
+    for (int w = 0; w < NW; ++w) {
+      const int d = dg[w * WAVE + lane];        // this lane's own digit row: no barrier needed
+      if (d == 0) continue;
+      const int ad = d < 0 ? -d : d;
+      const uint32_t* ent = tab + ((int64_t)w * ne + (ad - 1)) * ED_STRIDE;
+      uint32_t ypx[fe::L], ymx[fe::L], t2d[fe::L], a1[fe::L], a2[fe::L], nt[fe::L];
+#pragma unroll
+      for (int j = 0; j < fe::L; ++j) { ypx[j] = ent[j]; ymx[j] = ent[fe::L + j]; t2d[j] = ent[2 * fe::L + j]; }
+      const bool neg = d < 0;
+      fe::neg(nt, t2d);
+#pragma unroll
+      for (int j = 0; j < fe::L; ++j) {
+        a1[j] = neg ? ymx[j] : ypx[j];
+        a2[j] = neg ? ypx[j] : ymx[j];
+        t2d[j] = neg ? nt[j] : t2d[j];
+      }
+      add_niels(P, a1, a2, t2d);
+    }
+  }
+  FPt Q;
+#pragma unroll
+  for (int j = 0; j < fe::L; ++j) {
+    Q.X[j] = __shfl_xor(P.X[j], 1);
+    Q.Y[j] = __shfl_xor(P.Y[j], 1);
+    Q.Z[j] = __shfl_xor(P.Z[j], 1);
+    Q.T[j] = __shfl_xor(P.T[j], 1);
+  }
+  const bool ok1 = __shfl_xor((int)ok, 1) != 0;
+  if (!live || sub != 0) return;
+  FPt R;
+  add_ext(R, P, Q);
+#pragma unroll
+  for (int j = 0; j < fe::L; ++j) {                // radix-2^25.5 limbs (k_ed_finish converts)
+    a.xyz[(int64_t)j * np + p] = R.X[j];
+    a.xyz[(int64_t)(L + j) * np + p] = R.Y[j];
+    a.xyz[(int64_t)(2 * L + j) * np + p] = R.Z[j];
+  }
+  if (!(ok && ok1)) a.status[p] = ST_REJECT;
 }
 
 // Batched finish (Montgomery's trick, as k_ec_scalar_batch): thread i owns the
@@ -442,16 +560,33 @@ __global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_
 
 }  // namespace
 
+#ifndef JG_ED_SPLIT_MAX
+#define JG_ED_SPLIT_MAX 131072
+#endif
+constexpr int64_t ED_SPLIT_MAX_TOKENS = JG_ED_SPLIT_MAX;  // launches up to this many padded tokens: k_ed_point_split
+
 void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   if (waves <= 0) return;
   dim3 g((unsigned)waves), b(WAVE);
+  if (a.end - a.begin <= ED_SPLIT_MAX_TOKENS) {
+    // a launch of fewer waves than ~2 per SIMD: two lanes per token
+    dim3 g2((unsigned)(2 * waves));
+    switch (a.wa) {
+      case 24: hipLaunchKernelGGL(k_ed_point_split<24>, g2, b, 0, s, a); break;
+      case 22: hipLaunchKernelGGL(k_ed_point_split<22>, g2, b, 0, s, a); break;
+      case 20: hipLaunchKernelGGL(k_ed_point_split<20>, g2, b, 0, s, a); break;
+      case 18: hipLaunchKernelGGL(k_ed_point_split<18>, g2, b, 0, s, a); break;
+      default: hipLaunchKernelGGL(k_ed_point_split<16>, g2, b, 0, s, a); break;
+    }
+  } else {
   switch (a.wa) {
     case 24: hipLaunchKernelGGL(k_ed_point<24>, g, b, 0, s, a); break;
     case 22: hipLaunchKernelGGL(k_ed_point<22>, g, b, 0, s, a); break;
     case 20: hipLaunchKernelGGL(k_ed_point<20>, g, b, 0, s, a); break;
     case 18: hipLaunchKernelGGL(k_ed_point<18>, g, b, 0, s, a); break;
     default: hipLaunchKernelGGL(k_ed_point<16>, g, b, 0, s, a); break;
+  }
   }
   mk("point");
   // tokens per thread for the batched inversion: keep >= ~8 waves per CU

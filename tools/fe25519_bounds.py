@@ -88,6 +88,27 @@ def niels_addition_bounds():
     return norm
 
 
+def extended_addition_bounds():
+    """ed25519.hip add_ext (k_ed_point_split's lane combine): extended +
+    extended on the normalized outputs of the Niels additions, k = 2d canonical"""
+    norm = NORM if NORM is not None else niels_addition_bounds()
+    canon = list(MASK)
+    P_ = Q_ = norm
+    t = mx_mul(Q_, canon)                    # 2d T2 (f = T2, g = the constant)
+    C = mx_mul(t, P_)
+    D = mx_add(mx_mul(P_, Q_), mx_mul(P_, Q_))
+    F = mx_sub(D, C)
+    G = mx_add(D, C)
+    A = mx_mul(mx_sub(Q_, Q_), mx_sub(P_, P_))   # (Y2 - X2)(Y1 - X1)
+    B = mx_mul(mx_add(Q_, Q_), mx_add(P_, P_))   # (Y2 + X2)(Y1 + X1)
+    E = mx_sub(B, A)
+    H = mx_add(B, A)
+    outs = [mx_mul(F, E), mx_mul(H, G), mx_mul(H, E), mx_mul(F, G)]
+    new = [max(v) for v in zip(*outs)]
+    assert all(a <= b for a, b in zip(new, norm)), "add_ext outputs above the normalized maxima"
+    return new
+
+
 # ---------------------------------------------------------------- bit-exact model
 def to_limbs(v):
     return [(v >> OFF[i]) & MASK[i] for i in range(L)]
@@ -145,7 +166,8 @@ def model_canon(r):
 def main():
     norm = niels_addition_bounds()
     print("normalized limb maxima:", [hex(x) for x in norm])
-    print("ok: every product column of the Niels addition fits 64 bits, every limb and 19 g_j 32 bits")
+    extended_addition_bounds()
+    print("ok: every product column of the Niels addition and of add_ext fits 64 bits, every limb and 19 g_j 32 bits")
 
 
 if __name__ == "__main__":
