@@ -1073,6 +1073,14 @@ __global__ void k_ec_table_g(uint32_t* tab) {
 #ifndef JG_EC_SPLIT_MAX
 #define JG_EC_SPLIT_MAX 16384
 #endif
+// P-256 launches of 16 k ... 128 k tokens (a mixed batch's P-256 class) run
+// two lanes per token: point 0.30 -> 0.34-0.35 of the MAD roofline at
+// configs[4], the batch within the box noise (82.1 vs 81.4 / 84.2 M/s,
+// profiles/r05_s2/q_ab/); P-384 / P-521 lost there (split_ab) and stay whole.
+#ifndef JG_EC_SPLIT2_P256
+#define JG_EC_SPLIT2_P256 131072
+#endif
+constexpr int64_t EC_SPLIT2_MAX_P256 = JG_EC_SPLIT2_P256;
 constexpr int EC_SPLIT = JG_EC_SPLIT;                    // lanes per token of k_ec_point_split
 constexpr int64_t EC_SPLIT_MAX_TOKENS = JG_EC_SPLIT_MAX;  // launches up to this many padded tokens use it
 
@@ -1097,12 +1105,19 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   mk("scalar");
   // a launch of fewer waves than ~2 per SIMD runs its tokens S lanes each
   // (k_ec_point_split): one wave per SIMD leaves the madd chain's latency bare
+  bool launched = false;
   if (n <= EC_SPLIT_MAX_TOKENS) {
     hipLaunchKernelGGL((k_ec_point_split<CV, EC_SPLIT>), dim3((unsigned)((n * EC_SPLIT + WAVE - 1) / WAVE)), b, 0, s,
                        a);
-  } else {
-    hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
+    launched = true;
   }
+  if constexpr (CV::CLS == jgk::CLS_P256 && EC_SPLIT2_MAX_P256 > 0) {
+    if (!launched && n <= EC_SPLIT2_MAX_P256) {
+      hipLaunchKernelGGL((k_ec_point_split<CV, 2>), dim3((unsigned)((n * 2 + WAVE - 1) / WAVE)), b, 0, s, a);
+      launched = true;
+    }
+  }
+  if (!launched) hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
   mk("point");
   if (a.part == EC_FAST) return;
   hipLaunchKernelGGL(k_ec_exact<CV>, dim3(64), b, 0, s, a);

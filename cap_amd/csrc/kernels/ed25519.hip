@@ -560,8 +560,11 @@ __global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_
 
 }  // namespace
 
+// Measured (profiles/r05_s2/q_ab/, ed_split_ab/): a lone EdDSA batch of 1 ...
+// 4096 tokens 210-244 -> 182-218 us; configs[4]'s 38 k-token Ed25519 launch
+// unchanged (0.081 ms either way), so only small launches split.
 #ifndef JG_ED_SPLIT_MAX
-#define JG_ED_SPLIT_MAX 131072
+#define JG_ED_SPLIT_MAX 16384
 #endif
 constexpr int64_t ED_SPLIT_MAX_TOKENS = JG_ED_SPLIT_MAX;  // launches up to this many padded tokens: k_ed_point_split
 

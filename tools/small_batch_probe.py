@@ -2,7 +2,7 @@
 device round trip): ES256 tokens of the 4 bench kids, batch sizes 1 ... 4096,
 pinned host arena, p50 / p90 of many calls per size; optionally several
 threads submitting concurrently (pipelining on the device worker).
-usage: python tools/small_batch_probe.py [out.json] [threads]"""
+usage: python tools/small_batch_probe.py [out.json] [threads] [ES256|EdDSA]"""
 import ctypes
 import json
 import os
@@ -22,12 +22,13 @@ def main():
     nthr = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     from cap_amd import _lib
     L = _lib.lib()
-    kids = ["p256-a", "p256-b", "p256-c", "p256-d"]
+    alg = sys.argv[3] if len(sys.argv) > 3 else "ES256"
+    kids = ["ed-a"] if alg == "EdDSA" else ["p256-a", "p256-b", "p256-c", "p256-d"]
     ctx = _lib.Context()
     ctx.load_keys(bench.abi_keys(kids))
     ctx.wait_tables()
-    pool = bench.gen_tokens("ES256", 8192, bench.golden_keypaths(kids), 8, "sbp")
-    arena, toks = bench.pack(pool, [bench.ALG_IDS["ES256"]] * len(pool), np.arange(len(pool)) % 4, len(pool))
+    pool = bench.gen_tokens(alg, 8192, bench.golden_keypaths(kids), 8, "sbp")
+    arena, toks = bench.pack(pool, [bench.ALG_IDS[alg]] * len(pool), np.arange(len(pool)) % len(kids), len(pool))
     pa = _lib.PinnedBuffer(len(arena))
     ctypes.memmove(pa.ptr, arena, len(arena))
     res = {"threads": nthr, "sizes": {}}
