@@ -74,6 +74,36 @@ def test_ecdsa_comb_tier(crv, wq):
         ctx.close()
 
 
+@pytest.mark.parametrize("crv,wq", [t for t in _ec_tiers() if t[0] == "P-256"])
+def test_ecdsa_comb_tier_mid_launch(crv, wq):
+    """The same tokens tiled to ~40 k jobs, so the class launch is past the
+    4-lane split's 16 k and P-256 runs the 2-lane k_ec_point_split
+    (ecdsa_impl.hpp launch_chain); every verdict equals the fixture's."""
+    import bench
+    from cap_amd import _lib
+    s = next(x for x in fixtures()["ec"] if x["crv"] == crv and x["wq"] == wq)
+    keys = s["keys"]
+    reps = 40000 // len(s["tokens"]) + 1
+    toks = s["tokens"] * reps
+    assert len(toks) > 16384 * 2
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    ctx = _lib.Context()
+    try:
+        budget = len(keys) * bench.table_bytes(TAB[crv], wq)
+        ctx.set_table_budget(budget)
+        ctx.load_keys([H.abi_key(k) for k in keys])
+        assert ctx.table_widths() == [wq] * len(keys)
+        arena, slots = H.jobs_from_tokens(toks, kid_index)
+        out = ctx.verify(arena)
+        b = ctx.stage(arena)
+        res = b.run(want_verdicts=True)
+        b.free()
+        bad = [t["name"] for t, sl in zip(toks, slots) if out[sl] != t["verdict"] or res[sl] != t["verdict"]]
+        assert not bad, bad[:10]
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("wa", [24, 22, 20, 18, 16])
 def test_ed25519_comb_tier(wa):
     import bench
