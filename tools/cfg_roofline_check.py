@@ -29,12 +29,16 @@ import os
 import sys
 
 # bench.py roofline mark -> kernel symbol prefixes (one mark may launch
-# several instantiations, e.g. one per comb width)
+# several instantiations, e.g. one per comb width, or the split kernels that
+# launch_chain / launch_ed pick for launches of at most 16384 / 131072 tokens)
 MARKS = {
-    "p256_point": ["void (anonymous namespace)::k_ec_point<(anonymous namespace)::CurveP256W<"],
-    "p384_point": ["void (anonymous namespace)::k_ec_point<(anonymous namespace)::CurveP384W<"],
-    "p521_point": ["void (anonymous namespace)::k_ec_point<(anonymous namespace)::CurveP521W<"],
-    "ed25519_point": ["void (anonymous namespace)::k_ed_point<"],
+    "p256_point": ["void (anonymous namespace)::k_ec_point<(anonymous namespace)::CurveP256W<",
+                   "void (anonymous namespace)::k_ec_point_split<(anonymous namespace)::CurveP256W<"],
+    "p384_point": ["void (anonymous namespace)::k_ec_point<(anonymous namespace)::CurveP384W<",
+                   "void (anonymous namespace)::k_ec_point_split<(anonymous namespace)::CurveP384W<"],
+    "p521_point": ["void (anonymous namespace)::k_ec_point<(anonymous namespace)::CurveP521W<",
+                   "void (anonymous namespace)::k_ec_point_split<(anonymous namespace)::CurveP521W<"],
+    "ed25519_point": ["void (anonymous namespace)::k_ed_point<", "void (anonymous namespace)::k_ed_point_split<"],
     "ed25519_prep": ["(anonymous namespace)::k_prep_ed("],
     "ed25519_finish": ["(anonymous namespace)::k_ed_finish("],
     "p384_prep": ["void (anonymous namespace)::k_prep<4, "],
