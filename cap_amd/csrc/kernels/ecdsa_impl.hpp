@@ -248,7 +248,8 @@ __device__ __forceinline__ void store_digit_rows(const EcArgs& a, int64_t p, con
 #define JG_EC_SCALAR_PF 0
 #endif
 constexpr int EC_SCALAR_WPB = JG_EC_SCALAR_WPB;
-template <class CV>
+// WPB: waves per block sharing one inversion (small launches: 1, launch_chain)
+template <class CV, int WPB = EC_SCALAR_WPB>
 // JG_EC_SCALAR_ATTR: per translation unit.  ecdsa_p521.hip caps the kernel at
 // two waves per SIMD: left alone the compiler gives the P-521 instantiation
 // 295 VGPRs (+18 spilled), one wave per SIMD; capped it needs 198 and spills
@@ -258,7 +259,7 @@ template <class CV>
 #ifndef JG_EC_SCALAR_ATTR
 #define JG_EC_SCALAR_ATTR
 #endif
-__global__ void __launch_bounds__(64 * EC_SCALAR_WPB) JG_EC_SCALAR_ATTR k_ec_scalar_batch(EcArgs a, int B) {
+__global__ void __launch_bounds__(64 * WPB) JG_EC_SCALAR_ATTR k_ec_scalar_batch(EcArgs a, int B) {
   using Fn = typename CV::Fn;
   constexpr int L = Fn::L;
   const int64_t np = a.npad;
@@ -269,7 +270,7 @@ __global__ void __launch_bounds__(64 * EC_SCALAR_WPB) JG_EC_SCALAR_ATTR k_ec_sca
   // to it after this kernel; a separate memset would be one more dependent
   // launch on the lane, waiting for a free wave slot behind the modexps)
   if (a.exc_reset && i == 0) *a.exc_count = 0u;
-  if (EC_SCALAR_WPB == 1 && i >= S) return;        // (blocks of several waves keep every thread for the barriers)
+  if (WPB == 1 && i >= S) return;                  // (blocks of several waves keep every thread for the barriers)
   uint32_t acc[L];
   mp::set_const<Fn>(acc, Fn::ONE);
   int nb = 0;
@@ -303,7 +304,7 @@ __global__ void __launch_bounds__(64 * EC_SCALAR_WPB) JG_EC_SCALAR_ATTR k_ec_sca
     }
   }
   uint32_t inv[L];
-  mp::block_inv<Fn, EC_SCALAR_WPB>(inv, acc);
+  mp::block_inv<Fn, WPB>(inv, acc);
   if (nb > 0) {
     ScalarRaw2<CV> cur, nxt;
     int64_t p = a.begin + i + (int64_t)(nb - 1) * S;
@@ -342,7 +343,7 @@ __global__ void __launch_bounds__(64 * EC_SCALAR_WPB) JG_EC_SCALAR_ATTR k_ec_sca
     ++nb;
   }
   uint32_t inv[L];
-  mp::block_inv<Fn, EC_SCALAR_WPB>(inv, acc);
+  mp::block_inv<Fn, WPB>(inv, acc);
   for (int j = nb - 1; j >= 0; --j) {
     const int64_t p = a.begin + i + (int64_t)j * S;
     uint32_t cprev[L], sm[L], w[L];
@@ -1070,6 +1071,10 @@ __global__ void k_ec_table_g(uint32_t* tab) {
 #ifndef JG_EC_SPLIT
 #define JG_EC_SPLIT 4
 #endif
+#ifndef JG_EC_SCALAR_SOLO_MAX
+#define JG_EC_SCALAR_SOLO_MAX 16384
+#endif
+constexpr int64_t EC_SCALAR_SOLO_MAX = JG_EC_SCALAR_SOLO_MAX;   // launches up to this size: k_ec_scalar_batch<CV, 1>
 #ifndef JG_EC_SPLIT_MAX
 #define JG_EC_SPLIT_MAX 16384
 #endif
@@ -1100,8 +1105,14 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   constexpr int wpc = 8;
   int B = (int)std::min<int64_t>(16, std::max<int64_t>(1, n / (256 * wpc * WAVE)));
   const int64_t S = (n + B - 1) / B;
-  constexpr int TPB = WAVE * EC_SCALAR_WPB;
-  hipLaunchKernelGGL(k_ec_scalar_batch<CV>, dim3((unsigned)((S + TPB - 1) / TPB)), dim3(TPB), 0, s, a, B);
+  if (n <= EC_SCALAR_SOLO_MAX) {
+    // a small launch: one inversion per wave, no block barrier (the shared
+    // inversion saves inversions only when the chip is full)
+    hipLaunchKernelGGL((k_ec_scalar_batch<CV, 1>), dim3((unsigned)((S + WAVE - 1) / WAVE)), dim3(WAVE), 0, s, a, B);
+  } else {
+    constexpr int TPB = WAVE * EC_SCALAR_WPB;
+    hipLaunchKernelGGL(k_ec_scalar_batch<CV>, dim3((unsigned)((S + TPB - 1) / TPB)), dim3(TPB), 0, s, a, B);
+  }
   mk("scalar");
   // a launch of fewer waves than ~2 per SIMD runs its tokens S lanes each
   // (k_ec_point_split): one wave per SIMD leaves the madd chain's latency bare
