@@ -151,14 +151,30 @@ def test_timed_and_streamed_runs_agree(ctx):
     b.free()
 
 
+def _fresh_p256_key():
+    """A P-256 public key no earlier test loaded (comb tables are cached per
+    device by key content, across contexts): Q = k G for a random k."""
+    import secrets
+    from tests.test_gpu_mp import ec_mul
+    c = {"p": 2**256 - 2**224 + 2**192 + 2**96 - 1}
+    G = (0x6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296,
+         0x4FE342E2FE1A7F9B8EE7EB4A7C0F9E162BCE33576B315ECECBB6406837BF51F5)
+    Q = ec_mul(c, 1 + secrets.randbelow(2**255), G)
+    return {"kty": "EC", "crv": "P-256", "kid": "fresh-p256", "x": f"{Q[0]:064x}", "y": f"{Q[1]:064x}"}
+
+
 def test_key_reload_reuses_tables():
     """jg_keys_load keeps the comb tables of keys it already had (copied by
     content into the new key blob) and builds only new ones: reloading the
     golden key set in reverse order, then a subset, verifies every golden token
-    exactly as a fresh load does."""
+    exactly as a fresh load does.  The first load holds a key no earlier test
+    loaded, so it builds at least that key's table; the last reload builds
+    nothing and must be faster (the golden keys' own tables may already be in
+    the per-device cache from earlier tests of the session)."""
     import time
     from cap_amd import _lib
     keys, toks = H.golden()
+    keys = keys + [_fresh_p256_key()]
     c = _lib.Context()
     t0 = time.perf_counter()
     c.load_keys([H.abi_key(k) for k in keys])
