@@ -223,16 +223,20 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
   if (!ok) a.status[p] = ST_REJECT;
 }
 
-// k_ed_point with two lanes per token, for launches that fill the GPU poorly
-// (a coalesced single-token batch, a mixed batch's Ed25519 class): lane 0 sums
-// the [S]B windows, lane 1 the [k](-A) windows, each into its own extended
-// point, and lane 0 adds the two with the complete law (add_ext).  Each lane
-// runs the additions of one scalar: a token's latency about halves for one
-// extra addition.  Lane 0 checks S, lane 1 derives k = H mod L.
-template <int WA>
+// k_ed_point with S lanes per token (S = 2 or 4), for launches that fill the
+// GPU poorly (a coalesced single-token batch, a mixed batch's Ed25519 class):
+// the first S/2 lanes sum the [S]B windows, the others the [k](-A) windows,
+// each lane every (S/2)-th window into its own extended point; the partials
+// are added across lanes with the complete law (add_ext), and lane 0 writes
+// the sum.  A token's latency falls to about 2/S of k_ed_point's for
+// log2(S) extra additions on its path (S - 1 in all).  The B-side lanes check
+// S, the A-side lanes derive k = H mod L.
+template <int WA, int S>
 __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point_split(EdArgs a) {
-  const int lane = (int)threadIdx.x, sub = lane & 1;
-  const int64_t p = a.begin + (int64_t)blockIdx.x * (WAVE / 2) + (lane >> 1);
+  static_assert(S == 2 || S == 4, "two or four lanes per token");
+  constexpr int H = S / 2;                        // lanes per scalar
+  const int lane = (int)threadIdx.x, sub = lane % S, side = sub / H, par = sub % H;
+  const int64_t p = a.begin + (int64_t)blockIdx.x * (WAVE / S) + lane / S;
   const int64_t np = a.npad;
   bool live = p < a.end;
   JobDev jb{};
@@ -244,8 +248,8 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point_split(EdArgs a
   bool ok = live && a.status[p] == ST_OK && K.valid && a.siglen[p] == 64;
   constexpr int NB = ed_windows(true), NA = ed_windows_w(WA), NW = NB > NA ? NB : NA;
   __shared__ int dg[NW * WAVE];
-  uint32_t sc[L];                               // lane 0: S, lane 1: k
-  if (sub == 0) {
+  uint32_t sc[L];                               // B side: S, A side: k
+  if (side == 0) {
     // S: canonical, and sig[63] & 0xE0 == 0
     uint32_t sw[8];
 #pragma unroll
@@ -280,10 +284,10 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point_split(EdArgs a
   FPt P;                                        // the neutral element (0, 1, 1, 0)
   fe::set_small(P.X, 0u); fe::set_small(P.Y, 1u); fe::set_small(P.Z, 1u); fe::set_small(P.T, 0u);
   if (live) {
-    const uint32_t* __restrict__ tab = sub ? key_table(K) : a.btab;
-    const int ne = sub ? (1 << (WA - 1)) : ed_entries(true);
+    const uint32_t* __restrict__ tab = side ? key_table(K) : a.btab;
+    const int ne = side ? (1 << (WA - 1)) : ed_entries(true);
 #pragma unroll 1
-    for (int w = 0; w < NW; ++w) {
+    for (int w = par; w < NW; w += H) {
       const int d = dg[w * WAVE + lane];        // this lane's own digit row: no barrier needed
       if (d == 0) continue;
       const int ad = d < 0 ? -d : d;
@@ -302,25 +306,35 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point_split(EdArgs a
       add_niels(P, a1, a2, t2d);
     }
   }
-  FPt Q;
+  // the partner lane's partial (and verdict); every lane of the wave joins
+  auto partner = [&](FPt& Q, int off) {
 #pragma unroll
-  for (int j = 0; j < fe::L; ++j) {
-    Q.X[j] = __shfl_xor(P.X[j], 1);
-    Q.Y[j] = __shfl_xor(P.Y[j], 1);
-    Q.Z[j] = __shfl_xor(P.Z[j], 1);
-    Q.T[j] = __shfl_xor(P.T[j], 1);
+    for (int j = 0; j < fe::L; ++j) {
+      Q.X[j] = __shfl_xor(P.X[j], off);
+      Q.Y[j] = __shfl_xor(P.Y[j], off);
+      Q.Z[j] = __shfl_xor(P.Z[j], off);
+      Q.T[j] = __shfl_xor(P.T[j], off);
+    }
+    ok = ok && __shfl_xor((int)ok, off) != 0;
+  };
+  if constexpr (S == 4) {                       // lanes xor 1: the two partials of each scalar
+    FPt Q;
+    partner(Q, 1);
+    add_ext(P, P, Q);                           // (add_ext reads all of P before writing R)
   }
-  const bool ok1 = __shfl_xor((int)ok, 1) != 0;
-  if (!live || sub != 0) return;
-  FPt R;
-  add_ext(R, P, Q);
+  {                                             // lane 0: [S]B + [k](-A)
+    FPt Q;
+    partner(Q, H);
+    if (!live || sub != 0) return;
+    add_ext(P, P, Q);
+  }
 #pragma unroll
   for (int j = 0; j < fe::L; ++j) {                // radix-2^25.5 limbs (k_ed_finish converts)
-    a.xyz[(int64_t)j * np + p] = R.X[j];
-    a.xyz[(int64_t)(L + j) * np + p] = R.Y[j];
-    a.xyz[(int64_t)(2 * L + j) * np + p] = R.Z[j];
+    a.xyz[(int64_t)j * np + p] = P.X[j];
+    a.xyz[(int64_t)(L + j) * np + p] = P.Y[j];
+    a.xyz[(int64_t)(2 * L + j) * np + p] = P.Z[j];
   }
-  if (!(ok && ok1)) a.status[p] = ST_REJECT;
+  if (!ok) a.status[p] = ST_REJECT;
 }
 
 // Batched finish (Montgomery's trick, as k_ec_scalar_batch): thread i owns the
@@ -560,28 +574,44 @@ __global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_
 
 }  // namespace
 
-// Measured (profiles/r05_s2/q_ab/, ed_split_ab/): a lone EdDSA batch of 1 ...
-// 4096 tokens 210-244 -> 182-218 us; configs[4]'s 38 k-token Ed25519 launch
-// unchanged (0.081 ms either way), so only small launches split.
+// Measured (profiles/r05_s2/q_ab/, ed_split_ab/, r05_s7/ed4_ab/): a lone
+// EdDSA batch of 1 ... 4096 tokens 210-244 -> 182-218 us with two lanes and
+// 5-12 us less again with four; configs[4]'s 38 k-token Ed25519 launch
+// unchanged with two lanes (0.081 ms either way) and slower with four (0.083
+// -> 0.110 ms), so only small launches split (JG_ED_SPLIT4_MAX: A/B knob).
 #ifndef JG_ED_SPLIT_MAX
 #define JG_ED_SPLIT_MAX 16384
 #endif
+#ifndef JG_ED_SPLIT_LANES
+#define JG_ED_SPLIT_LANES 4
+#endif
+#ifndef JG_ED_SPLIT4_MAX
+#define JG_ED_SPLIT4_MAX 0
+#endif
 constexpr int64_t ED_SPLIT_MAX_TOKENS = JG_ED_SPLIT_MAX;  // launches up to this many padded tokens: k_ed_point_split
+constexpr int64_t ED_SPLIT4_MAX_TOKENS = JG_ED_SPLIT4_MAX;  // ... with 4 lanes per token above ED_SPLIT_MAX_TOKENS
+
+template <int S>
+void launch_ed_split(const EdArgs& a, int64_t waves, hipStream_t s) {
+  dim3 g((unsigned)(S * waves)), b(WAVE);
+  switch (a.wa) {
+    case 24: hipLaunchKernelGGL((k_ed_point_split<24, S>), g, b, 0, s, a); break;
+    case 22: hipLaunchKernelGGL((k_ed_point_split<22, S>), g, b, 0, s, a); break;
+    case 20: hipLaunchKernelGGL((k_ed_point_split<20, S>), g, b, 0, s, a); break;
+    case 18: hipLaunchKernelGGL((k_ed_point_split<18, S>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((k_ed_point_split<16, S>), g, b, 0, s, a); break;
+  }
+}
 
 void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;
   if (waves <= 0) return;
   dim3 g((unsigned)waves), b(WAVE);
   if (a.end - a.begin <= ED_SPLIT_MAX_TOKENS) {
-    // a launch of fewer waves than ~2 per SIMD: two lanes per token
-    dim3 g2((unsigned)(2 * waves));
-    switch (a.wa) {
-      case 24: hipLaunchKernelGGL(k_ed_point_split<24>, g2, b, 0, s, a); break;
-      case 22: hipLaunchKernelGGL(k_ed_point_split<22>, g2, b, 0, s, a); break;
-      case 20: hipLaunchKernelGGL(k_ed_point_split<20>, g2, b, 0, s, a); break;
-      case 18: hipLaunchKernelGGL(k_ed_point_split<18>, g2, b, 0, s, a); break;
-      default: hipLaunchKernelGGL(k_ed_point_split<16>, g2, b, 0, s, a); break;
-    }
+    // a launch of fewer waves than ~2 per SIMD: S lanes per token
+    launch_ed_split<JG_ED_SPLIT_LANES>(a, waves, s);
+  } else if (a.end - a.begin <= ED_SPLIT4_MAX_TOKENS) {
+    launch_ed_split<4>(a, waves, s);
   } else {
   switch (a.wa) {
     case 24: hipLaunchKernelGGL(k_ed_point<24>, g, b, 0, s, a); break;
