@@ -1015,7 +1015,8 @@ def run_configs(ctx, args, threads, rank, world, dist):
     # plan, kernels, verdicts back), chunks overlapping
     share = 10_000_000 // 8
     arena, toks = pack(pool, algs, keyidx, share)
-    st = measure_pcie(ctx, arena, toks, iters=4, chunks=("zc", 196608, 262144, 524288), warm=3)
+    chunks = tuple(c if c == "zc" else int(c) for c in args.stream_chunks.split(","))
+    st = measure_pcie(ctx, arena, toks, iters=4, chunks=chunks, warm=3)
     st["workload"] = f"{share} tokens per GPU (10M / 8) streamed with H2D"
     line["stream"] = st
     del arena, toks
@@ -1138,6 +1139,8 @@ def main():
                     help="unique tokens of configs[3] (EdDSA + ES384; default: the whole 1M batch)")
     ap.add_argument("--c5-table-budget-gb", type=float, default=160.0,
                     help="configs[4] table budget over all curves (160 GiB: every kid at its widest tier)")
+    ap.add_argument("--stream-chunks", default="zc,196608,262144,524288",
+                    help="configs[4] stream: the chunk sizes tried (\"zc\": zero-copy plans); the best is reported")
     ap.add_argument("--c5-legacy-pool", dest="c5_unique", action="store_false",
                     help="configs[4] from 1024 unique tokens per kid (round-2 layout)")
     ap.add_argument("--no-e2e", action="store_true")
