@@ -26,7 +26,8 @@ def main():
     e = jwt.Expected(Issuer="https://example.com/", Audiences=["www.example.com"], SigningAlgorithms=["ES256"],
                      Now=lambda: 1611699344 + 60)
     blob = b"\n".join(pool)
-    pre = os.environ.get("PROBE_PRE")        # "e2e": a 1M-token ValidateBatch on another key set first (the bench's order)
+    pre = os.environ.get("PROBE_PRE")        # "e2e": a 1M-token ValidateBatch on another key set first (the bench's order);
+    #                                          "headline": the bench's headline context (W = 26 tables) first, closed
     keep = None
     if pre == "e2e":
         ks2, _ = jwt.NewJSONWebKeySet(None, "https://bench.example/jwks", "",
@@ -39,9 +40,27 @@ def main():
             v2.ValidateBlob(big, e)
         keep = (ks2, v2) if os.environ.get("PROBE_PRE_KEEP") else None
         del big, v2, ks2
+    if pre == "headline":
+        # the bench's headline leg first: the 4 kids' W = 26 tables under a
+        # 110 GiB budget (~86 GB), a 1 M-token batch, then the context closed
+        import ctypes
+        from cap_amd import _lib
+        ctx = _lib.Context()
+        ctx.set_table_budget(110 << 30)
+        ctx.load_keys(bench.abi_keys(kids))
+        ctx.wait_tables()
+        big = (pool * 16)[:1 << 20]
+        arena, toks = bench.pack(big, [bench.ALG_IDS["ES256"]] * len(big), [i % 4 for i in range(len(big))], len(big))
+        out_v = (ctypes.c_uint8 * len(toks))()
+        L = _lib.lib()
+        for _ in range(3):
+            assert L.jg_verify_batch(ctx.h, ctypes.c_char_p(arena), len(arena), toks.ctypes.data_as(ctypes.POINTER(_lib.JgTok)),
+                                     len(toks), out_v) == 0, ctx.error()
+        ctx.close()
+        del arena, toks, big
     v.ValidateBlob(blob, e)
     ks.WaitTables()
-    res = {"cpu": cpu, "runs": []}
+    res = {"cpu": cpu, "pre": pre, "runs": []}
     for inflight, window in settings:
         ks.SetCoalescing(max_inflight=inflight, window_us=window)
         callers = os.environ.get("PROBE_CALLERS")
