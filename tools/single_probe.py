@@ -17,7 +17,11 @@ def main():
     from cap_amd import jwt
     cpu = bench.cpu_info()
     kids = ["p256-a", "p256-b", "p256-c", "p256-d"]
-    pool = bench.gen_tokens("ES256", 1 << 16, bench.golden_keypaths(kids), cpu["cores_used"], "single")
+    # PROBE_POOL_N / PROBE_TOTAL: pool size and calls per point (the bench's
+    # single line: 262144 unique tokens, each called once)
+    pool = bench.gen_tokens("ES256", int(os.environ.get("PROBE_POOL_N", 1 << 16)), bench.golden_keypaths(kids),
+                            cpu["cores_used"], "single")
+    total = int(os.environ.get("PROBE_TOTAL", 1 << 17))
     jwk = [{"kty": "EC", "kid": f"kid-{i:02d}", "crv": "P-256", **xy} for i, xy in enumerate(bench.p256_jwk_xy(kids))]
     jwks = json.dumps({"keys": jwk}).encode()
     ks, err = jwt.NewJSONWebKeySet(None, "https://bench.example/jwks", "",
@@ -68,7 +72,7 @@ def main():
             v._impl._concurrent_validate(blob, e._native(), c, 1 << 14)
             s0 = ks.CoalescingStats()
             h0 = bench.host_snapshot()
-            r = dict(v._impl._concurrent_validate(blob, e._native(), c, 1 << 17))
+            r = dict(v._impl._concurrent_validate(blob, e._native(), c, total))
             hd = bench.host_delta(h0, bench.host_snapshot())
             s1 = ks.CoalescingStats()
             r["host"] = {k: hd[k] for k in ("utime", "stime", "minflt", "nvcsw", "nivcsw", "cg_nr_throttled", "cg_throttled_usec",
