@@ -474,6 +474,10 @@ def host_delta(a, b):
         if used > 0:
             by_name[name] = by_name.get(name, 0.0) + used
     d["threads_now"] = len(b["thr"])
+    counts = {}
+    for name, _ in b["thr"].values():
+        counts[name] = counts.get(name, 0) + 1
+    d["threads_by_name"] = dict(sorted(counts.items(), key=lambda kv: -kv[1])[:10])
     d["cpu_by_thread_name"] = dict(sorted(by_name.items(), key=lambda kv: -kv[1])[:8])
     return d
 
@@ -547,7 +551,9 @@ def measure_single(pool, kids_jwk, threads, callers_list=None, total=1 << 18):
         # CPU the process spent per call, and whether the cgroup quota throttled it
         r["host"] = {"cpu_us_per_call": (hd["utime"] + hd["stime"]) / max(1, r["calls"]) * 1e6,
                      "stime_s": hd["stime"], "cg_throttled_ms": hd["cg_throttled_usec"] / 1e3,
-                     "voluntary_cs": hd["nvcsw"]}
+                     "voluntary_cs": hd["nvcsw"],
+                     "cpu_s_by_thread_name": dict(list(hd.get("cpu_by_thread_name", {}).items())[:6]),
+                     "threads_by_name": hd.get("threads_by_name")}
         r["value"] = r["calls"] / r["wall_s"]
         r["mean_batch"] = r["calls"] / max(1, batches)
         if r["accepted"] != r["calls"]:
