@@ -1,6 +1,6 @@
 # A/B measurements of one GPU call (run via gpurun from the repo root), each
 # step under its own time limit; results under gpurun_out/ab/.
-#   bash tools/ab_session.sh STEP ...
+#   bash tools/ab/ab_session.sh STEP ...
 # steps:
 #   cfg3:NAME[:LIB]      tools/config_probe.py eddsa_es384 (LIB: a cap_amd/ab_*.so, or VAR=VALUE)
 #   cfg2:NAME[:LIB]      tools/config_probe.py ps512
