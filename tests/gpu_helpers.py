@@ -29,11 +29,15 @@ def jobs_from_tokens(tokens, kid_index):
     signature job; tokens that fail to parse get no job (verdict 0 upstream)."""
     arena = _lib.Arena()
     slots = []
+    parsed = {}                     # tiled fixtures repeat tokens: parse each once
     for t in tokens:
-        p = jws.parse_jws(t["token"])
-        if p is None or not p.crit_ok:
+        if t["token"] not in parsed:
+            p = jws.parse_jws(t["token"])
+            parsed[t["token"]] = None if p is None or not p.crit_ok else \
+                (p.signing_input, jws.b64url_encode(p.signature).encode(), p.alg)
+        job = parsed[t["token"]]
+        if job is None:
             slots.append(None)
             continue
-        sig_b64 = jws.b64url_encode(p.signature).encode()
-        slots.append(arena.add(p.signing_input, sig_b64, p.alg, kid_index[t["key"]]))
+        slots.append(arena.add(job[0], job[1], job[2], kid_index[t["key"]]))
     return arena, slots

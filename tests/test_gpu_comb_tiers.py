@@ -74,11 +74,12 @@ def test_ecdsa_comb_tier(crv, wq):
         ctx.close()
 
 
-@pytest.mark.parametrize("crv,wq", [t for t in _ec_tiers() if t[0] == "P-256"])
+@pytest.mark.parametrize("crv,wq", _ec_tiers())
 def test_ecdsa_comb_tier_mid_launch(crv, wq):
     """The same tokens tiled to ~40 k jobs, so the class launch is past the
-    4-lane split's 16 k and P-256 runs the 2-lane k_ec_point_split
-    (ecdsa_impl.hpp launch_chain); every verdict equals the fixture's."""
+    4-lane split's 16 k: P-256 runs the 2-lane k_ec_point_split, P-384 and
+    P-521 the one-lane k_ec_point (ecdsa_impl.hpp launch_chain); every
+    verdict equals the fixture's."""
     import bench
     from cap_amd import _lib
     s = next(x for x in fixtures()["ec"] if x["crv"] == crv and x["wq"] == wq)
@@ -162,5 +163,31 @@ def test_mixed_width_class_with_exceptions_in_both_runs():
         assert ctx.table_widths() == [24] * len(keys)
         out2 = ctx.verify(arena)
         assert out2 == out
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("wa", [24, 20, 16])
+def test_ed25519_comb_tier_large_launch(wa):
+    """The tier's edge tokens tiled past 16 k jobs, so the class launch runs
+    k_ed_point (one lane per token) instead of the 4-lane k_ed_point_split
+    that every smaller launch takes (ed25519.hip launch_ed)."""
+    import bench
+    from cap_amd import _lib
+    s = fixtures()["ed25519"]
+    reps = 20000 // len(s["tokens"]) + 1
+    toks = s["tokens"] * reps
+    assert len(toks) > 16384
+    kid_index = {k["kid"]: i for i, k in enumerate(s["keys"])}
+    ctx = _lib.Context()
+    try:
+        ctx.set_table_budget(bench.table_bytes("ed25519", wa))
+        ctx.load_keys([H.abi_key(k) for k in s["keys"]])
+        assert ctx.table_widths() == [wa]
+        arena, slots = H.jobs_from_tokens(toks, kid_index)
+        out = ctx.verify(arena)
+        bad = [t["name"] for t, sl in zip(toks, slots)
+               if (0 if sl is None else out[sl]) != t["verdict"]]
+        assert not bad, bad[:10]
     finally:
         ctx.close()
