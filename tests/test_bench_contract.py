@@ -77,3 +77,51 @@ def test_rsa_modexp_layouts_match_the_library():
     # e = 65537: 2 full products (2 L^2 each) + 16 squarings (lanes^2 H(H+1)/2 + L^2)
     h = 112 // g3k
     assert bench.rsa_modexp_mads_per_token(112, g3k) == 4 * 112 * 112 + 16 * (g3k * g3k * h * (h + 1) // 2 + 112 * 112)
+
+
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config")
+
+
+def _full_result():
+    """A complete bench result (round 5's full line, the largest the bench has
+    printed: 22.9 KB) as the stub the line builder compacts."""
+    import json
+    path = os.path.join(ROOT, "profiles", "r05_s9", "bench_full.json")
+    return json.loads(open(path).read().strip().splitlines()[-1])
+
+
+def test_compact_line_fits_and_keeps_the_contract_keys(tmp_path):
+    import json
+    full = _full_result()
+    assert len(json.dumps(full)) > bench.LINE_MAX_BYTES           # the stub is the over-size line
+    full["multi_device"] = {"value": 1.0e9, "devices": [0, 0], "verify_batch": {"value": 5e8},
+                            "validate_batch": {"value": 2e7}, "accepted": 10, "expected_accepted": 10,
+                            "per_device": [{"dev": 0, "kernel_ms": {"x": 1.0}}] * 8}
+    line = bench.compact_line(full, "gpurun_out/bench_detail.json")
+    text = json.dumps(line)
+    assert len(text) <= bench.LINE_MAX_BYTES // 2, len(text)
+    for k in REQUIRED:
+        assert k in line, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in line["roofline"], k
+    assert 0 < line["roofline"]["frac"] < 1
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in line["cpu_baseline"], k
+    assert line["detail"] == "gpurun_out/bench_detail.json"
+    for name, c in line["configs"].items():
+        assert c["accepted"] == c["expected"], name
+        assert c["frac"], name
+    assert line["multi_device"]["verify_batch"] == 5e8
+
+
+def test_emit_line_writes_the_detail_file(tmp_path, capsys):
+    import json
+    full = _full_result()
+    path = str(tmp_path / "detail.json")
+    bench.emit_line(full, path)
+    out = capsys.readouterr().out.strip().splitlines()
+    assert len(out) == 1
+    line = json.loads(out[0])
+    assert line["detail"] == path
+    assert json.load(open(path)) == full
