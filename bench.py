@@ -520,6 +520,76 @@ def measure_e2e(pool, kids_jwk, total, threads):
                     "on host_threads cores + one jg_verify_batch (H2D included); not the headline value"}
 
 
+def md_devices(spec):
+    """--md-devices: "auto" = every visible GPU, or a one-GPU rehearsal [0, 0]
+    (two device slots on one card: the runtime's split, workers and completers
+    run as on two GPUs); else a comma list of device ids."""
+    if spec != "auto":
+        return [int(x) for x in spec.split(",")]
+    import torch
+    n = torch.cuda.device_count()              # does not initialise the GPU
+    return list(range(n)) if n > 1 else [0, 0]
+
+
+def measure_multi_device(pool, kids, kids_jwk, devices, per_dev, threads):
+    """The deployment shape of SURVEY §8(e): ONE process, one jg_ctx spanning
+    `devices`, the runtime's cost-weighted host-side split across them (per
+    device worker + completer, jg_runtime.cpp per_device), no collective.
+    (a) jg_verify_batch of len(devices) x per_dev ES256 tokens from pinned
+    host memory (H2D, plan, kernels, D2H on every device), best of 3;
+    (b) Validator.ValidateBatch over the same tokens through a JWKS key set on
+    the same devices (host parse, kid routing, claims on `threads` cores).
+    Accept counts are checked exactly."""
+    from cap_amd import _lib, jwt
+    total = len(devices) * per_dev
+    ctx = _lib.Context(devices)
+    ctx.load_keys(abi_keys(kids))
+    arena, toks = pack(pool, [ALG_IDS["ES256"]] * len(pool), np.arange(len(pool)) % len(kids), total)
+    vb = measure_pcie(ctx, arena, toks, iters=3, chunks=(262144,), warm=1)
+    L = _lib.lib()
+    out = (ctypes.c_uint8 * len(toks))()
+    pa = _lib.PinnedBuffer(len(arena))
+    ctypes.memmove(pa.ptr, arena, len(arena))
+    if L.jg_verify_batch(ctx.h, pa.ptr, len(arena), toks.ctypes.data_as(ctypes.POINTER(_lib.JgTok)), len(toks),
+                         out) != 0:
+        raise RuntimeError(ctx.error())
+    acc_vb = int(np.frombuffer(out, dtype=np.uint8).sum())
+    pa.free()
+    ctx.close()
+    del arena, toks
+    jwks = json.dumps({"keys": kids_jwk}).encode()
+    ks, err = jwt.NewJSONWebKeySet(None, "https://bench.example/jwks", "",
+                                   lambda url, ca: {"status": 200, "body": jwks, "max_age": 3600}, devices=devices)
+    assert err is None, err
+    v, _ = jwt.NewValidator(ks)
+    e = jwt.Expected(Issuer="https://example.com/", Audiences=["www.example.com"], SigningAlgorithms=["ES256"],
+                     Now=lambda: 1611699344 + 60)
+    reps = (total + len(pool) - 1) // len(pool)
+    blob = b"\n".join((pool * reps)[:total])
+    v.ValidateBlob(b"\n".join(pool[:4096]), e)
+    ks.WaitTables()
+    best, acc_v = float("inf"), 0
+    for _ in range(2):
+        t0 = time.perf_counter()
+        ok = v.ValidateBlob(blob, e)
+        best = min(best, time.perf_counter() - t0)
+        acc_v = sum(ok)
+    del blob
+    res = {"value": vb["value"], "unit": "verified JWTs/s", "devices": devices, "tokens": total,
+           "accepted": acc_vb, "expected_accepted": total,
+           "verify_batch": {"value": vb["value"], "ms_per_batch": vb["ms_per_batch"], "accepted": acc_vb,
+                            "h2d_bytes_per_token": vb["h2d_bytes_per_token"], "raw_h2d_GBps": vb["raw_h2d_GBps"]},
+           "validate_batch": {"value": total / best, "ms_per_batch": best * 1e3, "accepted": acc_v,
+                              "host_threads": threads},
+           "note": "one process, one jg_ctx over `devices` (the runtime's host-side split, per-device streams, no "
+                   "RCCL): jg_verify_batch from pinned host memory and Validator.ValidateBatch over the same "
+                   "ES256 tokens" + ("; [0, 0] = a one-GPU rehearsal: two device slots on one card"
+                                     if len(set(devices)) < len(devices) else "")}
+    if acc_vb != total or acc_v != total:
+        res["error"] = f"accepted {acc_vb} (verify_batch) / {acc_v} (ValidateBatch) of {total}"
+    return res
+
+
 def measure_single(pool, kids_jwk, threads, callers_list=None, total=1 << 18):
     """The drop-in path of an unchanged cap caller: C++
     threads, each calling Validator.Validate once per token -- Go's
@@ -1253,6 +1323,9 @@ def main():
     ap.add_argument("--c5-legacy-pool", dest="c5_unique", action="store_false",
                     help="configs[4] from 1024 unique tokens per kid (round-2 layout)")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--md-devices", default="auto",
+                    help="the one-process multi-device leg's device list (\"auto\": every visible GPU, or the "
+                         "one-GPU rehearsal 0,0); \"none\" skips it")
     ap.add_argument("--e2e-child", metavar="TOKFILE", help=argparse.SUPPRESS)   # measure_e2e_fresh's child
     ap.add_argument("--no-refresh", action="store_true", help="skip configs[4]'s JWKS refresh timings "
                     "(profiling passes: they build key tables)")
@@ -1286,7 +1359,12 @@ def main():
     from cap_amd import _lib
 
     cpu = cpu_info()
-    host_threads = cpu["cores_used"]          # every core this process may use (cgroup quota, affinity)
+    # every core this process may use (cgroup quota, affinity), divided among
+    # the ranks of one node: N ranks must not each take every core
+    host_threads = max(1, cpu["cores_used"] // world)
+    if dist:
+        cpu["cores_used_per_rank"] = host_threads
+        os.environ["CAPJWT_HOST_THREADS"] = str(host_threads)     # the host library's pool (read once, at first use)
     ctx = _lib.Context([dev])
     budget = int(args.table_budget_gb * (1 << 30))
     if dist and COLL_DEVICE == "cpu":
@@ -1449,6 +1527,10 @@ def main():
         inproc["in_process_over_fresh"] = inproc["value"] / fresh["value"]
         result["e2e"] = inproc
         result["single"] = measure_single(pool, jwk, host_threads)
+    if rank == 0 and world == 1 and args.md_devices != "none":
+        jwk = [{"kty": "EC", "kid": f"kid-{i:02d}", "crv": "P-256", **xy} for i, xy in enumerate(p256_jwk_xy(kids))]
+        result["multi_device"] = measure_multi_device(pool, kids, jwk, md_devices(args.md_devices), args.tokens,
+                                                      host_threads)
 
     # ---- CPU baselines (rank 0, N = 1 only), both on every core the process
     # may use.  `cpu_baseline` is OpenSSL libcrypto (tools/cpuverify): the

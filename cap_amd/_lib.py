@@ -23,7 +23,7 @@ EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_las
            "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
            "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_zero_copy", "jg_set_table_budget", "jg_keys_wait_tables",
            "jg_keys_table_widths", "jg_debug_fail_alloc", "jg_debug_table_digest",
-           "jg_debug_max_upgrades", "jg_debug_lifetime_check", "jg_debug_fail_verify"]
+           "jg_debug_max_upgrades", "jg_debug_lifetime_check", "jg_debug_fail_verify", "jg_debug_tables_built"]
 
 
 class JgKey(ctypes.Structure):
@@ -87,6 +87,7 @@ def lib():
         L.jg_debug_lifetime_check.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                               ctypes.POINTER(ctypes.c_uint64)]
         L.jg_debug_table_digest.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+        L.jg_debug_tables_built.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
         L.jg_version.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -211,6 +212,13 @@ class Context:
         v = ctypes.c_uint64()
         if lib().jg_debug_table_digest(self.h, int(key), ctypes.byref(v)) != 0:
             raise JgError(f"jg_debug_table_digest: {self.error()}")
+        return v.value
+
+    def tables_built(self):
+        """jg_debug_tables_built: comb tables this context has built (cache reuses excluded)."""
+        v = ctypes.c_uint64()
+        if lib().jg_debug_tables_built(self.h, ctypes.byref(v)) != 0:
+            raise JgError(f"jg_debug_tables_built: {self.error()}")
         return v.value
 
     def debug_max_upgrades(self, n):

@@ -104,12 +104,12 @@ class HostPool {
     }
     cv_.notify_all();
     size_t i;
-    while ((i = take(&j)) < nt) {
-      task(i);
-      finish(&j);
-    }
+    while ((i = take(&j)) < nt) run_one(&j, i);
+    // every index finishes (a throwing task counts as finished) before j,
+    // which pool threads still reference, leaves this frame
     std::unique_lock<std::mutex> lk(j.m);
     j.cv.wait(lk, [&] { return j.done == nt; });
+    if (j.err) std::rethrow_exception(j.err);
   }
 
  private:
@@ -117,6 +117,7 @@ class HostPool {
     const std::function<void(size_t)>* fn = nullptr;
     size_t nt = 0, next = 0;        // next: under the pool's m_
     size_t done = 0;                // under m
+    std::exception_ptr err;         // the first task exception, under m; rethrown by run()
     std::mutex m;
     std::condition_variable cv;
   };
@@ -136,6 +137,15 @@ class HostPool {
     std::lock_guard<std::mutex> g(j->m);     // the owner destroys j only after taking this lock
     if (++j->done == j->nt) j->cv.notify_all();
   }
+  static void run_one(Job* j, size_t i) {
+    try {
+      (*j->fn)(i);
+    } catch (...) {
+      std::lock_guard<std::mutex> g(j->m);
+      if (!j->err) j->err = std::current_exception();
+    }
+    finish(j);
+  }
   void worker() {
     pthread_setname_np(pthread_self(), "capjwt-host");
     tl_inside_ = true;
@@ -146,8 +156,7 @@ class HostPool {
       const size_t i = j->next++;
       if (j->next == j->nt) q_.pop_front();
       lk.unlock();
-      (*j->fn)(i);
-      finish(j);
+      run_one(j, i);
       lk.lock();
     }
   }
@@ -277,14 +286,28 @@ struct HdrCache {
   std::string recent_key[NRECENT];
   std::shared_ptr<const HdrInfo> recent_val[NRECENT];
   int nrecent = 0, next = 0;
+  // the cache lives as long as its pool thread and its segments come from
+  // callers: it is bounded by bytes, and a segment above kMaxSeg (far above
+  // any issuer's header) is decoded for this token only
+  static constexpr size_t kMaxSeg = 1024, kMaxBytes = 1 << 20;
   std::unordered_map<std::string, std::shared_ptr<const HdrInfo>> m;
+  size_t bytes = 0;
+  std::shared_ptr<const HdrInfo> uncached;
   const std::shared_ptr<const HdrInfo>& get(std::string_view seg) {
     for (int i = 0; i < nrecent; ++i)
       if (recent_key[i] == seg) return recent_val[i];
+    if (seg.size() > kMaxSeg) {
+      uncached = make_hdr(seg);
+      return uncached;
+    }
     auto it = m.find(std::string(seg));
     if (it == m.end()) {
-      if (m.size() > 4096) m.clear();
+      if (bytes + seg.size() > kMaxBytes) {
+        m.clear();
+        bytes = 0;
+      }
       it = m.emplace(std::string(seg), make_hdr(seg)).first;
+      bytes += seg.size() + 64;
     }
     const int slot = next;
     next = (next + 1) % NRECENT;
@@ -1162,7 +1185,17 @@ void Engine::verify(const uint8_t* arena, size_t arena_len, const void* jobs, si
   }
   jg_ticket* t = nullptr;
   const int rc = jg_submit(ctx_, arena, arena_len, (const jg_tok*)jobs, njobs, verdicts, &t);
-  if (submitted) submitted();
+  if (submitted) {
+    // the device worker reads `jobs` and the arena and writes `verdicts` until
+    // jg_wait returns: an exception from the overlapped host work must not
+    // unwind the caller's buffers (or return a pooled arena) before that
+    try {
+      submitted();
+    } catch (...) {
+      if (rc == 0) (void)jg_wait(ctx_, t);
+      throw;
+    }
+  }
   if (rc == -1) throw std::logic_error(std::string("capjwt: jg_submit rejected the host's jobs: ") + jg_last_error(ctx_));
   if (rc != 0) fail_device(std::string("capjwt: jg_verify_batch: ") + jg_last_error(ctx_));
   const int wc = jg_wait(ctx_, t);
@@ -1318,9 +1351,14 @@ void Coalescer::run(Req* r) {
     // every slot busy: whoever finishes a batch finds this request on the stack
     // (the push precedes this caller's view of the slots, which precedes the
     // holder's release, which precedes the holder's look at the stack -- all
-    // sequentially consistent).  No kick here: one futex call per request
-    // from 1024 callers cost 25 s of system time per 131 k calls on the box.
-    active_.fetch_sub(1, std::memory_order_seq_cst);
+    // sequentially consistent).  But the dispatcher that holder kicks may
+    // itself be refused by this caller's brief increment and go back to
+    // sleep; so if this decrement leaves a slot free while requests wait, kick
+    // again.  With every slot truly busy (the heavy-load case) no kick: one
+    // futex call per request from 1024 callers cost 25 s of system time per
+    // 131 k calls on the box.
+    const int prev = active_.fetch_sub(1, std::memory_order_seq_cst);
+    if (prev - 1 < max_inflight_.load(std::memory_order_relaxed) && head_.load(std::memory_order_seq_cst)) kick();
   }
   int st;
   while ((st = r->state.load(std::memory_order_acquire)) != Req::DONE) futex_wait(&r->state, (uint32_t)st);
@@ -1357,7 +1395,14 @@ void Coalescer::dispatch_loop() {
       continue;
     }
     if (active_.fetch_add(1, std::memory_order_seq_cst) >= max_inflight_.load(std::memory_order_relaxed)) {
-      active_.fetch_sub(1, std::memory_order_seq_cst);   // every slot busy: the holder kicks when done
+      // every slot busy: the holder kicks when done.  A slot seen busy only
+      // through another thread's brief increment is free by now: look again
+      // instead of sleeping through the kick that thread may already have sent
+      const int prev = active_.fetch_sub(1, std::memory_order_seq_cst);
+      if (prev - 1 < max_inflight_.load(std::memory_order_relaxed)) {
+        std::this_thread::yield();
+        continue;
+      }
       futex_wait(&seq_, s);
       continue;
     }

@@ -672,7 +672,7 @@ class Helper {
 struct Device {
   int id = 0;
   Lane lane0;                     // resident batches, hashing
-  Lane lane1;                     // resident batches staged second, fourth, ... (CAPJWT_BATCH_LANES)
+  Lane lane1;                     // resident batches staged second, fourth, ...
   hipStream_t kstream = nullptr;  // key loads (staging, narrow tables): beside the verify streams
   hipStream_t ustream = nullptr;  // background width upgrades of key comb tables
   uint32_t* gtab[NCLS] = {};
@@ -687,7 +687,7 @@ struct Device {
   Slot slots[NSLOT + NZSLOT];      // the chunk ring, then the zero-copy plans' ring
   int next_slot = 0, next_lane = 0, next_zslot = 0;
   double gload[3] = {0, 0, 0};    // class-grouped chunks: class cost queued per group lane (relative)
-  int next_res = 0;                // resident batches staged (CAPJWT_BATCH_LANES)
+  int next_res = 0;                // resident batches staged (lane0 / lane1 alternate)
   std::thread worker, completer;
   std::unique_ptr<Helper> planner;  // plans a pipeline item's next chunk (process_item)
   std::mutex qmu;
@@ -737,6 +737,7 @@ struct jg_ctx {
   std::atomic<size_t> zc_max{zc_env_max_jobs()};
   std::atomic<uint64_t> table_budget{default_table_budget()};   // HBM for key comb tables, all curves
   std::atomic<int> fail_alloc{0};            // jg_debug_fail_alloc countdown
+  std::atomic<uint64_t> tables_built{0};     // comb-table builds launched by this context (jg_debug_tables_built)
   // jg_debug_fail_verify: countdown to an injected device failure of a
   // submission; once it fires the context is `poisoned` (every later
   // submission fails, as after a sticky HIP error) until it is destroyed
@@ -2412,6 +2413,7 @@ std::shared_ptr<DevGen> stage_device(jg_ctx* ctx, Device* d, const StagedKeys& S
   }
   if (nk) HIPCHK(hipMemcpyAsync(dk, g->mirror.data(), sizeof(DevKey) * nk, hipMemcpyHostToDevice, s));
   build_tables(groups, dk, blob, di, s);          // synchronises s
+  ctx->tables_built.fetch_add(first.size());
   pc.lap("new comb tables (kernels)");
   for (const auto& f : fresh) cache_table(d->id, f.second.id + (char)f.second.w, f.second.buf);   // at its final width
   return g;
@@ -2491,6 +2493,7 @@ bool upgrade_one(jg_ctx* ctx, std::set<std::string>& skip) {
     // sliced: the upgrade stream may share a hardware queue with a verify
     // lane, which then waits at most one slice behind it (tables.hpp)
     build_tables(groups, tmp->as<DevKey>(), G.keyblob(), (int32_t*)((char*)tmp->p + sizeof(DevKey)), d->ustream, true);
+    ctx->tables_built.fetch_add(1);
     cache_table(d->id, key, t);
     built[i] = t;
   });
@@ -2869,6 +2872,12 @@ int jg_debug_table_digest(jg_ctx* ctx, int key, uint64_t* digest) {
     ctx->set_err(e.what());
     return -2;
   }
+}
+
+int jg_debug_tables_built(jg_ctx* ctx, uint64_t* built) {
+  if (!ctx || !built) return -1;
+  *built = ctx->tables_built.load();
+  return 0;
 }
 
 int jg_debug_fail_alloc(jg_ctx* ctx, int n) {

@@ -67,10 +67,11 @@ class KeySet:
     def VerifySignatureBatch(self, tokens: Sequence, ctx=None):
         return [tuple(r) for r in self._impl.verify_signature_batch(list(tokens))]
 
-    def SetCoalescing(self, max_inflight=2, max_batch=65536, window_us=0):
+    def SetCoalescing(self, max_inflight=4, max_batch=65536, window_us=0):
         """Batching of concurrent single-token calls (VerifySignature and
         Validator.Validate): at most `max_inflight` device batches at once, each
-        of at most `max_batch` tokens, collected for at most `window_us`."""
+        of at most `max_batch` tokens, collected for at most `window_us`.  The
+        defaults are the library's (host/cap_jwt.hpp CoalesceConfig)."""
         self._impl.set_coalescing(int(max_inflight), int(max_batch), int(window_us))
 
     def CoalescingStats(self):

@@ -147,6 +147,12 @@ int jg_debug_lifetime_check(int enable, uint64_t* violations, uint64_t* checked)
  * different paths must agree.  Returns 0, -1 or -2. */
 int jg_debug_table_digest(jg_ctx* ctx, int key, uint64_t* digest);
 
+/* Test hook: the number of key comb tables this context has built so far, on
+ * every device (key loads and background width upgrades; a table reused from
+ * the per-device cache -- same key content and width -- is not a build).
+ * Returns 0 or -1. */
+int jg_debug_tables_built(jg_ctx* ctx, uint64_t* built);
+
 /* Verify ntok jobs, blocking (= jg_submit + jg_wait).  Host buffers; copied to
  * the device(s) in chunks whose H2D copies overlap the kernels of the previous
  * chunk (direct DMA when `arena` is pinned -- jg_host_alloc -- else through
@@ -226,9 +232,9 @@ void jg_host_free(void* p);
  * the verify kernels on the resident inputs (no H2D) and, if verdict_out is
  * non-NULL, copies verdicts back.  jg_batch_run is asynchronous when
  * verdict_out is NULL; jg_batch_sync waits.  Consecutively staged batches of a
- * device alternate between two compute lanes on different hardware queues
- * (CAPJWT_BATCH_LANES=1: one lane): runs of one batch are in order, runs of
- * two batches enqueued back to back overlap on the device. */
+ * device alternate between two compute lanes on different hardware queues:
+ * runs of one batch are in order, runs of two batches enqueued back to back
+ * overlap on the device. */
 int jg_batch_stage(jg_ctx* ctx, int device_slot, const uint8_t* arena, size_t arena_len,
                    const jg_tok* toks, size_t ntok, jg_batch** out);
 int jg_batch_run(jg_ctx* ctx, jg_batch* b, uint8_t* verdict_out);

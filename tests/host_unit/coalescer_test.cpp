@@ -2,7 +2,10 @@
 // sanitizer by tests/test_coalescer.py: every request is carried by exactly
 // one batch, at the index the caller is told; a batch that throws reaches
 // exactly its own callers; reconfiguring the dispatcher count while calls are
-// in flight loses none.  The Exec stands in for KeySet::verify_raw (no device).
+// in flight loses none; bursts of callers at max_inflight = 1 followed by
+// silence all return (no lost wake-up).  The Exec stands in for KeySet::verify_raw (no device).
+#include <unistd.h>
+
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -94,6 +97,45 @@ int main() {
   if (g_bad.load()) return fail("a caller told a wrong index / outcome, or not carried");
   if (g_seen.size() != (size_t)T * M || st.calls != (uint64_t)T * M) return fail("request count");
   if (st.batches != g_batches.load() || st.max_batch_seen < 2) return fail("batch count");
+
+  // bursts at max_inflight = 1, then silence: every caller must return without
+  // a later call arriving to kick the dispatcher (a lost wake-up hangs here)
+  {
+    capjwt::CoalesceConfig c;
+    c.max_inflight = 1;
+    c.max_batch = 65536;
+    c.window_us = 0;
+    co.configure(c);
+  }
+  for (int round = 0; round < 300; ++round) {
+    const int B = 2 + round % 7;
+    std::atomic<int> ready{0}, back{0};
+    std::vector<std::thread> bt;
+    for (int t = 0; t < B; ++t)
+      bt.emplace_back([&, t] {
+        ready.fetch_add(1);
+        while (ready.load() < B) {
+        }
+        const std::string tok = "burst-" + std::to_string(round) + "-" + std::to_string(t);
+        Coalescer::Req q;
+        q.tok = tok;
+        try {
+          co.run(&q);
+        } catch (const std::runtime_error&) {
+        }
+        back.fetch_add(1);
+      });
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+    while (back.load() < B) {
+      if (std::chrono::steady_clock::now() > deadline) {
+        std::printf("FAIL: burst %d: %d of %d callers never returned (lost wake-up)\n", round, B - back.load(), B);
+        std::fflush(stdout);
+        _exit(1);
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    for (auto& x : bt) x.join();
+  }
   std::printf("coalescer test ok\n");
   return 0;
 }

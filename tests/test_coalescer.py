@@ -33,9 +33,8 @@ def test_coalescer_under_sanitizer(san):
         if san == "tsan" and r.returncode != 0 and "tsan" in r.stderr.lower():
             pytest.skip("no TSan runtime: " + r.stderr[-300:])
         assert r.returncode == 0, r.stderr[-3000:]
-        env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1",
+        env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0", UBSAN_OPTIONS="halt_on_error=1",
                    TSAN_OPTIONS="halt_on_error=1")
-        env.pop("LD_PRELOAD", None)
         r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
         assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
         assert "coalescer test ok" in r.stdout

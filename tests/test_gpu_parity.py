@@ -168,21 +168,20 @@ def test_key_reload_reuses_tables():
     content into the new key blob) and builds only new ones: reloading the
     golden key set in reverse order, then a subset, verifies every golden token
     exactly as a fresh load does.  The first load holds a key no earlier test
-    loaded, so it builds at least that key's table; the last reload builds
-    nothing and must be faster (the golden keys' own tables may already be in
-    the per-device cache from earlier tests of the session)."""
-    import time
+    loaded, so it builds at least that key's table; the final reload (the
+    first load's key list again) builds none (jg_debug_tables_built, a
+    counter: no wall-clock comparison).  The subset may build wider tables:
+    fewer keys share the budget."""
     from cap_amd import _lib
     keys, toks = H.golden()
     keys = keys + [_fresh_p256_key()]
     c = _lib.Context()
-    t0 = time.perf_counter()
     c.load_keys([H.abi_key(k) for k in keys])
-    first = time.perf_counter() - t0
+    c.wait_tables()
+    built = c.tables_built()
+    assert built >= 1                 # the fresh key's table at least
     for order in (keys[::-1], keys[::2], keys):
-        t0 = time.perf_counter()
         c.load_keys([H.abi_key(k) for k in order])
-        again = time.perf_counter() - t0
         kid_index = {k["kid"]: i for i, k in enumerate(order)}
         sel = [t for t in toks if t["key"] in kid_index]
         arena, slots = H.jobs_from_tokens(sel, kid_index)
@@ -190,7 +189,10 @@ def test_key_reload_reuses_tables():
         bad = [(t["name"], out[s] if s is not None else 0, t["verdict"]) for t, s in zip(sel, slots)
                if (0 if s is None else out[s]) != t["verdict"]]
         assert not bad, bad
-    assert again < first            # the last reload rebuilds nothing
+        c.wait_tables()
+        if order is keys:
+            assert c.tables_built() == built, (c.tables_built(), built)
+        built = c.tables_built()
     c.close()
 
 

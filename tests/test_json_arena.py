@@ -24,8 +24,7 @@ def test_json_arena_under_asan():
                             "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-o", exe] + srcs,
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-3000:]
-        env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
-        env.pop("LD_PRELOAD", None)
+        env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0", UBSAN_OPTIONS="halt_on_error=1")
         r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
         assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
         assert "json arena test ok" in r.stdout
