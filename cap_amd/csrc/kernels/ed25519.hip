@@ -48,6 +48,9 @@ struct EPt { uint32_t X[L], Y[L], Z[L], T[L]; };
 // convert at the boundary (entries are stored canonical in radix 2^25.5).
 struct FPt { uint32_t X[fe::L], Y[fe::L], Z[fe::L], T[fe::L]; };
 
+#ifndef JG_ED_SHARE_PRE
+#define JG_ED_SHARE_PRE 0
+#endif
 // extended + Niels (y+x, y-x, 2dxy) affine -> extended (complete, a = -1):
 // 7 products.  fe::mul's second operand carries the factor 19 and must be the
 // smaller one: the point side for A, B, C, then E and G (tools/fe25519_bounds.py)
@@ -56,12 +59,20 @@ __device__ __forceinline__ void add_niels(FPt& P, const uint32_t* ypx, const uin
   // ordered so that each input dies as early as it can (P.T and 2dxy first):
   // the live set stays near 4 field elements + one product's columns
   fe::mul(C, t2d, P.T);
-  fe::add(t, P.Z, P.Z);                                   // D
-  fe::sub(F, t, C); fe::add(G, t, C);
+  fe::sub_dbl(F, P.Z, C); fe::add_dbl(G, P.Z, C);         // D - C, D + C with D = 2 Z
   fe::sub(t, P.Y, P.X); fe::mul(A, ymx, t);
   fe::add(t, P.Y, P.X); fe::mul(B, ypx, t);
   fe::sub(E, B, A); fe::add(H, B, A);
+#if JG_ED_SHARE_PRE
+  // E and G are the g side of two products each, F and H the f side: their
+  // operand forms are prepared once
+  uint32_t e19[fe::L], g19[fe::L], f2[fe::L], h2[fe::L];
+  fe::pre_g(e19, E); fe::pre_g(g19, G); fe::pre_f(f2, F); fe::pre_f(h2, H);
+  fe::mul_pre(P.X, F, f2, E, e19); fe::mul_pre(P.T, H, h2, E, e19);
+  fe::mul_pre(P.Y, H, h2, G, g19); fe::mul_pre(P.Z, F, f2, G, g19);
+#else
   fe::mul(P.X, F, E); fe::mul(P.T, H, E); fe::mul(P.Y, H, G); fe::mul(P.Z, F, G);
+#endif
 }
 
 // extended + extended in radix 2^25.5 (complete, a = -1; add-2008-hwcd-3 with
@@ -152,11 +163,13 @@ __device__ __forceinline__ void recode(int* dg, const uint32_t* s, int stride = 
   }
 }
 
-// JG_ED_POINT_ATTR: occupancy A/B hook.  The compiler's choice, ~141 VGPRs,
-// gives 3 waves per SIMD; capped at 4 waves (128 VGPRs, 14-18 spilled) the
-// Ed25519 class cost went 1.53 -> 1.59 ns per token (profiles/r04_s6/)
+// JG_ED_POINT_ATTR: occupancy.  With fe::mul's asm columns the compiler takes
+// 129-132 VGPRs (3 waves per SIMD); capped at 4 waves it spills 5 registers
+// and runs 1 % faster (1 M EdDSA tokens at W = 24: 0.874 -> 0.866 ms, HEAD's
+// C++ columns 0.917 ms, profiles/r06_s2/ed_ab.json).  Round 4: with the C++
+// columns at ~141 VGPRs the same cap cost 4 % (profiles/r04_s6/).
 #ifndef JG_ED_POINT_ATTR
-#define JG_ED_POINT_ATTR
+#define JG_ED_POINT_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
 template <int WA>
 __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
