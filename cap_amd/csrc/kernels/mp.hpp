@@ -22,6 +22,7 @@
 #include "field_consts.hpp"
 #include "mad.hpp"
 #include "mad_blocks.hpp"
+#include "col_chains.hpp"
 
 #define MP_W 28
 #define MP_MASK 0x0fffffffu
@@ -347,13 +348,77 @@ MPD void mont_mul_p384_cols(uint32_t* r, const uint32_t* a, const uint32_t* b) {
   r[L - 1] = (uint32_t)carry & MP_MASK;    // column 2L-1: no products, only the carries
 }
 
+// mont_mul_p384_cols with every column as ONE asm MAD chain (col_chains.hpp):
+// the carry of column k-1 is the first addend, then the partial products
+// (v_mad_u64_u32) and the reduction terms (v_mad_i64_i32 with the SGPR
+// constants).  The same terms land in the same columns, so the value and the
+// column bounds are mont_mul_p384_cols'; LLVM's form adds each carry with a
+// separate 64-bit add (it reassociates the C++ sum), which this saves: one
+// instruction per column, 27 per product.
+#ifndef JG_P384_ASM
+#define JG_P384_ASM 1
+#endif
+template <bool SQR, int K>
+MPD void p384_col(uint32_t* r, const uint32_t* a, const uint32_t* a2, const uint32_t* b, int32_t* q, int64_t& carry,
+                  const int32_t* cs) {
+  constexpr int L = P384P::L;
+  constexpr int lo = K < L ? 0 : K - L + 1;
+  constexpr int hi = SQR ? K / 2 : (K < L ? K : L - 1);
+  constexpr int N = hi >= lo ? hi - lo + 1 : 0;
+  uint32_t x[N > 0 ? N : 1], y[N > 0 ? N : 1];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const int i = lo + n, j = K - i;
+    if constexpr (SQR) {
+      x[n] = i == j ? a[i] : a2[i];
+      y[n] = a[j];
+    } else {
+      x[n] = a[i];
+      y[n] = b[j];
+    }
+  }
+  constexpr bool t4 = K >= 1 && K - 1 < L, t12 = K >= 3 && K - 3 < L, t16 = K >= 4 && K - 4 < L,
+                 t20 = K >= 13 && K - 13 < L;
+  constexpr int M = (int)t4 + (int)t12 + (int)t16 + (int)t20;
+  int32_t qq[M > 0 ? M : 1], cc_[M > 0 ? M : 1];
+  int m = 0;
+  if constexpr (t4) { qq[m] = q[K - 1]; cc_[m++] = cs[0]; }
+  if constexpr (t12) { qq[m] = q[K - 3]; cc_[m++] = cs[1]; }
+  if constexpr (t16) { qq[m] = q[K - 4]; cc_[m++] = cs[2]; }
+  if constexpr (t20) { qq[m] = q[K - 13]; cc_[m++] = cs[3]; }
+  uint64_t acc = (uint64_t)carry;
+  cc::Chain<N, M, K == 0>::run(acc, x, y, qq, cc_);
+  const int64_t sv = (int64_t)acc;
+  if constexpr (K < L) q[K] = (int32_t)((uint32_t)sv & MP_MASK);
+  else r[K - L] = (uint32_t)sv & MP_MASK;
+  carry = sv >> MP_W;
+  if constexpr (K + 1 < 2 * L - 1) p384_col<SQR, K + 1>(r, a, a2, b, q, carry, cs);
+}
+
+template <bool SQR>
+MPD void mont_mul_p384_asm(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+  constexpr int L = P384P::L;
+  const int32_t cs[4] = {opaque_sgpr(16), opaque_sgpr(-4096), opaque_sgpr(-65536), opaque_sgpr(1048576)};
+  uint32_t a2[L];
+  if constexpr (SQR) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) a2[i] = a[i] << 1;
+  }
+  int32_t q[L];
+  int64_t carry = 0;
+  p384_col<SQR, 0>(r, a, a2, b, q, carry, cs);
+  r[L - 1] = (uint32_t)carry & MP_MASK;    // column 2L-1: no products, only the carries
+}
+
 // Products for the point-addition hot loop: the field's special-form
 // reduction where it has one (P-384), else mul / sqr.  Precondition (P-384):
 // at least one operand has limbs < 2^28 (squares: the operand itself).
 template <class F>
 MPD void mulf(uint32_t* r, const uint32_t* a, const uint32_t* b) {
   if constexpr (std::is_same<F, P384P>::value) {
-#if JG_P384_COLS
+#if JG_P384_COLS && JG_P384_ASM
+    mont_mul_p384_asm<false>(r, a, b);
+#elif JG_P384_COLS
     mont_mul_p384_cols<false>(r, a, b);
 #else
     uint64_t t[2 * F::L];
@@ -367,7 +432,9 @@ MPD void mulf(uint32_t* r, const uint32_t* a, const uint32_t* b) {
 template <class F>
 MPD void sqrf(uint32_t* r, const uint32_t* a) {
   if constexpr (std::is_same<F, P384P>::value) {
-#if JG_P384_COLS
+#if JG_P384_COLS && JG_P384_ASM
+    mont_mul_p384_asm<true>(r, a, a);
+#elif JG_P384_COLS
     mont_mul_p384_cols<true>(r, a, a);
 #else
     uint64_t t[2 * F::L];

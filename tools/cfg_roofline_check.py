@@ -53,9 +53,17 @@ EXTRA = {"eddsa_es384_mixed": ["ed25519_finish"], "ps512_rsa4096": ["rsa4096_pad
 
 
 def bench_line(path):
+    """The bench result of a run's stdout file: the full result from the
+    line's `detail` file (bench.py since round 6: the stdout line is compact),
+    looked up beside `path` first, or the line itself."""
     with open(path) as f:
-        lines = [ln for ln in f.read().splitlines() if ln.startswith("{")]
-    return json.loads(lines[-1])
+        line = json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
+    det = line.get("detail")
+    if det:
+        for cand in (os.path.join(os.path.dirname(path), os.path.basename(det)), det):
+            if os.path.exists(cand):
+                return json.load(open(cand))
+    return line
 
 
 def one_csv(d, pattern):
@@ -102,15 +110,20 @@ def sq_split(rows, window, mark):
 
 
 def main(d, out):
-    bench = bench_line(os.path.join(d, "bench.json"))["configs"]
     kt = bench_line(os.path.join(d, "kt.json"))["configs"]
-    fe = bench_line(os.path.join(d, "fetch.json"))["configs"]
-    wr = bench_line(os.path.join(d, "write.json"))["configs"]
-    sq = bench_line(os.path.join(d, "sq.json"))["configs"]
+    # bench.json: an un-profiled run; without one the traced run's own HIP-event
+    # fractions are checked.  No counter passes: trace only.
+    bp = os.path.join(d, "bench.json")
+    bench = bench_line(bp)["configs"] if os.path.exists(bp) else kt
+    counters = os.path.exists(os.path.join(d, "fetch.json"))
     kt_rows = list(csv.DictReader(open(one_csv(d, "kt/*kernel_trace.csv"))))
-    fe_rows = list(csv.DictReader(open(one_csv(d, "fetch/*counter_collection.csv"))))
-    wr_rows = list(csv.DictReader(open(one_csv(d, "write/*counter_collection.csv"))))
-    sq_rows = list(csv.DictReader(open(one_csv(d, "sq/*counter_collection.csv"))))
+    if counters:
+        fe = bench_line(os.path.join(d, "fetch.json"))["configs"]
+        wr = bench_line(os.path.join(d, "write.json"))["configs"]
+        sq = bench_line(os.path.join(d, "sq.json"))["configs"]
+        fe_rows = list(csv.DictReader(open(one_csv(d, "fetch/*counter_collection.csv"))))
+        wr_rows = list(csv.DictReader(open(one_csv(d, "write/*counter_collection.csv"))))
+        sq_rows = list(csv.DictReader(open(one_csv(d, "sq/*counter_collection.csv"))))
     res = {}
     for cfg, line in bench.items():
         marks = list(line.get("roofline", {})) + EXTRA.get(cfg, [])
@@ -126,6 +139,9 @@ def main(d, out):
                 e.update({"bench_frac": rl["frac"], "rocprof_frac": rl["frac"] * line["kernel_ms"][mark] / ms,
                           "bound": rl["bound"], "unit": rl["unit"]})
                 e["agree"] = abs(e["rocprof_frac"] / rl["frac"] - 1) <= 0.10
+            if not counters:
+                rc[mark] = e
+                continue
             f, nf = counter_sum(fe_rows, fe[cfg]["trace_window"], mark, "FETCH_SIZE")
             w, nw = counter_sum(wr_rows, wr[cfg]["trace_window"], mark, "WRITE_SIZE")
             e["hbm_bytes_per_run"] = (2 * f + w) * 1024          # FETCH/WRITE_SIZE are KiB
@@ -141,9 +157,9 @@ def main(d, out):
         for mark, e in rc.items():
             fr = (f"frac bench {e['bench_frac']:.3f} rocprof {e['rocprof_frac']:.3f}" if "bench_frac" in e
                   else "(no roofline)")
-            sqs = e["sq"] or {}
+            sqs = e.get("sq") or {}
             print(f"{cfg:18s} {mark:16s} ms {e['bench_ms']:.3f}/{e['rocprof_ms_per_run']:.3f} {fr}  "
-                  f"hbm {e['hbm_bytes_per_run'] / 1e6:8.1f} MB  valu {sqs.get('valu_active', 0):.2f} "
+                  f"hbm {e.get('hbm_bytes_per_run', 0) / 1e6:8.1f} MB  valu {sqs.get('valu_active', 0):.2f} "
                   f"stall {sqs.get('issue_stalled', 0):.2f}")
 
 

@@ -26,8 +26,17 @@ SYMS = {"p256_point": "void (anonymous namespace)::k_ec_point<(anonymous namespa
 
 
 def bench_line(path):
+    """The bench result of a run's stdout file: the full result from the
+    line's `detail` file (bench.py since round 6: the stdout line is compact),
+    looked up beside `path` first, or the line itself."""
     with open(path) as f:
-        return json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
+        line = json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
+    det = line.get("detail")
+    if det:
+        for cand in (os.path.join(os.path.dirname(path), os.path.basename(det)), det):
+            if os.path.exists(cand):
+                return json.load(open(cand))
+    return line
 
 
 def rows_of(d, pattern):
