@@ -394,7 +394,11 @@ template <class Fp>
 __device__ __forceinline__ void y3_from(uint32_t* Y, const uint32_t* r, const uint32_t* t, const uint32_t* y1,
                                         const uint32_t* hhh) {
   constexpr int L = Fp::L;
-  if constexpr (sum_ok<Fp>()) {
+  if constexpr (sum_ok<Fp>() && mp::use_ps<Fp>(2)) {
+    uint32_t ny1[L];
+    mp::neg<Fp>(ny1, y1);
+    mp::mont_ps<Fp, 2>(Y, r, t, ny1, hhh);
+  } else if constexpr (sum_ok<Fp>()) {
     uint32_t ny1[L];
     mp::neg<Fp>(ny1, y1);
     uint64_t T[2 * L];
@@ -423,7 +427,12 @@ struct has_kx3<Fp, std::void_t<decltype(Fp::KX3)>> : std::true_type {};
 template <class Fp>
 __device__ __forceinline__ void x3_from(uint32_t* X, const uint32_t* r, const uint32_t* hhh, const uint32_t* v) {
   constexpr int L = Fp::L;
-  if constexpr (has_kx3<Fp>::value) {
+  if constexpr (has_kx3<Fp>::value && mp::use_ps<Fp>(3)) {
+    uint32_t e[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) e[j] = Fp::KX3[j] - (hhh[j] + 2 * v[j]);
+    mp::mont_ps<Fp, 3>(X, r, r, nullptr, nullptr, e);
+  } else if constexpr (has_kx3<Fp>::value) {
     uint64_t T[2 * L];
     mp::sqprod<Fp>(T, r);
     const uint32_t c1 = (uint32_t)mp::opaque_sgpr(1);

@@ -203,6 +203,132 @@ MPD void mont_reduce(uint32_t* r, uint64_t* t) {
   }
 }
 
+// ---- product scanning for the unmasked-row fields (P-256, P-521) --------------
+// The product and its Montgomery reduction column by column, each column ONE
+// asm MAD chain (col_chains.hpp UChain): the carry in, the reduction terms
+// q_j (m+1)_{k-j} of the digits already known, then the partial products.  A
+// low column k <= L-2 yields the unmasked digit q_k = lo32 and carries
+// hi32 * 16 (one MAD at the head of the next chain, on the literal 0); column
+// L-1 yields a 28-bit digit and carries >> 28; a high column yields an output
+// limb (mask) and carries >> 28 -- or, semi-normalized, lo32 and hi32 * 16.
+// Every term lands in the column mont_reduce's row order puts it in, so the
+// value, the column bounds and the output are mont_reduce's bit for bit; the
+// row form pays a 64-bit add per carry of its final chain, which this saves
+// (and it keeps one column live instead of 2L).
+// OP: 0 = a*b, 1 = a^2, 2 = a*b + c*d, 3 = a^2 + e*R (e added to the high
+// columns: x3_from's column subtraction).
+#ifndef JG_PS_ASM
+#define JG_PS_ASM 1
+#endif
+template <class F>
+constexpr int ps_nmul(int k) {
+  const int lo = k - F::L + 1 > 0 ? k - F::L + 1 : 0, hi = k < F::L - 1 ? k : F::L - 1;
+  return hi >= lo ? hi - lo + 1 : 0;
+}
+template <class F>
+constexpr int ps_nsqr(int k) {
+  const int lo = k - F::L + 1 > 0 ? k - F::L + 1 : 0, hi = k / 2;
+  return hi >= lo ? hi - lo + 1 : 0;
+}
+template <class F>
+constexpr int ps_nprod(int op, int k) {
+  return op == 0 ? ps_nmul<F>(k) : op == 2 ? 2 * ps_nmul<F>(k) : ps_nsqr<F>(k);
+}
+template <class F>
+constexpr int ps_nred(int k) {        // digits q_j (j < L, j < k) whose constant (m+1)_{k-j} is non-zero
+  int n = 0;
+  for (int j = (k - F::L + 1 > 0 ? k - F::L + 1 : 0); j < k && j < F::L; ++j)
+    if (red_const<F>(k - j) != 0) ++n;
+  return n;
+}
+template <class F, bool SEMI>
+constexpr bool ps_carry_term(int k) {  // the carry into column k is hi32(column k-1) * 16
+  return (k >= 1 && k - 1 <= F::L - 2) || (SEMI && k - 1 >= F::L);
+}
+template <class F>
+constexpr bool ps_ok(int op) {         // every column fits a generated chain
+  for (int k = 0; k < 2 * F::L - 1; ++k)
+    if (ps_nprod<F>(op, k) > 20 || ps_nred<F>(k) + 2 > 6) return false;
+  return true;
+}
+
+template <class F, int OP, bool SEMI, int K>
+MPD void ps_col(uint32_t* r, const uint32_t* a, const uint32_t* a2, const uint32_t* b, const uint32_t* c,
+                const uint32_t* d, const uint32_t* e, uint32_t* q, uint64_t& carry, uint32_t& hi, uint32_t c16,
+                uint32_t c1) {
+  constexpr int L = F::L;
+  constexpr int N = ps_nprod<F>(OP, K);
+  constexpr bool CT = ps_carry_term<F, SEMI>(K);
+  constexpr bool EX = OP == 3 && K >= L;
+  constexpr int R = (CT ? 1 : 0) + ps_nred<F>(K) + (EX ? 1 : 0);
+  constexpr bool Z = K == 0 || CT;
+  uint32_t x[N > 0 ? N : 1], y[N > 0 ? N : 1], u[R > 0 ? R : 1], kc[R > 0 ? R : 1];
+  int n = 0, m = 0;
+  if constexpr (CT) { u[m] = hi; kc[m++] = c16; }
+  constexpr int jlo = K - L + 1 > 0 ? K - L + 1 : 0;
+#pragma unroll
+  for (int j = jlo; j < K && j < L; ++j)
+    if (red_const<F>(K - j) != 0) { u[m] = q[j]; kc[m++] = red_const<F>(K - j); }
+  if constexpr (EX) { u[m] = e[K - L]; kc[m++] = c1; }
+  constexpr int ilo = K - L + 1 > 0 ? K - L + 1 : 0;
+  if constexpr (OP == 1 || OP == 3) {
+#pragma unroll
+    for (int i = ilo; i <= K / 2; ++i) { x[n] = i == K - i ? a[i] : a2[i]; y[n++] = a[K - i]; }
+  } else {
+#pragma unroll
+    for (int i = ilo; i <= K && i < L; ++i) { x[n] = a[i]; y[n++] = b[K - i]; }
+    if constexpr (OP == 2) {
+#pragma unroll
+      for (int i = ilo; i <= K && i < L; ++i) { x[n] = c[i]; y[n++] = d[K - i]; }
+    }
+  }
+  uint64_t s = carry;
+  cc::UChain<N, R, Z>::run(s, x, y, u, kc);
+  if constexpr (K <= L - 2) {
+    q[K] = (uint32_t)s;
+    hi = (uint32_t)(s >> 32);
+  } else if constexpr (K == L - 1) {
+    q[K] = (uint32_t)s & MP_MASK;
+    carry = s >> MP_W;
+  } else if constexpr (SEMI) {
+    r[K - L] = (uint32_t)s;
+    hi = (uint32_t)(s >> 32);
+  } else {
+    r[K - L] = (uint32_t)s & MP_MASK;
+    carry = s >> MP_W;
+  }
+  if constexpr (K + 1 < 2 * L - 1) ps_col<F, OP, SEMI, K + 1>(r, a, a2, b, c, d, e, q, carry, hi, c16, c1);
+}
+
+template <class F, int OP, bool SEMI = false>
+MPD void mont_ps(uint32_t* r, const uint32_t* a, const uint32_t* b, const uint32_t* c = nullptr,
+                 const uint32_t* d = nullptr, const uint32_t* e = nullptr) {
+  constexpr int L = F::L;
+  static_assert(unmasked_rows<F>() && ps_ok<F>(OP), "product scanning: unmasked-row fields whose columns fit a chain");
+  uint32_t a2[L];
+  if constexpr (OP == 1 || OP == 3) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) a2[i] = a[i] << 1;
+  }
+  uint32_t q[L];
+  uint64_t carry = 0;
+  uint32_t hi = 0;
+  const uint32_t c16 = (uint32_t)opaque_sgpr(16), c1 = (uint32_t)opaque_sgpr(1);
+  ps_col<F, OP, SEMI, 0>(r, a, a2, b, c, d, e, q, carry, hi, c16, c1);
+  // column 2L-1: no products, the carry (and OP 3's top term e_{L-1})
+  if constexpr (SEMI) r[L - 1] = hi * 16u;
+  else if constexpr (OP == 3) r[L - 1] = ((uint32_t)carry + e[L - 1]) & MP_MASK;
+  else r[L - 1] = (uint32_t)carry & MP_MASK;
+}
+template <class F>
+constexpr bool use_ps(int op) {
+  if constexpr (!F::NP1) {
+    return false;
+  } else {
+    return JG_PS_ASM && unmasked_rows<F>() && ps_ok<F>(op);
+  }
+}
+
 // t = a*b (2L 64-bit columns, t[2L-1] = 0)
 template <class F>
 MPD void prod(uint64_t* t, const uint32_t* a, const uint32_t* b) {
@@ -251,17 +377,25 @@ MPD void sqprod(uint64_t* t, const uint32_t* a) {
 // r = a*b/R mod m
 template <class F>
 MPD void mul(uint32_t* r, const uint32_t* a, const uint32_t* b) {
-  uint64_t t[2 * F::L];
-  prod<F>(t, a, b);
-  mont_reduce<F>(r, t);
+  if constexpr (use_ps<F>(0)) {
+    mont_ps<F, 0>(r, a, b);
+  } else {
+    uint64_t t[2 * F::L];
+    prod<F>(t, a, b);
+    mont_reduce<F>(r, t);
+  }
 }
 
 // r = a^2/R mod m
 template <class F>
 MPD void sqr(uint32_t* r, const uint32_t* a) {
-  uint64_t t[2 * F::L];
-  sqprod<F>(t, a);
-  mont_reduce<F>(r, t);
+  if constexpr (use_ps<F>(1)) {
+    mont_ps<F, 1>(r, a, a);
+  } else {
+    uint64_t t[2 * F::L];
+    sqprod<F>(t, a);
+    mont_reduce<F>(r, t);
+  }
 }
 
 
@@ -450,7 +584,9 @@ MPD void sqrf(uint32_t* r, const uint32_t* a) {
 // allows it (semi_ok), else sqrf's normalized result
 template <class F>
 MPD void sqr_semi(uint32_t* r, const uint32_t* a) {
-  if constexpr (semi_ok<F>()) {
+  if constexpr (semi_ok<F>() && use_ps<F>(1)) {
+    mont_ps<F, 1, true>(r, a, a);
+  } else if constexpr (semi_ok<F>()) {
     uint64_t t[2 * F::L];
     sqprod<F>(t, a);
     mont_reduce<F, true>(r, t);

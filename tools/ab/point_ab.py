@@ -2,7 +2,7 @@
 with AB_ALG=ES384, ES384) tokens on one key (32 GiB budget: W = 24 tables),
 per-kernel times of synchronous runs (bench.measure), one child process per
 library variant (CAPJWT_LIB), the variants alternated 3 times.
-usage: [AB_ALG=ES384] python tools/ab/ed_point_ab.py out.json name=lib.so [name=lib.so ...]"""
+usage: [AB_ALG=ES384|ES256|ES512] python tools/ab/ed_point_ab.py out.json name=lib.so [name=lib.so ...]"""
 import json
 import os
 import subprocess
@@ -13,6 +13,8 @@ sys.path.insert(0, ROOT)
 
 
 ALGS = {"EdDSA": ("ed-a", "ed25519_point", "ed25519_point_mads_per_token"),
+        "ES256": ("p256-a", "p256_point", "p256_point_mads_per_token"),
+        "ES512": ("p521-a", "p521_point", "p521_point_mads_per_token"),
         "ES384": ("p384-a", "p384_point", "p384_point_mads_per_token")}
 
 
