@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 KEYDIR = os.path.join(ROOT, "tests", "golden", "keys")
 BENCHKEYS = os.path.join(ROOT, "tools", "benchkeys")
 TOKGEN = os.path.join(ROOT, "tools", "tokgen", "tokgen")
-TRAFFIC = os.path.join(ROOT, "profiles", "r04_s5_pmc_traffic.json")
+TRAFFIC = os.path.join(ROOT, "profiles", "r06_s3_pmc_traffic.json")
 COLL_DEVICE = "cuda"            # device of the timing all-reduce (RCCL); "cpu" under gloo
 
 # measured v_mad_u64_u32 issue rate, chip-wide: the integer multiply-add
