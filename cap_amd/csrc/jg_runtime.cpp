@@ -62,6 +62,7 @@ namespace {
 
 constexpr size_t ARENA_SLACK = 256;   // aligned SHA word reads may run past the last string
 constexpr int NLANE = 3;              // compute streams per device (HW queues 1..3; the copy stream has 0)
+constexpr size_t SMALL_SUBMIT = 4096;  // submissions up to this many jobs go whole to one device slot
 constexpr int NSLOT = 8;              // chunk buffer sets per device (pipeline depth)
 constexpr int NZSLOT = 2;             // buffer sets of zero-copy plans (whole items; after the NSLOT ring)
 constexpr int NALG = 16;              // alg ids 0..15 in the class table (jg_alg <= 10)
@@ -738,6 +739,7 @@ struct jg_ctx {
   std::atomic<uint64_t> table_budget{default_table_budget()};   // HBM for key comb tables, all curves
   std::atomic<int> fail_alloc{0};            // jg_debug_fail_alloc countdown
   std::atomic<uint64_t> tables_built{0};     // comb-table builds launched by this context (jg_debug_tables_built)
+  std::atomic<uint64_t> small_rr{0};         // device slot of the next small submission (submit_to)
   // jg_debug_fail_verify: countdown to an injected device failure of a
   // submission; once it fires the context is `poisoned` (every later
   // submission fails, as after a sticky HIP error) until it is destroyed
@@ -1259,7 +1261,8 @@ struct GroupFan {
 
 // vpad_zeroed: the device plan fill zeroed every padded slot's verdict (pipeline chunks)
 void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, const Plan& P, jg_batch* marks,
-              bool fanout = true, const GroupFan* gf = nullptr, bool vpad_zeroed = false) {
+              bool fanout = true, const GroupFan* gf = nullptr, bool vpad_zeroed = false,
+              uint8_t* verdict_dst = nullptr) {
   if (check_keys_env()) check_device_records(G);
   const bool timed = marks && marks->timing;
   int nact = 0;
@@ -1408,7 +1411,8 @@ void run_plan(Device* d, const KeyState& K, const DevGen& G, Lane* L, Bufs* B, c
     }
   }
   for (const auto& [c, x] : exact_later) launch_ec(c, x, s0, Marker{});   // s0 waited for every class
-  launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p, (uint8_t*)B->verdict.p, np, s0);
+  launch_scatter((const int32_t*)B->perm.p, (const uint8_t*)B->vpad.p,
+                 verdict_dst ? verdict_dst : (uint8_t*)B->verdict.p, np, s0);
   mark(marks, "scatter");
   HIPCHK(hipGetLastError());
   // the class streams logged their uses above; the chunk's control stream
@@ -1720,8 +1724,6 @@ void issue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const ChunkPl
   if (tr) S.host_ms[4] = ms_since(t_enq);
   const uint8_t* hbd = (const uint8_t*)S.h_meta.dp;
   const hipStream_t cs = d->copy;
-  if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
-  if (bytes && !zc) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, cs));
   int nact = 0, jgrp = 0;
   double gcost[3] = {0, 0, 0};
   for (int c = 1; c < NCLS; ++c) {
@@ -1734,11 +1736,20 @@ void issue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const ChunkPl
     if (gcost[g] > gcost[jgrp]) jgrp = g;
   // a zero-copy plan always runs grouped: its classes' gathers ride on the GroupFan
   const bool grouped = (it.grouped && nact >= 2) || zc;
+  // A small ungrouped chunk (coalesced single-token calls) runs its whole
+  // chain on its lane: the arena copy on the lane itself (no copy-stream event
+  // and wait) and the verdicts scattered straight into pinned memory (no copy
+  // kernel) -- 3 of its ~14 HIP calls fewer.  The device's submission thread,
+  // which issues them, is what bounds small-batch throughput
+  // (profiles/r06_s6/single_probe.log).  (Traced runs keep the copy stream.)
+  const bool small = !grouped && n <= SMALL_SUBMIT && !tr;
+  if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
+  if (bytes && !zc) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, small ? s : cs));
   // grouped chunks: the whole plan block goes over by DMA behind the arena
   // (the plan fill then reads device memory); else the header by a copy
   // kernel and the jobs read in place from pinned memory
   if (grouped) HIPCHK(hipMemcpyAsync(dm, hb, L.bytes, hipMemcpyHostToDevice, cs));
-  HIPCHK(hipEventRecord(S.copied, cs));
+  if (!small) HIPCHK(hipEventRecord(S.copied, cs));
   if (tr) HIPCHK(hipEventRecord(S.tr_b, cs));
   if (tr) S.host_ms[3] = ms_since(t_enq);
   GroupFan gf;
@@ -1774,7 +1785,7 @@ void issue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const ChunkPl
     for (int c = 0; c < NCLS; ++c) gf.done[c] = S.ev_cls[c];
     fs = gf.ctrl;
   }
-  if (fs != cs) HIPCHK(hipStreamWaitEvent(fs, S.copied, 0));
+  if (fs != cs && !small) HIPCHK(hipStreamWaitEvent(fs, S.copied, 0));
   if (!grouped) launch_copy(hbd, dm, L.toks_off, fs);
   {
     PlanFillArgs fa{};
@@ -1793,16 +1804,16 @@ void issue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const ChunkPl
   }
   const auto t_run = std::chrono::steady_clock::now();
   if (tr) S.host_ms[5] = ms_since(t_enq);
+  S.h_verdict.get(std::max<size_t>(n, 1));
   if (grouped) {
     run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, &gf, true);
     s = gf.join;                                   // verdicts leave once every class is done
   } else {
-    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, nullptr, true);
+    run_plan(d, K, G, &LN, &S.bufs, P, nullptr, false, nullptr, true, small ? (uint8_t*)S.h_verdict.dp : nullptr);
   }
   if (tr) S.host_ms[6] = ms_since(t_run);
   if (tr) HIPCHK(hipEventRecord(S.tr_c, s));
-  S.h_verdict.get(std::max<size_t>(n, 1));
-  launch_copy(S.bufs.verdict.p, S.h_verdict.dp, n, s);
+  if (!small) launch_copy(S.bufs.verdict.p, S.h_verdict.dp, n, s);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(S.done, s));
   if (tr) S.host_ms[2] = ms_since(t_enq);
@@ -2576,7 +2587,15 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
   const size_t nd = ctx->devs.size();
   std::vector<size_t> cut(nd + 1, 0);
   cut[nd] = ntok;
-  if (nd > 1) {
+  if (nd > 1 && ntok <= SMALL_SUBMIT) {
+    // a small submission (coalesced single-token calls) goes whole to one
+    // device slot, round robin: split, it would pay one full chain latency on
+    // each of several devices and hold each device's submission thread, which
+    // is what bounds small-batch throughput (~15 k batches/s per slot: the
+    // ~15 HIP calls of a chunk, profiles/r06_s6/single_probe.log)
+    const size_t k = (size_t)(ctx->small_rr.fetch_add(1) % nd);
+    for (size_t j = 0; j <= nd; ++j) cut[j] = j > k ? ntok : 0;
+  } else if (nd > 1) {
     std::vector<double> pre(ntok + 1, 0.0);
     const size_t nk = ks->keys.size();
     for (size_t i = 0; i < ntok; ++i) {

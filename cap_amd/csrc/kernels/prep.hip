@@ -501,6 +501,9 @@ void launch_prep(int cls, int hash_mask, const PrepArgs& a0, hipStream_t s) {
   if (waves <= 0) return;
   PrepArgs a = a0;
   if (cls == CLS_ED25519 || !(hash_mask & 1)) a.mid = nullptr;      // SHA-256 block 0 only
+  // a launch of a few waves (a coalesced single-token batch): one dependent
+  // launch fewer on its chain outweighs the shared block 0
+  if (waves <= 2) a.mid = nullptr;
   if (a.mid) hipLaunchKernelGGL(k_prep_mid, dim3((unsigned)((waves + 63) / 64)), dim3(64), 0, s, a);
   dim3 g((unsigned)waves), b(WAVE);
   switch (cls) {

@@ -24,8 +24,10 @@ def main():
     total = int(os.environ.get("PROBE_TOTAL", 1 << 17))
     jwk = [{"kty": "EC", "kid": f"kid-{i:02d}", "crv": "P-256", **xy} for i, xy in enumerate(bench.p256_jwk_xy(kids))]
     jwks = json.dumps({"keys": jwk}).encode()
+    # PROBE_DEVICES: the key set's device slots ("0,0": two submission pipelines on one GPU)
+    devs = [int(x) for x in os.environ.get("PROBE_DEVICES", "").split(",") if x]
     ks, err = jwt.NewJSONWebKeySet(None, "https://bench.example/jwks", "",
-                                   lambda url, ca: {"status": 200, "body": jwks, "max_age": 3600})
+                                   lambda url, ca: {"status": 200, "body": jwks, "max_age": 3600}, devices=devs)
     v, _ = jwt.NewValidator(ks)
     e = jwt.Expected(Issuer="https://example.com/", Audiences=["www.example.com"], SigningAlgorithms=["ES256"],
                      Now=lambda: 1611699344 + 60)
