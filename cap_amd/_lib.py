@@ -23,7 +23,8 @@ EXPORTS = ["jg_create", "jg_destroy", "jg_keys_load", "jg_verify_batch", "jg_las
            "jg_batch_free", "jg_batch_kernel_times", "jg_batch_exceptions", "jg_hash_batch", "jg_version",
            "jg_submit", "jg_wait", "jg_set_chunk", "jg_set_zero_copy", "jg_set_table_budget", "jg_keys_wait_tables",
            "jg_keys_table_widths", "jg_debug_fail_alloc", "jg_debug_table_digest",
-           "jg_debug_max_upgrades", "jg_debug_lifetime_check", "jg_debug_fail_verify", "jg_debug_tables_built"]
+           "jg_debug_max_upgrades", "jg_debug_lifetime_check", "jg_debug_fail_verify", "jg_debug_tables_built",
+           "jg_debug_small_path"]
 
 
 class JgKey(ctypes.Structure):
@@ -88,6 +89,7 @@ def lib():
                                               ctypes.POINTER(ctypes.c_uint64)]
         L.jg_debug_table_digest.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         L.jg_debug_tables_built.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64)]
+        L.jg_debug_small_path.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         L.jg_version.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -225,6 +227,15 @@ class Context:
         """jg_debug_max_upgrades: the background upgrader widens at most n more tables (-1 = no limit)."""
         if lib().jg_debug_max_upgrades(self.h, int(n)) != 0:
             raise JgError("jg_debug_max_upgrades failed")
+
+    def debug_small_path(self, enable=None):
+        """jg_debug_small_path: small ECDSA submissions as one launch per curve (True, the
+        default) or through the batch chain (False; None leaves it); returns the
+        number of one-launch verifications enqueued so far.  Verdicts are identical."""
+        v = ctypes.c_uint64()
+        if lib().jg_debug_small_path(self.h, -1 if enable is None else (1 if enable else 0), ctypes.byref(v)) != 0:
+            raise JgError("jg_debug_small_path failed")
+        return v.value
 
     def debug_fail_alloc(self, n):
         """jg_debug_fail_alloc: the n-th device allocation of later key loads fails (0 = off)."""

@@ -620,6 +620,8 @@ struct Item {                     // one device's share of a submission
   std::vector<size_t> cuts;       // chunk boundaries (chunk_cuts)
   bool grouped = false;           // mixed classes: chunks run class-grouped (plan_chunk / issue_chunk)
   bool zc = false;                // class-major zero-copy plans (zc_enabled): no arena copy
+  bool small_ec = true;           // small ECDSA chunks as one launch per (curve, key width) (issue_small_ec)
+  std::atomic<uint64_t>* small_launches = nullptr;   // the context's count of them
 };
 
 // A thread that runs one job at a time for its owner (the device worker's
@@ -740,6 +742,8 @@ struct jg_ctx {
   std::atomic<int> fail_alloc{0};            // jg_debug_fail_alloc countdown
   std::atomic<uint64_t> tables_built{0};     // comb-table builds launched by this context (jg_debug_tables_built)
   std::atomic<uint64_t> small_rr{0};         // device slot of the next small submission (submit_to)
+  std::atomic<bool> small_ec{true};          // one-launch ECDSA small chunks (jg_debug_small_path)
+  std::atomic<uint64_t> small_launches{0};   // k_ec_small launches enqueued (jg_debug_small_path)
   // jg_debug_fail_verify: countdown to an injected device failure of a
   // submission; once it fires the context is `poisoned` (every later
   // submission fails, as after a sticky HIP error) until it is destroyed
@@ -1694,6 +1698,69 @@ void plan_chunk(Slot& S, const Item& it, const jg_tok* toks, size_t n, size_t jo
   if (pipe_trace()) S.host_ms[1] = ms_since(t_start);
 }
 
+// A small chunk whose jobs are all ECDSA (or rejected) -- coalesced
+// single-token calls -- runs as ONE launch per (curve, key-table width):
+// k_ec_small (kernels/ec_small.hpp) reads the jobs from its arguments and the
+// arena in place (pinned host memory: the caller's, or the slot's staging)
+// and writes each verdict byte straight to the slot's pinned verdicts.  No
+// arena DMA, plan fill, prep / scalar / point / exact / scatter chain: the
+// batch chain paid ~9 dependent launches and ~40 us of launch gaps for a lone
+// token (profiles/r06_s9/small_chain).  Rejected jobs (alg / key mismatch, an
+// invalid key) get verdict 0 here.  Returns false, having enqueued nothing,
+// when the chunk does not qualify: another class, a signing input over
+// EC_SMALL_IN_MAX bytes, an arena without a device view, a key whose comb
+// table is not in place.
+bool issue_small_ec(Device* d, Slot& S, const Item& it, const ChunkPlan& CP, const KeyState& K, const DevGen& G,
+                    hipStream_t s) {
+  const size_t n = CP.n;
+  if (!it.small_ec || n == 0 || n > (size_t)EC_SMALL_MAX || CP.zc || !CP.src) return false;
+  const size_t NB = K.keys.size() + 1;
+  const jg_tok* ht = (const jg_tok*)((const uint8_t*)S.h_meta.p + PlanBlock(NB, n).toks_off);
+  int cls[EC_SMALL_MAX];
+  for (size_t i = 0; i < n; ++i) {
+    const int c = classify(K, ht[i]);
+    cls[i] = c;
+    if (c == CLS_REJECT) continue;
+    if (c < CLS_P256 || c > CLS_P521 || ht[i].sig_in_len > EC_SMALL_IN_MAX || !d->gtab[c]) return false;
+    const int32_t k = ht[i].key_idx;
+    const DevKey& rec = G.mirror[(size_t)k];
+    if (G.kw[(size_t)k] == 0 || rec.tab == 0 || rec.tab_w != G.kw[(size_t)k]) return false;
+  }
+  // the arena's device view: the caller's page-locked arena, or the staging copy
+  const uint8_t* dsrc = nullptr;
+  if (CP.src == (const uint8_t*)S.h_arena.p) dsrc = (const uint8_t*)S.h_arena.dp;
+  else if (it.dev_arena && CP.src >= it.arena && CP.src < it.arena + it.arena_len) dsrc = it.dev_arena + (CP.src - it.arena);
+  if (!dsrc) return false;
+  uint8_t* vh = (uint8_t*)S.h_verdict.get(n);
+  std::memset(vh, 0, n);
+  uint8_t* vd = (uint8_t*)S.h_verdict.dp;
+  bool done[EC_SMALL_MAX] = {};
+  for (size_t i = 0; i < n; ++i) {
+    if (done[i] || cls[i] == CLS_REJECT) continue;
+    const int c = cls[i], w = G.kw[ht[i].key_idx];
+    EcSmallArgs A{};
+    A.arena = dsrc;
+    A.keys = G.keys();
+    A.keyblob = G.keyblob();
+    A.gtab = d->gtab[c];
+    A.verdict = vd;
+    for (size_t j = i; j < n; ++j) {
+      if (done[j] || cls[j] != c || G.kw[ht[j].key_idx] != w) continue;
+      const jg_tok& t = ht[j];
+      const uint64_t o = t.off - CP.dbase;
+      A.jobs[A.n] = JobDev{(uint32_t)o, t.sig_in_len, (uint32_t)(o + t.sig_rel_off),
+                           job_pack(t.key_idx, t.alg, t.sig_b64_len)};
+      A.out[A.n] = (uint16_t)j;
+      ++A.n;
+      done[j] = true;
+    }
+    launch_ec_small(c, w, A, s);
+    if (it.small_launches) it.small_launches->fetch_add(1, std::memory_order_relaxed);
+  }
+  G.uses.record(s, "small ec");
+  return true;
+}
+
 // The device half of a chunk planned by plan_chunk: arena DMA, plan fill,
 // the class launches and the verdict copy (device worker thread only).
 void issue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const ChunkPlan& CP, uint8_t* out) {
@@ -1743,6 +1810,15 @@ void issue_chunk(Device* d, size_t dslot, Slot& S, const Item& it, const ChunkPl
   // which issues them, is what bounds small-batch throughput
   // (profiles/r06_s6/single_probe.log).  (Traced runs keep the copy stream.)
   const bool small = !grouped && n <= SMALL_SUBMIT && !tr;
+  if (!tr && issue_small_ec(d, S, it, CP, K, G, s)) {
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(S.done, s));
+    S.ticket = it.t;
+    S.ks = it.ks;
+    S.out = out;
+    S.n = n;
+    return;
+  }
   if (tr) HIPCHK(hipEventRecord(S.tr_a, cs));
   if (bytes && !zc) HIPCHK(hipMemcpyAsync(S.bufs.arena.p, src, bytes, hipMemcpyHostToDevice, small ? s : cs));
   // grouped chunks: the whole plan block goes over by DMA behind the arena
@@ -2636,6 +2712,8 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
     it.dev_arena = dview;
     it.chunk = C;
     it.grouped = mixed_classes(*ks, toks + it.lo, it.hi - it.lo);
+    it.small_ec = ctx->small_ec.load();
+    it.small_launches = &ctx->small_launches;
     // grouped chunks serialise each class group's launches on one lane, so a
     // long ramp of small chunks would queue latency-bound launches (an
     // RSA-4096 modexp takes ~1.5 ms at any size): start at C / 4
@@ -2896,6 +2974,13 @@ int jg_debug_table_digest(jg_ctx* ctx, int key, uint64_t* digest) {
 int jg_debug_tables_built(jg_ctx* ctx, uint64_t* built) {
   if (!ctx || !built) return -1;
   *built = ctx->tables_built.load();
+  return 0;
+}
+
+int jg_debug_small_path(jg_ctx* ctx, int enable, uint64_t* launches) {
+  if (!ctx || enable < -1 || enable > 1) return -1;
+  if (enable >= 0) ctx->small_ec.store(enable != 0);
+  if (launches) *launches = ctx->small_launches.load();
   return 0;
 }
 

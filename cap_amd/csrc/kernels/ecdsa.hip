@@ -22,6 +22,9 @@ void launch_ec_keytables_p521(int wq, DevKey* keys, uint32_t* blob, const int32_
 void launch_ec_gtable_p256(uint32_t* tab, hipStream_t s);
 void launch_ec_gtable_p384(uint32_t* tab, hipStream_t s);
 void launch_ec_gtable_p521(uint32_t* tab, hipStream_t s);
+void launch_ec_small_p256(const EcSmallArgs& a, int wq, hipStream_t s);
+void launch_ec_small_p384(const EcSmallArgs& a, int wq, hipStream_t s);
+void launch_ec_small_p521(const EcSmallArgs& a, int wq, hipStream_t s);
 
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const Marker& mk) {
   if (a.end <= a.begin) return;
@@ -59,6 +62,16 @@ void launch_ec_gtable(int cls, uint32_t* tab, hipStream_t s) {
     case CLS_P256: launch_ec_gtable_p256(tab, s); break;
     case CLS_P384: launch_ec_gtable_p384(tab, s); break;
     case CLS_P521: launch_ec_gtable_p521(tab, s); break;
+    default: break;
+  }
+}
+
+void launch_ec_small(int cls, int wq, const EcSmallArgs& a, hipStream_t s) {
+  if (a.n == 0) return;
+  switch (cls) {
+    case CLS_P256: launch_ec_small_p256(a, wq, s); break;
+    case CLS_P384: launch_ec_small_p384(a, wq, s); break;
+    case CLS_P521: launch_ec_small_p521(a, wq, s); break;
     default: break;
   }
 }

@@ -108,6 +108,27 @@ static_assert(ec_top_window_ok(jgk::CLS_P256, 26) && ec_top_window_ok(jgk::CLS_P
               ec_top_window_ok(jgk::CLS_P521, 16), "comb window count leaves no room for the top carry");
 
 void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);
+
+// One-launch verification of a small batch (ec_small.hpp): one two-wave block
+// per token runs the whole chain -- signing input and signature read straight
+// from the (pinned host or device) arena, hash, scalar stage, comb sum, x(R)
+// check -- and writes the verdict byte to verdict[out[i]] (pinned host memory).
+// The jobs travel in the kernel arguments.  Every token of a launch has a key
+// of class `cls` whose comb table has width `wq`, a signing input of at most
+// EC_SMALL_IN_MAX bytes, and its alg in the key's family (the host plan).
+constexpr int EC_SMALL_MAX = 64;            // tokens per launch
+constexpr uint32_t EC_SMALL_IN_MAX = 8192;  // signing-input bytes staged in LDS
+struct EcSmallArgs {
+  const uint8_t* arena;                     // JobDev offsets are relative to it
+  const jgk::DevKey* keys;
+  const uint32_t* keyblob;
+  const uint32_t* gtab;
+  uint8_t* verdict;
+  uint32_t n;
+  jgk::JobDev jobs[EC_SMALL_MAX];
+  uint16_t out[EC_SMALL_MAX];
+};
+void launch_ec_small(int cls, int wq, const EcSmallArgs& a, hipStream_t s);
 // key staging: validate each listed key (plain 28-bit limbs x,y at aux_off:
 // coordinates < p, on the curve) and write its Montgomery affine coordinates
 // back to aux_off

@@ -790,25 +790,15 @@ __device__ void affine_point(JPt<typename CV::Fp>& P, const uint32_t* xm, const 
   P.inf = false;
 }
 
+// x(u1 G + u2 Q) mod n == r by double-and-add with complete case handling
+// (the exceptional tokens of the fast sums; Q's affine Montgomery coordinates
+// at aux; u1, u2, r canonical plain limbs)
 template <class CV>
-__global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
+__device__ bool ec_exact_ok(const uint32_t* aux, const uint32_t* r, const uint32_t* u1, const uint32_t* u2) {
   using Fp = typename CV::Fp;
   using Fn = typename CV::Fn;
   constexpr int L = Fp::L;
-  const uint32_t cnt = *a.exc_count;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
-    const int64_t p = a.exc_list[i];
-    const int kidx = job_key(a.jobs[p]);
-    const uint32_t* aux = a.keyblob + a.keys[kidx].aux_off;
-    // u1 = e / s, u2 = r / s (mod n), recomputed with one inversion per token
-    // (the status goes back to OK first: ec_scalar_inputs checks it)
-    a.status[p] = ST_OK;
-    uint32_t r[L], s[L], e[L], sm[L], w[L], u1[L], u2[L];
-    (void)ec_scalar_inputs<CV>(a, p, r, s, e);
-    mp::to_mont<Fn>(sm, s);
-    mp::inv<Fn>(w, sm);                          // s^-1 R
-    mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
-    mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
+  {
     JPt<Fp> G, Q, GQ, R;
     uint32_t gx[L], gy[L];
     mp::set_const<Fp>(gx, CV::C::GX_M); mp::set_const<Fp>(gy, CV::C::GY_M);
@@ -849,7 +839,29 @@ __global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
       for (int j = 0; j < L; ++j) o |= x[j] ^ r[j];
       ok = o == 0;
     }
-    a.verdict_pad[p] = ok;
+    return ok;
+  }
+}
+
+template <class CV>
+__global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
+  using Fn = typename CV::Fn;
+  constexpr int L = Fn::L;
+  const uint32_t cnt = *a.exc_count;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    const int64_t p = a.exc_list[i];
+    const int kidx = job_key(a.jobs[p]);
+    const uint32_t* aux = a.keyblob + a.keys[kidx].aux_off;
+    // u1 = e / s, u2 = r / s (mod n), recomputed with one inversion per token
+    // (the status goes back to OK first: ec_scalar_inputs checks it)
+    a.status[p] = ST_OK;
+    uint32_t r[L], s[L], e[L], sm[L], w[L], u1[L], u2[L];
+    (void)ec_scalar_inputs<CV>(a, p, r, s, e);
+    mp::to_mont<Fn>(sm, s);
+    mp::inv<Fn>(w, sm);                          // s^-1 R
+    mp::mul<Fn>(u1, e, w); mp::csub<Fn>(u1);
+    mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);
+    a.verdict_pad[p] = ec_exact_ok<CV>(aux, r, u1, u2);
     a.status[p] = ST_OK;
   }
 }

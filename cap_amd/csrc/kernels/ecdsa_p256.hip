@@ -1,6 +1,7 @@
 // ecdsa_p256.hip -- the P256 instantiations of ecdsa_impl.hpp: the verify
 // chain, key staging and generator table for every key-table width.
 #include "ecdsa_impl.hpp"
+#include "ec_small.hpp"
 
 void launch_ec_p256(const EcArgs& a, hipStream_t s, const Marker& mk) {
   if (a.wq == 26) launch_chain<CurveP256W<26>>(a, s, mk);
@@ -22,3 +23,10 @@ void launch_ec_keytables_p256(int wq, DevKey* keys, uint32_t* blob, const int32_
 }
 
 void launch_ec_gtable_p256(uint32_t* tab, hipStream_t s) { gtable_chain<CurveP256W<20>>(tab, s); }
+
+void launch_ec_small_p256(const EcSmallArgs& a, int wq, hipStream_t s) {
+  if (wq == 26) small_launch<CurveP256W<26>>(a, s);
+  else if (wq == 24) small_launch<CurveP256W<24>>(a, s);
+  else if (wq == 22) small_launch<CurveP256W<22>>(a, s);
+  else small_launch<CurveP256W<20>>(a, s);
+}

@@ -1,6 +1,7 @@
 // ecdsa_p384.hip -- the P384 instantiations of ecdsa_impl.hpp: the verify
 // chain, key staging and generator table for every key-table width.
 #include "ecdsa_impl.hpp"
+#include "ec_small.hpp"
 
 void launch_ec_p384(const EcArgs& a, hipStream_t s, const Marker& mk) {
   if (a.wq == 24) launch_chain<CurveP384W<24>>(a, s, mk);
@@ -22,3 +23,10 @@ void launch_ec_keytables_p384(int wq, DevKey* keys, uint32_t* blob, const int32_
 }
 
 void launch_ec_gtable_p384(uint32_t* tab, hipStream_t s) { gtable_chain<CurveP384W<16>>(tab, s); }
+
+void launch_ec_small_p384(const EcSmallArgs& a, int wq, hipStream_t s) {
+  if (wq == 24) small_launch<CurveP384W<24>>(a, s);
+  else if (wq == 20) small_launch<CurveP384W<20>>(a, s);
+  else if (wq == 18) small_launch<CurveP384W<18>>(a, s);
+  else small_launch<CurveP384W<16>>(a, s);
+}

@@ -931,6 +931,100 @@ MPD void inv_plain(uint32_t* r, const uint32_t* a) {
   sg_normalize<F>(r, d, f[L - 1]);
 }
 
+// ---- variable-time safegcd (public inputs only) -----------------------------
+// Wuille's var-time divsteps (original divstep, eta = -delta): the trailing
+// zeros of g go in one step, and each odd step cancels up to 6 (after a swap)
+// or 4 low bits of g with one multiple of f.  A 28-divstep batch produces the
+// same transition matrix meaning as sg_divsteps28 (f 2^28 = u f0 + v g0,
+// g 2^28 = q f0 + r g0), so sg_update_fg / sg_update_de apply unchanged; the
+// loop stops once g == 0.  For 256-bit moduli that is ~19.4 batches of ~7
+// odd steps each instead of 22 batches of 28 masked steps (tools/safegcd_var_sim.py).
+// Used where the value is public and one lane works alone (the one-launch
+// small-batch path: a signature's s), so its branches cost nothing.
+MPD int32_t sg_divsteps28_var(int32_t eta, uint32_t f, uint32_t g, int32_t* t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  int i = 28;
+  for (;;) {
+    const int zeros = (int)__builtin_ctz(g | (0xffffffffu << i));   // the sentinel stops at i
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    uint32_t w;
+    if (eta < 0) {
+      eta = -eta;
+      uint32_t x = f;
+      f = g; g = 0u - x;
+      x = u; u = q; q = 0u - x;
+      x = v; v = r; r = 0u - x;
+      const int limit = eta + 1 < i ? eta + 1 : i;
+      const uint32_t m = (0xffffffffu >> (32 - limit)) & 63u;
+      w = (f * g * (f * f - 2u)) & m;                 // g + w f == 0 mod 2^min(limit, 6)
+    } else {
+      const int limit = eta + 1 < i ? eta + 1 : i;
+      const uint32_t m = (0xffffffffu >> (32 - limit)) & 15u;
+      w = f + (((f + 1u) & 4u) << 1);                 // -f^-1 mod 16
+      w = (0u - w * g) & m;
+    }
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t[0] = (int32_t)u;
+  t[1] = (int32_t)v;
+  t[2] = (int32_t)q;
+  t[3] = (int32_t)r;
+  return eta;
+}
+
+// A value the compiler must treat as per-lane (divergent): code that runs on
+// one active lane with inputs it can prove wave-uniform (LDS reads at uniform
+// addresses, constants) is otherwise scalarised -- 64-bit products as 4-5
+// SALU instructions each, VALU-only ops (v_alignbit) bracketed by
+// v_readfirstlane -- measured 2-3x slower than the same code on VGPRs.
+MPD uint32_t lane_value(uint32_t v) {
+  uint32_t r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// plain canonical a in [1, m) -> a^-1 mod m, variable time (a is public).
+// For ONE active lane: the divsteps run on the wave-uniform copies of f[0],
+// g[0] (readfirstlane), so they are scalar code -- SGPRs, s_ff1 for the
+// trailing zeros, branches on SCC -- and the matrix reaches the limb updates
+// as SGPR operands; with several active lanes every lane would get the first
+// one's inverse.
+template <class F>
+MPD void inv_plain_var(uint32_t* r, const uint32_t* a) {
+  constexpr int L = F::L;
+  int32_t d[L], e[L], f[L], g[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {     // the limbs on VGPRs, the divsteps scalar
+    d[i] = (int32_t)lane_value(0u);
+    e[i] = (int32_t)lane_value(i == 0 ? 1u : 0u);
+    f[i] = (int32_t)lane_value(F::M[i]);
+    g[i] = (int32_t)lane_value(a[i]);
+  }
+  int32_t eta = -1;
+  // every input reaches g == 0 well inside the constant-time bound; the cap
+  // only guarantees that the loop ends
+#pragma unroll 1
+  for (int b = 0; b < 2 * Sg<F>::BATCHES; ++b) {
+    int32_t t[4];
+    eta = sg_divsteps28_var(eta, __builtin_amdgcn_readfirstlane((uint32_t)f[0]),
+                            __builtin_amdgcn_readfirstlane((uint32_t)g[0]), t);
+    sg_update_de<F>(d, e, t);
+    sg_update_fg<L>(f, g, t);
+    int32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) o |= g[i];
+    if (__builtin_amdgcn_readfirstlane(o) == 0) break;
+  }
+  sg_normalize<F>(r, d, f[L - 1]);
+}
+
 // inverse in Montgomery form: x = aR  ->  a^-1 R  (lazy input accepted)
 template <class F>
 MPD void inv(uint32_t* r, const uint32_t* x) {

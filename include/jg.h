@@ -116,6 +116,15 @@ int jg_keys_wait_tables(jg_ctx* ctx);
  * RSA and invalid keys): widths[0..min(n, cap)).  Returns n, the key count. */
 int jg_keys_table_widths(jg_ctx* ctx, int* widths, int cap);
 
+/* Test / A-B hook: small submissions (at most 64 jobs, every job ECDSA or
+ * rejected) run as one launch per (curve, key-table width) that does the whole
+ * verification per token -- enable 1: on (the default), 0: off (they take the
+ * batch chain: arena DMA, plan fill, prep, scalar, point, exact, scatter),
+ * -1: unchanged.  Verdicts are identical either way.  Applies to later
+ * submissions.  *launches (may be NULL) receives the number of such one-launch
+ * verifications this context has enqueued.  Returns 0 or -1. */
+int jg_debug_small_path(jg_ctx* ctx, int enable, uint64_t* launches);
+
 /* Test hook: the n-th device allocation of later key loads (counting from 1)
  * fails as if hipMalloc ran out of memory; 0 disables.  Returns 0 or -1. */
 int jg_debug_fail_alloc(jg_ctx* ctx, int n);

@@ -1,0 +1,199 @@
+"""The one-launch small-batch ECDSA path (kernels/ec_small.hpp k_ec_small,
+jg_runtime.cpp issue_small_ec): coalesced single-token calls behind
+/root/reference/jwt/keyset.go:27-32 (VerifySignature) and jwt/jwt.go:95-97
+(Validate) reach jg_verify_batch as batches of a few tokens, which run as one
+launch per (curve, key-table width) instead of the batch chain.
+
+Every verdict must equal the fixture's (the Go rule) and the C oracle's, and
+the batch chain's on the same tokens (jg_debug_small_path off): the golden
+ECDSA tokens (ES256 / ES384 / ES512 on P-256, P-384 and P-521 keys, tampered,
+wrong-key, alg/curve mismatches, malformed signatures) one at a time and in
+small batches; every comb-tier token of every EC width tier; the exceptional
+tokens of ec_edge.json (the complete double-and-add inside the same launch);
+a signing input past the LDS stage (falls back to the chain); mixed RSA + EC
+batches (fall back); a caller arena in pinned memory read in place."""
+import ctypes
+import json
+import os
+
+import pytest
+
+from oracle import jws
+from tests import gpu_helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+def _verify_each(ctx, arena_toks, kid_index, per_call):
+    """verdicts of `arena_toks` (fixture tokens) verified `per_call` at a time"""
+    out = []
+    for i in range(0, len(arena_toks), per_call):
+        arena, slots = H.jobs_from_tokens(arena_toks[i:i + per_call], kid_index)
+        got = ctx.verify(arena) if arena.toks else b""
+        out += [0 if s is None else got[s] for s in slots]
+    return out
+
+
+def _golden_ec():
+    keys, toks = H.golden()
+    ec = {k["kid"] for k in keys if k["kty"] == "EC"}
+    return keys, [t for t in toks if t["key"] in ec]
+
+
+def test_golden_ec_tokens_small_path_equals_chain_and_oracle():
+    from cap_amd import _lib
+    keys, toks = _golden_ec()
+    assert len(toks) >= 60 and sum(t["verdict"] for t in toks) >= 20
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    okeys = {k["kid"]: jws.Key.from_fixture(k) for k in keys}
+    want = []
+    for t in toks:
+        p = jws.parse_jws(t["token"])
+        w = int(jws.verify_sig(p, okeys[t["key"]])) if p is not None and p.crit_ok else 0
+        assert w == t["verdict"], t["name"]
+        want.append(w)
+    ctx = _lib.Context()
+    try:
+        ctx.load_keys([H.abi_key(k) for k in keys])
+        n0 = ctx.debug_small_path()
+        lone = _verify_each(ctx, toks, kid_index, 1)
+        n1 = ctx.debug_small_path()
+        few = _verify_each(ctx, toks, kid_index, 7)
+        full = _verify_each(ctx, toks, kid_index, 64)
+        n2 = ctx.debug_small_path()
+        # one launch per lone token that is ECDSA on its key (others are rejected on the host)
+        es = sum(1 for t in toks if (lambda p: p is not None and p.crit_ok and p.alg in ("ES256", "ES384", "ES512"))(
+            jws.parse_jws(t["token"])))
+        assert n1 - n0 == es
+        assert n2 > n1
+        ctx.debug_small_path(False)
+        chain = _verify_each(ctx, toks, kid_index, 7)
+        assert ctx.debug_small_path(True) == n2          # no one-launch verification while off
+        bad = [t["name"] for t, a, b, c, d, w in zip(toks, lone, few, full, chain, want) if not a == b == c == d == w]
+        assert not bad, bad
+    finally:
+        ctx.close()
+
+
+def _ec_tiers():
+    d = json.load(open(os.path.join(H.ROOT, "tests", "golden", "comb_tiers.json")))
+    return [(s["crv"], s["wq"]) for s in d["ec"]]
+
+
+@pytest.mark.parametrize("crv,wq", _ec_tiers())
+def test_comb_tier_tokens_small_path(crv, wq):
+    """Digit patterns at the table edges for this width: k_ec_small<width>
+    reads the same comb entries as the batch kernels."""
+    import bench
+    from cap_amd import _lib
+    d = json.load(open(os.path.join(H.ROOT, "tests", "golden", "comb_tiers.json")))
+    s = next(x for x in d["ec"] if x["crv"] == crv and x["wq"] == wq)
+    tab = {"P-256": "p256", "P-384": "p384", "P-521": "p521"}[crv]
+    keys = s["keys"]
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    ctx = _lib.Context()
+    try:
+        ctx.set_table_budget(len(keys) * bench.table_bytes(tab, wq))
+        ctx.load_keys([H.abi_key(k) for k in keys])
+        assert ctx.table_widths() == [wq] * len(keys)
+        n0 = ctx.debug_small_path()
+        lone = _verify_each(ctx, s["tokens"], kid_index, 1)
+        batch = _verify_each(ctx, s["tokens"], kid_index, 64)
+        assert ctx.debug_small_path() - n0 >= len(s["tokens"])
+        want = [t["verdict"] for t in s["tokens"]]
+        assert lone == want and batch == want, [t["name"] for t, a, b in zip(s["tokens"], lone, batch)
+                                               if not a == b == t["verdict"]]
+    finally:
+        ctx.close()
+
+
+def test_exceptional_tokens_small_path():
+    """Comb sums that meet P == +-Q: the lane partials flag the exception and
+    the block runs the complete double-and-add itself (ec_exact_ok)."""
+    from cap_amd import _lib
+    d = json.load(open(os.path.join(H.ROOT, "tests", "golden", "ec_edge.json")))
+    kid_index = {k["kid"]: i for i, k in enumerate(d["keys"])}
+    toks = d["tokens"]
+    assert any(t.get("exceptional") and t["verdict"] == 1 for t in toks)
+    ctx = _lib.Context()
+    try:
+        ctx.set_table_budget(0)                     # the crafted exceptions are for 26/20 combs
+        ctx.load_keys([H.abi_key(k) for k in d["keys"]])
+        lone = _verify_each(ctx, toks, kid_index, 1)
+        ctx.debug_small_path(False)
+        chain = _verify_each(ctx, toks, kid_index, 1)
+        want = [t["verdict"] for t in toks]
+        assert lone == want, [t["name"] for t, a in zip(toks, lone) if a != t["verdict"]]
+        assert chain == want
+    finally:
+        ctx.close()
+
+
+def test_long_signing_input_and_mixed_batches_fall_back():
+    """A signing input past EC_SMALL_IN_MAX (8 KiB) and a batch with RSA jobs
+    take the batch chain; verdicts stay exact."""
+    import bench
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    os.environ["TOKGEN_PAD"] = "9000"
+    try:
+        longt = bench.gen_tokens("ES256", 3, bench.golden_keypaths(["p256-a"]), 1, "smallpad")
+    finally:
+        del os.environ["TOKGEN_PAD"]
+    assert all(len(t) > 9000 for t in longt)
+    ctx = _lib.Context()
+    try:
+        ctx.load_keys([H.abi_key(k) for k in keys])
+        arena = _lib.Arena()
+        for i, t in enumerate(longt):
+            si, sig = t[:t.rfind(b".")], t[t.rfind(b".") + 1:]
+            if i == 2:
+                sig = sig[:-2] + (b"A" if sig[-2:-1] != b"A" else b"B") + sig[-1:]
+            arena.add(si, sig, "ES256", kid_index["p256-a"])
+        n0 = ctx.debug_small_path()
+        assert list(ctx.verify(arena)) == [1, 1, 0]
+        assert ctx.debug_small_path() == n0
+        # RSA + ECDSA in one small batch: the chain, exact verdicts
+        rs = [t for t in toks if t["alg"] == "RS256"][:3]
+        es = [t for t in toks if t["alg"] == "ES256"][:3]
+        mix = rs + es
+        arena, slots = H.jobs_from_tokens(mix, kid_index)
+        got = ctx.verify(arena)
+        assert [0 if s is None else got[s] for s in slots] == [t["verdict"] for t in mix]
+        assert ctx.debug_small_path() == n0
+    finally:
+        ctx.close()
+
+
+def test_pinned_caller_arena_read_in_place():
+    """An arena in jg_host_alloc memory at an odd offset: the kernel reads the
+    caller's bytes over PCIe (no staging copy); unaligned starts included."""
+    from cap_amd import _lib
+    keys, toks = _golden_ec()
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    sel = [t for t in toks if t["alg"] in ("ES256", "ES384", "ES512")][:24]
+    arena, slots = H.jobs_from_tokens(sel, kid_index)
+    ctx = _lib.Context()
+    L = _lib.lib()
+    try:
+        ctx.load_keys([H.abi_key(k) for k in keys])
+        for lead in (0, 1, 3):
+            buf = bytes(lead) + bytes(arena.buf)
+            pa = _lib.PinnedBuffer(len(buf))
+            ctypes.memmove(pa.ptr + 0, buf, len(buf))
+            arr = arena.tok_array()
+            for i in range(len(arena.toks)):
+                arr[i].off += lead
+            out = (ctypes.c_uint8 * len(arena.toks))()
+            n0 = ctx.debug_small_path()
+            for i in range(len(arena.toks)):       # one token per call, as the coalescer sends a lone call
+                one = (_lib.JgTok * 1)(arr[i])
+                v = (ctypes.c_uint8 * 1)()
+                assert L.jg_verify_batch(ctx.h, pa.ptr, len(buf), one, 1, v) == 0, ctx.error()
+                out[i] = v[0]
+            assert ctx.debug_small_path() - n0 == len(arena.toks)
+            pa.free()
+            assert [0 if s is None else out[s] for s in slots] == [t["verdict"] for t in sel], lead
+    finally:
+        ctx.close()

@@ -2,7 +2,8 @@
 device round trip): ES256 tokens of the 4 bench kids, batch sizes 1 ... 4096,
 pinned host arena, p50 / p90 of many calls per size; optionally several
 threads submitting concurrently (pipelining on the device worker).
-usage: python tools/small_batch_probe.py [out.json] [threads] [ES256|EdDSA]"""
+usage: python tools/small_batch_probe.py [out.json] [threads] [ES256|EdDSA]
+(SBP_SIZES=1,64 picks the batch sizes)"""
 import ctypes
 import json
 import os
@@ -32,7 +33,8 @@ def main():
     pa = _lib.PinnedBuffer(len(arena))
     ctypes.memmove(pa.ptr, arena, len(arena))
     res = {"threads": nthr, "sizes": {}}
-    for n in (1, 8, 64, 256, 1024, 4096):
+    sizes = [int(x) for x in os.environ.get("SBP_SIZES", "1,8,64,256,1024,4096").split(",")]
+    for n in sizes:
         reps = 400 if n <= 256 else 100
         lat = [[] for _ in range(nthr)]
 

@@ -61,14 +61,28 @@ static int es_size(const char* alg) {
 
 static void* worker(void* arg) {
   job* j = (job*)arg;
-  char hdr[256], pay[512], hb[512], pb[1024], sb[1500];
+  /* TOKGEN_PAD=n: a "pad" claim of n 'x' bytes (long signing inputs) */
+  const char* pe = getenv("TOKGEN_PAD");
+  const size_t padn = pe ? (size_t)atol(pe) : 0;
+  char hdr[256], hb[512], sb[1500];
+  char* pay = malloc(512 + padn);
+  char* pb = malloc(2 * (512 + padn) + 8);
+  char* padv = malloc(padn + 1);
+  memset(padv, 'x', padn);
+  padv[padn] = 0;
   unsigned char sig[1024], raw[200];
   for (long i = j->lo; i < j->hi; ++i) {
     const int k = (int)(i % j->nkeys);
     snprintf(hdr, sizeof hdr, "{\"alg\":\"%s\",\"kid\":\"kid-%02d\",\"typ\":\"JWT\"}", j->alg, j->kid_base + k);
-    snprintf(pay, sizeof pay,
-             "{\"aud\":[\"www.example.com\"],\"exp\":1611699944,\"iat\":1611699344,"
-             "\"iss\":\"https://example.com/\",\"jti\":\"%ld\",\"nbf\":1611699344,\"sub\":\"alice@example.com\"}", i);
+    if (padn)
+      snprintf(pay, 512 + padn,
+               "{\"aud\":[\"www.example.com\"],\"exp\":1611699944,\"iat\":1611699344,"
+               "\"iss\":\"https://example.com/\",\"jti\":\"%ld\",\"nbf\":1611699344,\"pad\":\"%s\","
+               "\"sub\":\"alice@example.com\"}", i, padv);
+    else
+      snprintf(pay, 512,
+               "{\"aud\":[\"www.example.com\"],\"exp\":1611699944,\"iat\":1611699344,"
+               "\"iss\":\"https://example.com/\",\"jti\":\"%ld\",\"nbf\":1611699344,\"sub\":\"alice@example.com\"}", i);
     size_t hl = b64url((const unsigned char*)hdr, strlen(hdr), hb);
     size_t pl = b64url((const unsigned char*)pay, strlen(pay), pb);
     char* si = malloc(hl + pl + 2);
@@ -105,6 +119,9 @@ static void* worker(void* arg) {
     free(si);
     j->out[i] = tok;
   }
+  free(pay);
+  free(pb);
+  free(padv);
   return NULL;
 }
 
