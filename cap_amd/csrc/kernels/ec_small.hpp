@@ -29,7 +29,7 @@
 namespace {
 
 constexpr int SM_THREADS = 128;
-constexpr int SM_SPLIT = 8;                                       // point lanes per token
+constexpr int SM_SPLIT = 16;                                      // point lanes per token
 constexpr uint32_t SM_IN_DW = EC_SMALL_IN_MAX / 4 + 72;           // staged signing input + SHA padding blocks
 constexpr uint32_t SM_SIG_CHARS = 176;                            // ES512's 132 bytes; longer is rejected
 
@@ -99,6 +99,93 @@ __device__ bool ec_x_matches(const uint32_t* X, const uint32_t* Z, const uint32_
     }
   }
   return ok;
+}
+
+// One level of the cross-lane combine: lane a (bit `off` clear, "lo") and lane
+// a ^ off ("hi") hold Jacobian partials P_lo, P_hi (normalized coordinates)
+// and split the products of P_lo + P_hi between them (jadd's arithmetic, same
+// operations, same bounds): each lane first brings the OTHER lane's Z into
+// its own U and S (lo: U1 = X1 Z2^2, S1 = Y1 Z2^3; hi: U2, S2), then
+// lo takes HH, HHH, V while hi takes r^2, Z1 Z2, Z3, and the last pair of
+// products (r (V - X3), S1 HHH) runs one per lane: 8 dependent products
+// instead of jadd's 16 on one lane.  The sum lands in lo; hi's copy is
+// garbage.  H == 0 (P_lo == +-P_hi: a doubling or an inverse pair) is not
+// handled here: both lanes set `exc` and the token takes the complete
+// double-and-add (ec_exact_ok).  Every lane of the wave must call it (shuffles).
+template <class CV>
+__device__ __forceinline__ void jadd_pair(JPt<typename CV::Fp>& P, int off, bool& exc) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  const bool lo = (threadIdx.x & off) == 0;
+  uint32_t oz[L], ox[L], oy[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    ox[j] = __shfl_xor(P.X[j], off);
+    oy[j] = __shfl_xor(P.Y[j], off);
+    oz[j] = __shfl_xor(P.Z[j], off);
+  }
+  const bool oinf = __shfl_xor((int)P.inf, off) != 0;
+  exc = exc || __shfl_xor((int)exc, off) != 0;
+  const bool both = !P.inf && !oinf && !exc;
+  // stage 1: own U, S against the other lane's Z
+  uint32_t zz[L], u[L], t[L], sv[L], uo[L], so[L];
+  mp::sqr<Fp>(zz, oz);
+  mp::mul<Fp>(u, P.X, zz);
+  mp::mul<Fp>(t, oz, zz);
+  mp::mul<Fp>(sv, P.Y, t);
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    uo[j] = __shfl_xor(u[j], off);
+    so[j] = __shfl_xor(sv[j], off);
+  }
+  uint32_t u1[L], s1[L], h[L], r[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    u1[j] = lo ? u[j] : uo[j];
+    s1[j] = lo ? sv[j] : so[j];
+    h[j] = lo ? uo[j] : u[j];            // U2
+    r[j] = lo ? so[j] : sv[j];           // S2
+  }
+  mp::sub<Fp>(h, h, u1); mp::freduce<Fp>(h);
+  mp::sub<Fp>(r, r, s1); mp::freduce<Fp>(r);
+  const bool hzero = is_zero_mod<Fp>(h);
+  // stage 2: lo HH, HHH, V | hi r^2, Z1 Z2, Z3
+  uint32_t a[L], b[L], p1[L], p2[L], p3[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) a[j] = lo ? h[j] : r[j];
+  mp::sqr<Fp>(p1, a);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { a[j] = lo ? h[j] : P.Z[j]; b[j] = lo ? p1[j] : oz[j]; }
+  mp::mul<Fp>(p2, a, b);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { a[j] = lo ? u1[j] : p2[j]; b[j] = lo ? p1[j] : h[j]; }
+  mp::mul<Fp>(p3, a, b);
+  uint32_t q1[L], q2[L], q3[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    q1[j] = __shfl_xor(p1[j], off);      // lo: r^2   hi: HH
+    q2[j] = __shfl_xor(p2[j], off);      // lo: Z1 Z2 hi: HHH
+    q3[j] = __shfl_xor(p3[j], off);      // lo: Z3    hi: V
+  }
+  // stage 3 (lo): X3 = r^2 - HHH - 2V; then lo r (V - X3) | hi S1 HHH
+  uint32_t x3[L], t2[L];
+  mp::add<Fp>(t, p2, p3); mp::add<Fp>(t, t, p3); mp::freduce<Fp>(t);
+  mp::sub<Fp>(x3, q1, t); mp::freduce<Fp>(x3);
+  mp::sub<Fp>(t2, p3, x3);
+#pragma unroll
+  for (int j = 0; j < L; ++j) { a[j] = lo ? r[j] : s1[j]; b[j] = lo ? t2[j] : q2[j]; }
+  uint32_t m[L], mo[L];
+  mp::mul<Fp>(m, a, b);
+#pragma unroll
+  for (int j = 0; j < L; ++j) mo[j] = __shfl_xor(m[j], off);
+  if (lo && both && !hzero) {
+    mp::sub<Fp>(m, m, mo); mp::freduce<Fp>(m);
+    mp::copy<Fp>(P.X, x3); mp::copy<Fp>(P.Y, m); mp::copy<Fp>(P.Z, q3);
+  } else if (lo && P.inf && !oinf) {     // an empty partial takes the other one
+    mp::copy<Fp>(P.X, ox); mp::copy<Fp>(P.Y, oy); mp::copy<Fp>(P.Z, oz);
+    P.inf = false;
+  }
+  if (both && hzero) exc = true;
 }
 
 // signed W-bit recoding of u into digits d[0..NWIN) (store_digit_rows, into LDS)
@@ -331,6 +418,8 @@ __global__ void __launch_bounds__(SM_THREADS) k_ec_small(EcSmallArgs a) {
   if (wave != 0) return;
   JPt<Fp> P;
   P.inf = true;
+#pragma unroll
+  for (int j = 0; j < L; ++j) { P.X[j] = 0; P.Y[j] = 0; P.Z[j] = 0; }
   bool exc = false;
   const int sub = lane;
   if (run && sub < S) {
@@ -357,6 +446,7 @@ __global__ void __launch_bounds__(SM_THREADS) k_ec_small(EcSmallArgs a) {
     };
     uint32_t xc[L], yc[L], xn[L], yn[L];
     int dc = fetch(0, xc, yc);
+    int nadd = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       int dn = 0;
@@ -368,9 +458,12 @@ __global__ void __launch_bounds__(SM_THREADS) k_ec_small(EcSmallArgs a) {
           mp::copy<Fp>(Y, yc); mp::freduce<Fp>(Y);
           mp::set_const<Fp>(Z, Fp::ONE);
           empty = false;
+        } else if (nadd == 1) {
+          madd_z1<Fp>(X, Y, Z, xc, yc);             // the accumulator is one entry (Z == 1)
         } else {
           madd<Fp>(X, Y, Z, xc, yc);
         }
+        ++nadd;
       }
       if (k + 1 < K) {
         mp::copy<Fp>(xc, xn);
@@ -386,19 +479,10 @@ __global__ void __launch_bounds__(SM_THREADS) k_ec_small(EcSmallArgs a) {
     }
   }
   SM_STAMP(6);
+  // lanes past S (and every lane of a token that does not run) carry empty
+  // partials through the pairwise levels
 #pragma unroll 1
-  for (int off = 1; off < S; off <<= 1) {
-    JPt<Fp> Q;
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-      Q.X[j] = __shfl_xor(P.X[j], off);
-      Q.Y[j] = __shfl_xor(P.Y[j], off);
-      Q.Z[j] = __shfl_xor(P.Z[j], off);
-    }
-    Q.inf = __shfl_xor((int)P.inf, off) != 0;
-    exc = exc || __shfl_xor((int)exc, off) != 0;
-    if (run && sub < S && (sub & off) == 0 && !exc) jadd<CV>(P, P, Q);
-  }
+  for (int off = 1; off < S; off <<= 1) jadd_pair<CV>(P, off, exc);
   if (lane != 0) return;
   SM_STAMP(7);
   bool ok = false;
