@@ -369,7 +369,7 @@ __global__ void __launch_bounds__(SM_THREADS) k_ec_small(EcSmallArgs a) {
     }
   }
   uint32_t w[L];                                   // s^-1 R (wave 1 lane 0)
-  if (wave == 1 && lane == 0) {
+  if (wave == 1 && lane < 4) {                     // four lanes: the inversion's limb rows (mp::inv_plain_var4)
     bool ok = size_ok && flag[0] == 0 && K.valid != 0 && (uint32_t)alg - 7u < 3u;
     uint32_t rw[CW], sw[CW], r[L], s[L], nl[L];
 #pragma unroll
@@ -378,14 +378,16 @@ __global__ void __launch_bounds__(SM_THREADS) k_ec_small(EcSmallArgs a) {
     mp::words_to_limbs<L, CW>(s, sw);
     mp::set_const<Fn>(nl, Fn::M);
     ok = ok && !zero_limbs<L>(r) && !zero_limbs<L>(s) && lt_limbs<L>(r, nl) && lt_limbs<L>(s, nl);
-    if (ok) {
+    if (ok) {                                      // the same on the four lanes
       uint32_t si[L], u2[L];
-      mp::inv_plain_var<Fn>(si, s);                 // s^-1 (plain)
-      mp::to_mont<Fn>(w, si);                       // s^-1 R
-      mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);      // r s^-1
+      mp::inv_plain_var4<Fn>(si, s);                // s^-1 (plain)
+      if (lane == 0) {
+        mp::to_mont<Fn>(w, si);                     // s^-1 R
+        mp::mul<Fn>(u2, r, w); mp::csub<Fn>(u2);    // r s^-1
 #pragma unroll
-      for (int j = 0; j < L; ++j) { sc[j] = r[j]; sc[2 * L + j] = u2[j]; }
-      flag[1] = 1;
+        for (int j = 0; j < L; ++j) { sc[j] = r[j]; sc[2 * L + j] = u2[j]; }
+        flag[1] = 1;
+      }
     }
   }
   SM_STAMP(3);

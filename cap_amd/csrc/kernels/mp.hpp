@@ -1025,6 +1025,68 @@ MPD void inv_plain_var(uint32_t* r, const uint32_t* a) {
   sg_normalize<F>(r, d, f[L - 1]);
 }
 
+// inv_plain_var with its four limb rows on four lanes: lanes 0..3 of the wave
+// (all four active, the same `a` on each) hold f, g, d, e's update rows --
+// lane 0 computes f' = (u f + v g) / 2^28, lane 1 g' = (q f + r g) / 2^28,
+// lane 2 d', lane 3 e' (with the Montgomery-style correction) -- each one
+// carry chain instead of four in a row, then the pairs swap rows so lanes
+// 0, 1 hold (f, g) and lanes 2, 3 hold (d, e) again.  The divsteps stay
+// scalar, on lane 0's f[0], g[0].  The inverse lands in every one of the four
+// lanes.
+template <class F>
+MPD void inv_plain_var4(uint32_t* r, const uint32_t* a) {
+  constexpr int L = F::L;
+  const int l = (int)(threadIdx.x & 3);
+  const bool de = l >= 2, second = (l & 1) != 0;
+  int32_t X[L], Y[L];                 // lanes 0, 1: (f, g); lanes 2, 3: (d, e)
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    X[i] = (int32_t)lane_value(de ? 0u : F::M[i]);
+    Y[i] = (int32_t)lane_value(de ? (i == 0 ? 1u : 0u) : a[i]);
+  }
+  int32_t eta = -1;
+#pragma unroll 1
+  for (int b = 0; b < 2 * Sg<F>::BATCHES; ++b) {
+    int32_t t[4];
+    eta = sg_divsteps28_var(eta, (uint32_t)__builtin_amdgcn_readlane(X[0], 0),
+                            (uint32_t)__builtin_amdgcn_readlane(Y[0], 0), t);
+    const int32_t ca = second ? t[2] : t[0], cb = second ? t[3] : t[1];
+    // d, e rows: the multiple of m that makes the division by 2^28 exact and
+    // keeps the row in (-2m, m) (sg_update_de, one row); f, g rows add none
+    const int32_t sx = X[L - 1] >> 31, sy = Y[L - 1] >> 31;
+    int32_t mm = (ca & sx) + (cb & sy);
+    int64_t c = smul(ca, X[0]) + smul(cb, Y[0]);
+    mm -= (int32_t)((Sg<F>::INV28 * (uint32_t)c + (uint32_t)mm) & MP_MASK);
+    if (!de) mm = 0;
+    c += smul((int32_t)F::M[0], mm);
+    c >>= MP_W;
+    int32_t nw[L];
+#pragma unroll
+    for (int i = 1; i < L; ++i) {
+      c += smul(ca, X[i]) + smul(cb, Y[i]);
+      if (F::M[i] != 0) c += smul((int32_t)F::M[i], mm);
+      nw[i - 1] = (int32_t)c & (int32_t)MP_MASK;
+      c >>= MP_W;
+    }
+    nw[L - 1] = (int32_t)c;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int32_t o = __shfl_xor(nw[i], 1);
+      X[i] = second ? o : nw[i];
+      Y[i] = second ? nw[i] : o;
+    }
+    int32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) o |= Y[i];
+    if (__builtin_amdgcn_readlane(o, 0) == 0) break;      // g == 0
+  }
+  const int32_t fsign = __builtin_amdgcn_readlane(X[L - 1], 0);
+  uint32_t out[L];
+  sg_normalize<F>(out, X, fsign);                          // lanes 2, 3: d
+#pragma unroll
+  for (int i = 0; i < L; ++i) r[i] = (uint32_t)__builtin_amdgcn_readlane((int32_t)out[i], 2);
+}
+
 // inverse in Montgomery form: x = aR  ->  a^-1 R  (lazy input accepted)
 template <class F>
 MPD void inv(uint32_t* r, const uint32_t* x) {
