@@ -2,7 +2,7 @@
 device round trip): ES256 tokens of the 4 bench kids, batch sizes 1 ... 4096,
 pinned host arena, p50 / p90 of many calls per size; optionally several
 threads submitting concurrently (pipelining on the device worker).
-usage: python tools/small_batch_probe.py [out.json] [threads] [ES256|EdDSA]
+usage: python tools/small_batch_probe.py [out.json] [threads] [ES256|ES384|ES512|EdDSA|RS256|PS256]
 (SBP_SIZES=1,64 picks the batch sizes)"""
 import ctypes
 import json
@@ -24,7 +24,8 @@ def main():
     from cap_amd import _lib
     L = _lib.lib()
     alg = sys.argv[3] if len(sys.argv) > 3 else "ES256"
-    kids = ["ed-a"] if alg == "EdDSA" else ["p256-a", "p256-b", "p256-c", "p256-d"]
+    kids = {"EdDSA": ["ed-a"], "RS256": ["rsa2048-a", "rsa2048-b"], "PS256": ["rsa2048-a", "rsa2048-b"],
+            "ES384": ["p384-a"], "ES512": ["p521-a"]}.get(alg, ["p256-a", "p256-b", "p256-c", "p256-d"])
     ctx = _lib.Context()
     ctx.load_keys(bench.abi_keys(kids))
     ctx.wait_tables()
