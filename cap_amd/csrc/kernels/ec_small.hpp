@@ -125,7 +125,12 @@ __device__ __forceinline__ void jadd_pair(JPt<typename CV::Fp>& P, int off, bool
     oz[j] = __shfl_xor(P.Z[j], off);
   }
   const bool oinf = __shfl_xor((int)P.inf, off) != 0;
-  exc = exc || __shfl_xor((int)exc, off) != 0;
+  // the partner's flag is read by every lane: `exc || __shfl_xor(...)` left the
+  // shuffle to the lanes whose own flag was clear, and a lane reading from one
+  // that had skipped it got 0 -- an exceptional partial lost on its way to lane 0
+  // (ec_edge.json exc-p521-G-accept-deq at equal G / key widths)
+  const int pexc = __shfl_xor((int)exc, off);
+  exc = exc || pexc != 0;
   const bool both = !P.inf && !oinf && !exc;
   // stage 1: own U, S against the other lane's Z
   uint32_t zz[L], u[L], t[L], sv[L], uo[L], so[L];

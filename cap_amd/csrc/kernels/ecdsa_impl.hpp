@@ -924,7 +924,8 @@ __global__ void __launch_bounds__(64) k_ec_point_split(EcArgs a) {
       Q.Z[j] = __shfl_xor(P.Z[j], off);
     }
     Q.inf = __shfl_xor((int)P.inf, off) != 0;
-    exc = exc || __shfl_xor((int)exc, off) != 0;
+    const int pexc = __shfl_xor((int)exc, off);    // every lane reads (see ec_small.hpp jadd_pair)
+    exc = exc || pexc != 0;
     if (run && (sub & off) == 0 && !exc) jadd<CV>(P, P, Q);
   }
   if (!run || sub != 0) return;

@@ -328,7 +328,8 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point_split(EdArgs a
       Q.Z[j] = __shfl_xor(P.Z[j], off);
       Q.T[j] = __shfl_xor(P.T[j], off);
     }
-    ok = ok && __shfl_xor((int)ok, off) != 0;
+    const int pok = __shfl_xor((int)ok, off);      // every lane reads (see ec_small.hpp jadd_pair)
+    ok = ok && pok != 0;
   };
   if constexpr (S == 4) {                       // lanes xor 1: the two partials of each scalar
     FPt Q;

@@ -107,9 +107,14 @@ def test_comb_tier_tokens_small_path(crv, wq):
         ctx.close()
 
 
-def test_exceptional_tokens_small_path():
+@pytest.mark.parametrize("budget", [0, None])
+def test_exceptional_tokens_small_path(budget):
     """Comb sums that meet P == +-Q: the lane partials flag the exception and
-    the block runs the complete double-and-add itself (ec_exact_ok)."""
+    the block runs the complete double-and-add itself (ec_exact_ok).  At the
+    default budget the P-384 / P-521 keys get the generator's width, so a key
+    Q = G has the generator's table: window partials G_w[d] + Q_w[-d] meet the
+    infinity in lanes far from lane 0 and the flag must reach it (a lane that
+    skipped the flag shuffle once lost exc-p521-G-accept-deq)."""
     from cap_amd import _lib
     d = json.load(open(os.path.join(H.ROOT, "tests", "golden", "ec_edge.json")))
     kid_index = {k["kid"]: i for i, k in enumerate(d["keys"])}
@@ -117,7 +122,8 @@ def test_exceptional_tokens_small_path():
     assert any(t.get("exceptional") and t["verdict"] == 1 for t in toks)
     ctx = _lib.Context()
     try:
-        ctx.set_table_budget(0)                     # the crafted exceptions are for 26/20 combs
+        if budget is not None:
+            ctx.set_table_budget(budget)            # the crafted exceptions are for 26/20 combs
         ctx.load_keys([H.abi_key(k) for k in d["keys"]])
         lone = _verify_each(ctx, toks, kid_index, 1)
         ctx.debug_small_path(False)
