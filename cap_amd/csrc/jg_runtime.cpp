@@ -1698,9 +1698,10 @@ void plan_chunk(Slot& S, const Item& it, const jg_tok* toks, size_t n, size_t jo
   if (pipe_trace()) S.host_ms[1] = ms_since(t_start);
 }
 
-// A small chunk whose jobs are all ECDSA (or rejected) -- coalesced
-// single-token calls -- runs as ONE launch per (curve, key-table width):
-// k_ec_small (kernels/ec_small.hpp) reads the jobs from its arguments and the
+// A small chunk whose jobs are all ECDSA or RS256/384/512 on RSA-2K-class
+// keys (or rejected) -- coalesced single-token calls -- runs as ONE launch per
+// (curve, key-table width) and one for the RSA jobs: k_ec_small
+// (kernels/ec_small.hpp) and k_rsa_small (kernels/rsa.hip) read the jobs from their arguments and the
 // arena in place (pinned host memory: the caller's, or the slot's staging)
 // and writes each verdict byte straight to the slot's pinned verdicts.  No
 // arena DMA, plan fill, prep / scalar / point / exact / scatter chain: the
@@ -1713,17 +1714,22 @@ void plan_chunk(Slot& S, const Item& it, const jg_tok* toks, size_t n, size_t jo
 bool issue_small_ec(Device* d, Slot& S, const Item& it, const ChunkPlan& CP, const KeyState& K, const DevGen& G,
                     hipStream_t s) {
   const size_t n = CP.n;
-  if (!it.small_ec || n == 0 || n > (size_t)EC_SMALL_MAX || CP.zc || !CP.src) return false;
+  if (!it.small_ec || n == 0 || n > (size_t)SMALL_MAX || CP.zc || !CP.src) return false;
   const size_t NB = K.keys.size() + 1;
   const jg_tok* ht = (const jg_tok*)((const uint8_t*)S.h_meta.p + PlanBlock(NB, n).toks_off);
-  int cls[EC_SMALL_MAX];
+  int cls[SMALL_MAX];
   for (size_t i = 0; i < n; ++i) {
     const int c = classify(K, ht[i]);
     cls[i] = c;
     if (c == CLS_REJECT) continue;
-    if (c < CLS_P256 || c > CLS_P521 || ht[i].sig_in_len > EC_SMALL_IN_MAX || !d->gtab[c]) return false;
+    if (ht[i].sig_in_len > SMALL_IN_MAX) return false;
     const int32_t k = ht[i].key_idx;
     const DevKey& rec = G.mirror[(size_t)k];
+    if (c == CLS_RSA2K) {                          // k_rsa_small: PKCS#1 v1.5 only
+      if (ht[i].alg < JG_RS256 || ht[i].alg > JG_RS512 || rec.rr2_off == 0) return false;
+      continue;
+    }
+    if (c < CLS_P256 || c > CLS_P521 || !d->gtab[c]) return false;
     if (G.kw[(size_t)k] == 0 || rec.tab == 0 || rec.tab_w != G.kw[(size_t)k]) return false;
   }
   // the arena's device view: the caller's page-locked arena, or the staging copy
@@ -1734,10 +1740,31 @@ bool issue_small_ec(Device* d, Slot& S, const Item& it, const ChunkPlan& CP, con
   uint8_t* vh = (uint8_t*)S.h_verdict.get(n);
   std::memset(vh, 0, n);
   uint8_t* vd = (uint8_t*)S.h_verdict.dp;
-  bool done[EC_SMALL_MAX] = {};
+  bool done[SMALL_MAX] = {};
   for (size_t i = 0; i < n; ++i) {
     if (done[i] || cls[i] == CLS_REJECT) continue;
-    const int c = cls[i], w = G.kw[ht[i].key_idx];
+    const int c = cls[i];
+    if (c == CLS_RSA2K) {
+      RsaSmallArgs A{};
+      A.arena = dsrc;
+      A.keys = G.keys();
+      A.keyblob = G.keyblob();
+      A.verdict = vd;
+      for (size_t j = i; j < n; ++j) {
+        if (done[j] || cls[j] != c) continue;
+        const jg_tok& t = ht[j];
+        const uint64_t o = t.off - CP.dbase;
+        A.jobs[A.n] = JobDev{(uint32_t)o, t.sig_in_len, (uint32_t)(o + t.sig_rel_off),
+                             job_pack(t.key_idx, t.alg, t.sig_b64_len)};
+        A.out[A.n] = (uint16_t)j;
+        ++A.n;
+        done[j] = true;
+      }
+      launch_rsa_small(A, s);
+      if (it.small_launches) it.small_launches->fetch_add(1, std::memory_order_relaxed);
+      continue;
+    }
+    const int w = G.kw[ht[i].key_idx];
     EcSmallArgs A{};
     A.arena = dsrc;
     A.keys = G.keys();
@@ -2166,13 +2193,22 @@ void build_keys(const jg_key* keys, int nkeys, uint64_t table_budget, StagedKeys
       K.e_lo = (uint32_t)k.e;
       K.e_hi = (uint32_t)(k.e >> 32);
       K.nlimbs = (uint32_t)L;
-      K.n_off = blob_alloc(S.blob, L);
+      // RSA-2K keys also serve the one-launch small path (k_rsa_small): n
+      // zero-padded to its RSA_SMALL_L limbs and R'^2 mod n for R' = 2^(28 * 80)
+      const int Ln = cls == CLS_RSA2K ? std::max(L, RSA_SMALL_L) : L;
+      K.n_off = blob_alloc(S.blob, Ln);
       K.rr_off = blob_alloc(S.blob, L);
-      if (nl > 0) be_to_limbs(n, nl, S.blob.data() + K.n_off, L);
+      K.rr2_off = 0;
+      if (nl > 0) be_to_limbs(n, nl, S.blob.data() + K.n_off, Ln);
       // R^2 mod n (R = 2^(28 L)) and n' on the host: ~0.2 ms for an RSA-4096
       // key (host_mont.hpp; the device's 56 L modular doublings took ~200 ms
       // for the 32-kid bench set, profiles/r04_s1_keyload_trace.log)
       if (ok) hostmont::rsa_key_constants(S.blob.data() + K.n_off, L, S.blob.data() + K.rr_off, &K.np);
+      if (ok && cls == CLS_RSA2K) {
+        K.rr2_off = blob_alloc(S.blob, RSA_SMALL_L);
+        uint32_t np2 = 0;
+        hostmont::rsa_key_constants(S.blob.data() + K.n_off, RSA_SMALL_L, S.blob.data() + K.rr2_off, &np2);
+      }
       if (ok) S.rsa_idx.push_back(i);
       hk.cls = cls;
       hk.valid = ok;

@@ -21,6 +21,12 @@ enum Cls : int {
 
 constexpr int WAVE = 64;
 
+// One-launch small batches (ec_small.hpp, rsa.hip k_rsa_small): at most
+// SMALL_MAX jobs per launch, each signing input at most SMALL_IN_MAX bytes
+// (staged in LDS); longer ones take the batch chain.
+constexpr int SMALL_MAX = 64;
+constexpr uint32_t SMALL_IN_MAX = 8192;
+
 // per-token status codes in the scratch status byte
 enum : uint8_t { ST_OK = 0, ST_REJECT = 1, ST_EXCEPTIONAL = 2 };
 
@@ -68,6 +74,8 @@ struct DevKey {
   uint64_t aux_off;    // EC: Q affine Montgomery (x,y) / Ed: raw public key words
   int32_t embits;      // RSA: bitlen(n) - 1
   int32_t tab_w;       // EC / Ed: comb width of `tab`
+  uint64_t rr2_off;    // RSA-2K: R^2 mod n for the one-launch layout (RSA_SMALL_L limbs; n_off holds
+                       // that many limbs, zero-padded), 0 = none
 };
 __host__ __device__ inline const uint32_t* key_table(const DevKey& K) { return (const uint32_t*)K.tab; }
 

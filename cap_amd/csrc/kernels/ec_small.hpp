@@ -24,56 +24,14 @@
 // pinned host memory (no scatter or copy launch).
 #pragma once
 #include "ecdsa_impl.hpp"
-#include "sha2.hpp"
+#include "small_common.hpp"
 
 namespace {
 
-constexpr int SM_THREADS = 128;
 constexpr int SM_SPLIT = 16;                                      // point lanes per token
-constexpr uint32_t SM_IN_DW = EC_SMALL_IN_MAX / 4 + 72;           // staged signing input + SHA padding blocks
 constexpr uint32_t SM_SIG_CHARS = 176;                            // ES512's 132 bytes; longer is rejected
 
-// JG_SMALL_PROF=1 (A/B builds only, tools/small_prof.sh): lane 0 of each wave
-// stamps s_memrealtime (100 MHz) at the phase boundaries and the block prints
-// one line per token -- where a lone token's ~85 us go.
-#ifndef JG_SMALL_PROF
-#define JG_SMALL_PROF 0
-#endif
-#if JG_SMALL_PROF
-#define SM_STAMP(i) do { if (lane == 0) stamp[wave][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define SM_STAMP(i) do { } while (0)
-#endif
-
-__device__ __forceinline__ int sm_b64val(uint32_t c) {
-  if (c - 'A' < 26u) return (int)(c - 'A');
-  if (c - 'a' < 26u) return (int)(c - 'a' + 26);
-  if (c - '0' < 10u) return (int)(c - '0' + 52);
-  if (c == '-') return 62;
-  if (c == '_') return 63;
-  return -1;
-}
-
 __device__ __forceinline__ int sm_hash_bits(int alg) { return alg == 7 ? 256 : alg == 8 ? 384 : 512; }
-
-// N big-endian words of the SHA-padded message from word w0 (length words
-// are the caller's), the message staged in LDS as aligned dwords starting
-// `shift` bytes before it (sha2::MemString::padded_words on an LDS array)
-template <int N>
-__device__ __forceinline__ void sm_words(const uint32_t* lds, uint32_t w0, uint32_t shift, uint32_t len,
-                                         uint32_t* out) {
-  uint32_t u[N + 1];
-#pragma unroll
-  for (int k = 0; k <= N; ++k) u[k] = mp::lane_value(lds[w0 + k]);   // keep the SHA on VALU (mp::lane_value)
-#pragma unroll
-  for (int k = 0; k < N; ++k) {
-    const uint32_t raw = sha2::bswap32(__builtin_amdgcn_alignbyte(u[k + 1], u[k], shift));
-    const int rem = (int)len - (int)(4u * (w0 + k));
-    const uint32_t keep = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : (0xffffffffu << (32 - 8 * rem)));
-    const uint32_t pad = (rem >= 0 && rem < 4) ? (0x80u << (24 - 8 * rem)) : 0u;
-    out[k] = (raw & keep) | pad;
-  }
-}
 
 // x(R) mod n == r for R = (X : Y : Z) Jacobian, Z != 0:
 // X == r Z^2, or r + n < p and X == (r + n) Z^2
@@ -254,60 +212,21 @@ __global__ void __launch_bounds__(SM_THREADS) k_ec_small(EcSmallArgs a) {
 
   // ---- phase 1: both streams into LDS
   if (wave == 0 && in_ok) {
-    const uint32_t len = jb.sig_in_len;
-    const uint32_t shift = in_shift;
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(a.arena + jb.off - shift);
-    const uint32_t ndw = (shift + len + 3) / 4;                 // dwords holding message bytes
-    const int hb = sm_hash_bits(alg);
-    const uint32_t nblk = hb == 256 ? (len + 9 + 63) / 64 : (len + 17 + 127) / 128;
-    const uint32_t need = nblk * (hb == 256 ? 16u : 32u) + 1u; // padded stream + the alignbyte dword
-    for (uint32_t base = 0; base < need; base += 64 * 8) {
-      uint32_t v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t i = base + (uint32_t)lane + 64u * k;
-        v[k] = i < ndw ? g[i] : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t i = base + (uint32_t)lane + 64u * k;
-        if (i < need) in_w[i] = v[k];
-      }
-    }
+    sm_stage_input(in_w, reinterpret_cast<const uint32_t*>(a.arena + jb.off - in_shift), in_shift, jb.sig_in_len,
+                   sm_hash_bits(alg), lane);
   } else if (wave == 1) {
-    const uint32_t sshift = sig_shift;
-    const uint32_t* g = reinterpret_cast<const uint32_t*>(a.arena + jb.sig_off - sshift);
-    const uint32_t nd = nch <= SM_SIG_CHARS ? (sshift + nch + 3) / 4 : 0u;
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(a.arena + jb.sig_off - sig_shift);
+    const uint32_t nd = nch <= SM_SIG_CHARS ? (sig_shift + nch + 3) / 4 : 0u;
     if ((uint32_t)lane < nd) sig_w[lane] = g[lane];
   }
   SM_STAMP(1);
   __syncthreads();
 
   // ---- phase 2: signature characters -> bytes (wave 1, a quad per lane)
-  const uint32_t D = (nch & 3u) == 1u ? 0u : (nch >> 2) * 3u + ((nch & 3u) == 2u ? 1u : (nch & 3u) == 3u ? 2u : 0u);
+  const uint32_t D = sm_b64_len(nch);
   const bool size_ok = nch <= SM_SIG_CHARS && (nch & 3u) != 1u && D == 2u * (uint32_t)ks;
   if (wave == 1 && size_ok) {
-    const uint32_t sshift = sig_shift;
-    const uint32_t c0 = 4u * (uint32_t)lane;
-    bool bad = false;
-    if (c0 < nch) {
-      uint32_t acc = 0;
-      const uint32_t cnt = nch - c0 < 4u ? nch - c0 : 4u;
-      for (uint32_t k = 0; k < 4; ++k) {
-        int v = 0;
-        if (k < cnt) {
-          const uint32_t b = sshift + c0 + k;
-          v = sm_b64val((sig_w[b >> 2] >> (8u * (b & 3u))) & 0xffu);
-          bad |= v < 0;
-        }
-        acc = (acc << 6) | (uint32_t)(v < 0 ? 0 : v);
-      }
-      // cnt characters carry 6 cnt bits: 3 bytes from 4, 2 from 3, 1 from 2
-      const uint32_t nb = cnt == 4 ? 3u : cnt - 1u;
-      const uint32_t o = 3u * (uint32_t)lane;
-      for (uint32_t k = 0; k < nb; ++k) sig_b[o + k] = (uint8_t)(acc >> (16u - 8u * k));
-    }
-    if (__ballot(bad) != 0ull && lane == 0) flag[0] = 1;
+    if (sm_b64_decode(sig_w, sig_shift, nch, sig_b, lane) && lane == 0) flag[0] = 1;
   }
   __syncthreads();
 
@@ -340,38 +259,7 @@ __global__ void __launch_bounds__(SM_THREADS) k_ec_small(EcSmallArgs a) {
   if (wave == 0 && lane == 0 && in_ok) {
     // the padded message words straight from the LDS stage (ds_read; through
     // sha2::MemString's generic pointer they were flat loads: ~6.7 us per block)
-    const uint32_t len = jb.sig_in_len;
-    const int hb = sm_hash_bits(alg);
-    if (hb == 256) {
-      uint32_t h[8];
-      sha2::sha256_init(h);
-      const uint32_t nblk = (len + 9 + 63) / 64;
-#pragma unroll 1
-      for (uint32_t blk = 0; blk < nblk; ++blk) {
-        uint32_t w[16];
-        sm_words<16>(in_w, blk * 16, in_shift, len, w);
-        if (blk == nblk - 1) { w[14] = len >> 29; w[15] = len << 3; }
-        sha2::sha256_compress(h, w);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) dig_w[k] = h[k];
-    } else {
-      uint64_t h[8];
-      sha2::sha512_init(h, hb == 384);
-      const uint32_t nblk = (len + 17 + 127) / 128;
-#pragma unroll 1
-      for (uint32_t blk = 0; blk < nblk; ++blk) {
-        uint32_t v[32];
-        sm_words<32>(in_w, blk * 32, in_shift, len, v);
-        if (blk == nblk - 1) { v[30] = len >> 29; v[31] = len << 3; }
-        uint64_t w[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) w[k] = ((uint64_t)v[2 * k] << 32) | v[2 * k + 1];
-        sha2::sha512_compress(h, w);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { dig_w[2 * k] = (uint32_t)(h[k] >> 32); dig_w[2 * k + 1] = (uint32_t)h[k]; }
-    }
+    sm_hash(in_w, in_shift, jb.sig_in_len, sm_hash_bits(alg), dig_w);
   }
   uint32_t w[L];                                   // s^-1 R (wave 1 lane 0)
   if (wave == 1 && lane < 4) {                     // four lanes: the inversion's limb rows (mp::inv_plain_var4)

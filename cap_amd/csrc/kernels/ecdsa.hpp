@@ -116,8 +116,8 @@ void launch_ec(int cls, const EcArgs& a, hipStream_t s, const jgk::Marker& mk);
 // The jobs travel in the kernel arguments.  Every token of a launch has a key
 // of class `cls` whose comb table has width `wq`, a signing input of at most
 // EC_SMALL_IN_MAX bytes, and its alg in the key's family (the host plan).
-constexpr int EC_SMALL_MAX = 64;            // tokens per launch
-constexpr uint32_t EC_SMALL_IN_MAX = 8192;  // signing-input bytes staged in LDS
+constexpr int EC_SMALL_MAX = jgk::SMALL_MAX;              // tokens per launch
+constexpr uint32_t EC_SMALL_IN_MAX = jgk::SMALL_IN_MAX;   // signing-input bytes staged in LDS
 struct EcSmallArgs {
   const uint8_t* arena;                     // JobDev offsets are relative to it
   const jgk::DevKey* keys;

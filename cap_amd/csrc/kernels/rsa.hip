@@ -20,6 +20,7 @@
 #include "sha2.hpp"
 #include "mad.hpp"
 #include "mad_blocks.hpp"
+#include "small_common.hpp"
 
 using namespace jgk;
 
@@ -652,7 +653,215 @@ __global__ void __launch_bounds__(64) JG_RSA_PAD_ATTR k_rsa_pad(RsaArgs a) {
   a.verdict_pad[p] = verdict;
 }
 
+// ------------------------------------------------------------------ one launch (small batches)
+// k_rsa_small: one 128-thread block per RS256 / RS384 / RS512 token on an
+// RSA-2K-class key, the whole verification in one launch (the batch chain's
+// prep, modexp and pad kernels), for coalesced single-token calls
+// (jwt/keyset.go:27-32).  A lone token's modexp is a chain of 17 dependent
+// Montgomery products; here each runs on 16 lanes of 5 limbs (R = 2^2240, the
+// key's rr2_off constants): 80 CIOS rows of ~10 MADs per lane instead of the
+// batch layout's 74 rows of 74 MADs on 2 lanes.  Wave 0 hashes the signing
+// input on one lane meanwhile (s^e does not depend on it).  The four 16-lane
+// groups of wave 1 run the same token (lanes of groups 1-3 compute copies);
+// group 0's result is compared with EM = 00 01 FF..FF 00 || DigestInfo || H
+// word by word across the wave (R15).
+constexpr uint32_t RS_SIG_CHARS = 352;          // 264 bytes; the RSA-2K class has k <= 259
+__global__ void __launch_bounds__(SM_THREADS) k_rsa_small(RsaSmallArgs a) {
+  constexpr int H = RSA_SMALL_H, G = RSA_SMALL_G, L = RSA_SMALL_L, TPW = WAVE / G, U = 8;
+  constexpr int NWOUT = (W28 * L + 31) / 32;
+  __shared__ uint32_t in_w[SM_IN_DW];
+  __shared__ uint32_t sig_w[RS_SIG_CHARS / 4 + 2];
+  __shared__ uint8_t sig_b[3 * (RS_SIG_CHARS / 4) + 4];
+  __shared__ uint32_t dig_w[16];
+  __shared__ uint32_t lds[L * TPW];
+  __shared__ uint32_t yw[NWOUT];
+  __shared__ int32_t flag[2];                   // [0] signature characters bad, [1] the modexp ran
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const JobDev jb = a.jobs[blockIdx.x];
+  const int alg = job_alg(jb);
+  const DevKey& K = a.keys[job_key(jb)];
+  const int k = K.kbytes;
+  const uint32_t nch = job_siglen(jb);
+  const int hb = alg == 1 ? 256 : alg == 2 ? 384 : 512;
+  const bool in_ok = jb.sig_in_len <= SMALL_IN_MAX;
+  const uint32_t in_shift = (uint32_t)((uintptr_t)(a.arena + jb.off) & 3u);
+  const uint32_t sig_shift = (uint32_t)((uintptr_t)(a.arena + jb.sig_off) & 3u);
+  if (tid == 0) { flag[0] = 0; flag[1] = 0; }
+  // ---- both streams into LDS
+  if (wave == 0 && in_ok) {
+    sm_stage_input(in_w, reinterpret_cast<const uint32_t*>(a.arena + jb.off - in_shift), in_shift, jb.sig_in_len, hb,
+                   lane);
+  } else if (wave == 1) {
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(a.arena + jb.sig_off - sig_shift);
+    const uint32_t nd = nch <= RS_SIG_CHARS ? (sig_shift + nch + 3) / 4 : 0u;
+    for (uint32_t i = (uint32_t)lane; i < nd; i += 64) sig_w[i] = g[i];
+  }
+  __syncthreads();
+  // ---- characters -> bytes; len(sig) == k (R13)
+  const bool size_ok = nch <= RS_SIG_CHARS && (nch & 3u) != 1u && sm_b64_len(nch) == (uint32_t)k;
+  if (wave == 1 && size_ok) {
+    if (sm_b64_decode(sig_w, sig_shift, nch, sig_b, lane) && lane == 0) flag[0] = 1;
+  }
+  __syncthreads();
+  const bool ok0 = in_ok && size_ok && flag[0] == 0 && K.valid != 0 && K.rr2_off != 0 && alg >= 1 && alg <= 3;
+  // ---- hash (wave 0 lane 0) || s^e mod n (wave 1, 16 lanes per group)
+  if (wave == 0 && lane == 0 && in_ok) sm_hash(in_w, in_shift, jb.sig_in_len, hb, dig_w);
+  if (wave == 1 && ok0) {
+    const int g = lane % G, tl = lane / G;
+    const bool lane0 = g == 0, lastl = g == G - 1;
+    const uint32_t ml0 = opaque_mask(!lane0), mlast = opaque_mask(!lastl);
+    const uint32_t* __restrict__ N = a.keyblob + K.n_off;
+    const uint32_t* __restrict__ RR = a.keyblob + K.rr2_off;
+    const uint32_t np28 = K.np;
+    const uint64_t e = ((uint64_t)K.e_hi << 32) | K.e_lo;
+    uint32_t* la = lds + tl;
+    uint32_t n[H], v[H], xl[H], xm[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) n[j] = N[g * H + j];
+    // x: limb j = bits [28 j, 28 j + 28) of the big-endian k-byte signature
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      const int bit = W28 * (g * H + j), i0 = bit >> 3, sh = bit & 7;
+      uint64_t acc = 0;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const int i = i0 + t;                       // little-endian byte index of the integer
+        acc |= (uint64_t)(i < k ? sig_b[k - 1 - i] : 0u) << (8 * t);
+      }
+      v[j] = (uint32_t)(acc >> sh) & M28;
+      xl[j] = v[j];
+    }
+    // sig < N (Go >= 1.20, R14): the highest differing lane of the group decides
+    bool act = true;
+    {
+      int lt = 0, gt = 0;
+#pragma unroll
+      for (int j = H - 1; j >= 0; --j) {
+        const int und = !(lt | gt);
+        lt |= und & (v[j] < n[j]);
+        gt |= und & (v[j] > n[j]);
+      }
+      int dec = lt ? 1 : (gt ? 2 : 0);
+#pragma unroll
+      for (int r = 0; r < G - 1; ++r) {
+        const int up = (int)from_next<G>((uint32_t)dec);
+        dec = (up & (int)mlast) != 0 ? (up & (int)mlast) : dec;
+      }
+      dec = (int)bcast0<G>((uint32_t)dec);
+      act = dec == 1;
+    }
+    enum { TOMONT, SQUARE, MULXM, MULX, MULONE };
+    const int ebits = 64 - __builtin_clzll(e);
+    int op = TOMONT, bit = ebits - 2;
+    for (;;) {
+      lds_store<H, TPW>(la, v, g);
+      if (op == TOMONT) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) v[j] = RR[g * H + j];
+      } else if (op == MULXM) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) v[j] = xm[j];
+      } else if (op == MULX) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) v[j] = xl[j];
+      } else if (op == MULONE) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) v[j] = (j == 0 && lane0) ? 1u : 0u;
+      }
+      if (op == SQUARE) mont_sqr<H, G, TPW>(v, la, n, np28, g, lane0, mlast, ml0);
+      else mont_mul<H, G, U, TPW>(v, la, n, np28, lane0, mlast, ml0);
+      if (op == TOMONT) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) xm[j] = v[j];
+        op = SQUARE;
+      } else if (op == SQUARE) {
+        if ((e >> bit) & 1ull) op = bit > 0 ? MULXM : MULX;
+        else if (bit == 0) op = MULONE;
+        else --bit;
+      } else if (op == MULXM) {
+        --bit;
+        op = SQUARE;
+      } else {
+        break;
+      }
+    }
+    // canonical: v < 2n -> v mod n (borrow rippled up the group)
+    {
+      uint32_t d[H];
+      int32_t bout = 0;
+#pragma unroll
+      for (int r = 0; r < G; ++r) {
+        int32_t br = (int32_t)(from_prev<G>((uint32_t)bout) & ml0);
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+          const int32_t t = (int32_t)v[j] - (int32_t)n[j] + br;
+          d[j] = (uint32_t)t & M28;
+          br = t >> W28;
+        }
+        bout = br;
+      }
+      const int32_t b_top = (int32_t)bcast_last<G>((uint32_t)bout);
+#pragma unroll
+      for (int j = 0; j < H; ++j) v[j] = b_top < 0 ? v[j] : d[j];
+    }
+    // y as LE 32-bit words (group 0)
+    lds_store<H, TPW>(la, v, g);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    constexpr int PER = (NWOUT + G - 1) / G;
+#pragma unroll
+    for (int kk = 0; kk < PER; ++kk) {
+      const int q = g * PER + kk;
+      if (q < NWOUT && tl == 0) {
+        const int b32 = 32 * q, j0 = b32 / W28, s0 = b32 % W28;
+        uint64_t acc = (uint64_t)la[j0 * TPW] >> s0;
+        int have = W28 - s0;
+        int j = j0 + 1;
+        while (have < 32 && j < L) { acc |= (uint64_t)la[j * TPW] << have; have += W28; ++j; }
+        yw[q] = (uint32_t)acc;
+      }
+    }
+    if (lane == 0) flag[1] = act ? 1 : 0;
+  }
+  __syncthreads();
+  // ---- PKCS#1 v1.5 (R15): EM == 00 01 FF..FF 00 || DigestInfo || H, word by
+  // word on the little-endian y (k_rsa_pad's rule), one word per lane
+  if (wave != 1) return;
+  const int hlen = hb / 8, tlen = 19 + hlen, nw = (k + 3) / 4;
+  const uint8_t* DI = hb == 256 ? DI256 : hb == 384 ? DI384 : DI512;
+  uint32_t diff = 0;
+  if (ok0 && flag[1] != 0) {
+    for (int q = lane; q < nw; q += 64) {
+      uint32_t ev;
+      if (q < hlen / 4) {
+        ev = dig_w[hlen / 4 - 1 - q];
+      } else {
+        ev = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const int j = 4 * q + bb;
+          uint32_t ex;
+          if (j < tlen) ex = DI[tlen - 1 - j];
+          else if (j == tlen) ex = 0;
+          else if (j < k - 2) ex = 0xff;
+          else if (j == k - 2) ex = 1;
+          else ex = 0;
+          ev |= ex << (8 * bb);
+        }
+      }
+      diff |= yw[q] ^ ev;
+    }
+  }
+  const bool any = __ballot(diff != 0) != 0ull;
+  if (lane == 0) a.verdict[a.out[blockIdx.x]] = (ok0 && flag[1] != 0 && k >= tlen + 11 && !any) ? 1 : 0;
+}
+
 }  // namespace
+
+void launch_rsa_small(const RsaSmallArgs& a, hipStream_t s) {
+  if (a.n == 0) return;
+  hipLaunchKernelGGL(k_rsa_small, dim3(a.n), dim3(SM_THREADS), 0, s, a);
+}
 
 void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const Marker& mk) {
   const int64_t waves = (a.end - a.begin) / WAVE;

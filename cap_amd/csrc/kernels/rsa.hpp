@@ -74,3 +74,23 @@ static_assert(rsa_sig_rows_l(rsa4k_layout_limbs(RSA4K_NLAYOUT - 1)) <= jgk::SIGW
               "RSA-16K signature rows exceed the scratch");
 
 void launch_rsa(int cls, const RsaArgs& a, hipStream_t s, const jgk::Marker& mk);
+
+// One-launch verification of a small batch of PKCS#1 v1.5 tokens (RS256 /
+// RS384 / RS512) on RSA-2K-class keys (k_rsa_small, rsa.hip): one two-wave
+// block per token -- the signing input hashed on one lane while the other
+// wave decodes the signature and runs s^e mod n on 16 lanes of 5 limbs
+// (RSA_SMALL_L = 80 limbs, R = 2^2240: each key carries R^2 mod n for that R
+// at rr2_off), then the EM compare -- writing verdict[out[i]] (pinned host
+// memory).  Jobs in the arguments, arena read in place (as EcSmallArgs).
+constexpr int RSA_SMALL_H = 5, RSA_SMALL_G = 16, RSA_SMALL_L = RSA_SMALL_H * RSA_SMALL_G;
+static_assert(RSA_SMALL_L * 28 - 2 >= 74 * 28 - 2, "the small layout holds every RSA-2K modulus");
+struct RsaSmallArgs {
+  const uint8_t* arena;
+  const jgk::DevKey* keys;
+  const uint32_t* keyblob;
+  uint8_t* verdict;
+  uint32_t n;
+  jgk::JobDev jobs[jgk::SMALL_MAX];
+  uint16_t out[jgk::SMALL_MAX];
+};
+void launch_rsa_small(const RsaSmallArgs& a, hipStream_t s);

@@ -1,5 +1,6 @@
-"""The one-launch small-batch ECDSA path (kernels/ec_small.hpp k_ec_small,
-jg_runtime.cpp issue_small_ec): coalesced single-token calls behind
+"""The one-launch small-batch paths (kernels/ec_small.hpp k_ec_small,
+kernels/rsa.hip k_rsa_small, jg_runtime.cpp issue_small_ec): coalesced
+single-token calls behind
 /root/reference/jwt/keyset.go:27-32 (VerifySignature) and jwt/jwt.go:95-97
 (Validate) reach jg_verify_batch as batches of a few tokens, which run as one
 launch per (curve, key-table width) instead of the batch chain.
@@ -203,3 +204,90 @@ def test_pinned_caller_arena_read_in_place():
             assert [0 if s is None else out[s] for s in slots] == [t["verdict"] for t in sel], lead
     finally:
         ctx.close()
+
+
+def test_golden_rsa_tokens_small_path():
+    """RS256 / RS384 / RS512 on RSA-2K-class keys (2047 / 2048 / 2049 bits,
+    e = 65537 and e = 3) run k_rsa_small: s^e mod n on 16 lanes of 5 limbs
+    with the key's R = 2^2240 constants; PS* tokens and bigger keys take the
+    chain.  Every verdict equals the fixture's, the oracle's and the chain's."""
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    rsa = {k["kid"] for k in keys if k["kty"] == "RSA"}
+    toks = [t for t in toks if t["key"] in rsa]
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    okeys = {k["kid"]: jws.Key.from_fixture(k) for k in keys}
+    small_kids = {k["kid"] for k in keys if k["kty"] == "RSA" and int(k["n"], 16).bit_length() <= 74 * 28 - 2}
+    assert {"rsa2048-a", "rsa2048-e3", "rsa2047-a", "rsa2049-a"} <= small_kids
+    want = []
+    for t in toks:
+        p = jws.parse_jws(t["token"])
+        w = int(jws.verify_sig(p, okeys[t["key"]])) if p is not None and p.crit_ok else 0
+        assert w == t["verdict"], t["name"]
+        want.append(w)
+    assert sum(w for w, t in zip(want, toks) if t["key"] in small_kids and t["alg"].startswith("RS")) >= 5
+    ctx = _lib.Context()
+    try:
+        ctx.load_keys([H.abi_key(k) for k in keys])
+        n0 = ctx.debug_small_path()
+        lone = _verify_each(ctx, toks, kid_index, 1)
+        n1 = ctx.debug_small_path()
+        few = _verify_each(ctx, toks, kid_index, 5)
+        ctx.debug_small_path(False)
+        chain = _verify_each(ctx, toks, kid_index, 5)
+        ctx.debug_small_path(True)
+        small = sum(1 for t in toks if t["key"] in small_kids and
+                    (lambda p: p is not None and p.crit_ok and p.alg in ("RS256", "RS384", "RS512"))(jws.parse_jws(t["token"])))
+        assert small >= 10 and n1 - n0 == small
+        bad = [t["name"] for t, a, b, c, w in zip(toks, lone, few, chain, want) if not a == b == c == w]
+        assert not bad, bad
+    finally:
+        ctx.close()
+
+
+def test_rsa_small_path_random_signatures():
+    """s^e mod n against Python's pow() through the verdicts: for random
+    signatures s < n the EM compare fails, for s = EM^d it passes -- here with
+    OpenSSL-signed RS256 / RS512 tokens of the bench keys plus a one-bit flip
+    of every one, lone and 64 at a time."""
+    import bench
+    from cap_amd import _lib
+    kids = ["rsa2048-a", "rsa2048-b"]
+    pool = bench.gen_tokens("RS256", 96, bench.golden_keypaths(kids), 4, "rsasmall") + \
+        bench.gen_tokens("RS512", 32, bench.golden_keypaths(kids), 4, "rsasmall")
+    ctx = _lib.Context()
+    try:
+        ctx.load_keys(bench.abi_keys(kids))
+        arena = _lib.Arena()
+        want = []
+        for i, t in enumerate(pool):
+            si, sig = t[:t.rfind(b".")], t[t.rfind(b".") + 1:]
+            alg = "RS512" if i >= 96 else "RS256"
+            if i % 3 == 2:                                  # flip one character of the signature
+                j = 7 + (i % 300)
+                sig = sig[:j] + (b"A" if sig[j:j + 1] != b"A" else b"B") + sig[j + 1:]
+                want.append(0)
+            else:
+                want.append(1)
+            arena.add(si, sig, alg, i % 2)
+        n0 = ctx.debug_small_path()
+        got = list(ctx.verify(_sub(arena, 0, 64))) + list(ctx.verify(_sub(arena, 64, 128)))
+        assert ctx.debug_small_path() - n0 == 2
+        assert got == want
+        lone = []
+        for i in range(0, len(pool), 9):
+            lone.append(ctx.verify(_sub(arena, i, i + 1))[0])
+        assert lone == want[::9]
+    finally:
+        ctx.close()
+
+
+def _sub(arena, lo, hi):
+    """the jobs [lo, hi) of an Arena as an Arena of their own"""
+    from cap_amd import _lib
+    out = _lib.Arena()
+    for t in arena.toks[lo:hi]:
+        off, sil, rel, sl, key, alg = t
+        out.buf += arena.buf[off:off + rel + sl]
+        out.toks.append((len(out.buf) - rel - sl, sil, rel, sl, key, alg))
+    return out
