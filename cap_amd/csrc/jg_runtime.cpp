@@ -1698,10 +1698,11 @@ void plan_chunk(Slot& S, const Item& it, const jg_tok* toks, size_t n, size_t jo
   if (pipe_trace()) S.host_ms[1] = ms_since(t_start);
 }
 
-// A small chunk whose jobs are all ECDSA or RS256/384/512 on RSA-2K-class
-// keys (or rejected) -- coalesced single-token calls -- runs as ONE launch per
-// (curve, key-table width) and one for the RSA jobs: k_ec_small
-// (kernels/ec_small.hpp) and k_rsa_small (kernels/rsa.hip) read the jobs from their arguments and the
+// A small chunk whose jobs are all ECDSA, EdDSA or RS256/384/512 on RSA-2K-
+// class keys (or rejected) -- coalesced single-token calls -- runs as ONE
+// launch per (curve, key-table width) and one for the RSA jobs: k_ec_small
+// (kernels/ec_small.hpp), k_ed_small (ed25519.hip) and k_rsa_small (rsa.hip)
+// read the jobs from their arguments and the
 // arena in place (pinned host memory: the caller's, or the slot's staging)
 // and writes each verdict byte straight to the slot's pinned verdicts.  No
 // arena DMA, plan fill, prep / scalar / point / exact / scatter chain: the
@@ -1729,7 +1730,11 @@ bool issue_small_ec(Device* d, Slot& S, const Item& it, const ChunkPlan& CP, con
       if (ht[i].alg < JG_RS256 || ht[i].alg > JG_RS512 || rec.rr2_off == 0) return false;
       continue;
     }
-    if (c < CLS_P256 || c > CLS_P521 || !d->gtab[c]) return false;
+    if (c == CLS_ED25519) {
+      if (ht[i].alg != JG_EDDSA || !d->btab) return false;
+    } else if (c < CLS_P256 || c > CLS_P521 || !d->gtab[c]) {
+      return false;
+    }
     if (G.kw[(size_t)k] == 0 || rec.tab == 0 || rec.tab_w != G.kw[(size_t)k]) return false;
   }
   // the arena's device view: the caller's page-locked arena, or the staging copy
@@ -1765,6 +1770,27 @@ bool issue_small_ec(Device* d, Slot& S, const Item& it, const ChunkPlan& CP, con
       continue;
     }
     const int w = G.kw[ht[i].key_idx];
+    if (c == CLS_ED25519) {
+      EdSmallArgs A{};
+      A.arena = dsrc;
+      A.keys = G.keys();
+      A.keyblob = G.keyblob();
+      A.btab = d->btab;
+      A.verdict = vd;
+      for (size_t j = i; j < n; ++j) {
+        if (done[j] || cls[j] != c || G.kw[ht[j].key_idx] != w) continue;
+        const jg_tok& t = ht[j];
+        const uint64_t o = t.off - CP.dbase;
+        A.jobs[A.n] = JobDev{(uint32_t)o, t.sig_in_len, (uint32_t)(o + t.sig_rel_off),
+                             job_pack(t.key_idx, t.alg, t.sig_b64_len)};
+        A.out[A.n] = (uint16_t)j;
+        ++A.n;
+        done[j] = true;
+      }
+      launch_ed_small(w, A, s);
+      if (it.small_launches) it.small_launches->fetch_add(1, std::memory_order_relaxed);
+      continue;
+    }
     EcSmallArgs A{};
     A.arena = dsrc;
     A.keys = G.keys();

@@ -20,6 +20,7 @@
 #include "fe25519.hpp"
 #include "mp.hpp"
 #include "tables.hpp"
+#include "small_common.hpp"
 
 using namespace jgk;
 
@@ -430,6 +431,167 @@ __global__ void __launch_bounds__(64 * ED_FINISH_WPB) k_ed_finish(EdArgs a, int 
   }
 }
 
+// ------------------------------------------------------------------ one launch (small batches)
+// k_ed_small: one 128-thread block per EdDSA token (jwt/keyset.go:27-32 single
+// calls), the work of k_prep_ed, k_ed_point_split and k_ed_finish in one launch:
+//   wave 1 decodes the signature (R, S; len 64, S < L, sig[63] & 0xE0 == 0:
+//   R24) and recodes S; wave 0 hashes R || A || M on one lane and recodes
+//   k = H mod L; 16 lanes of wave 0 each add one or two windows of both combs
+//   (complete Niels additions from the neutral point), the partials meet in
+//   four levels of complete extended additions across lanes; Z^-1 runs on
+//   four lanes (mp::inv_plain_var4: Z is public); encode(R') == R (R26).
+constexpr uint32_t ED_SIG_CHARS = 88;
+template <int WA>
+__global__ void __launch_bounds__(SM_THREADS) k_ed_small(EdSmallArgs a) {
+  constexpr int NB = ed_windows(true), NA = ed_windows_w(WA), NW = NB > NA ? NB : NA, S = 16;
+  constexpr int K = (NW + S - 1) / S;            // windows per lane
+  __shared__ uint32_t in_w[SM_IN_DW];
+  __shared__ uint32_t sig_w[ED_SIG_CHARS / 4 + 2];
+  __shared__ uint8_t sig_b[3 * (ED_SIG_CHARS / 4) + 4];
+  __shared__ uint32_t dig_w[16];
+  __shared__ int32_t dg[NB + NA];
+  __shared__ int32_t flag[2];                    // [0] characters bad, [1] the token runs
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const JobDev jb = a.jobs[blockIdx.x];
+  const DevKey& Kk = a.keys[job_key(jb)];
+  const uint32_t nch = job_siglen(jb);
+  const bool in_ok = jb.sig_in_len <= SMALL_IN_MAX;
+  const uint32_t in_shift = (uint32_t)((uintptr_t)(a.arena + jb.off) & 3u);
+  const uint32_t sig_shift = (uint32_t)((uintptr_t)(a.arena + jb.sig_off) & 3u);
+  if (tid == 0) { flag[0] = 0; flag[1] = 0; }
+  if (wave == 0 && in_ok) {
+    sm_stage_input(in_w, reinterpret_cast<const uint32_t*>(a.arena + jb.off - in_shift), in_shift, jb.sig_in_len, 512,
+                   lane, 64);
+  } else if (wave == 1) {
+    const uint32_t* g = reinterpret_cast<const uint32_t*>(a.arena + jb.sig_off - sig_shift);
+    const uint32_t nd = nch <= ED_SIG_CHARS ? (sig_shift + nch + 3) / 4 : 0u;
+    if ((uint32_t)lane < nd) sig_w[lane] = g[lane];
+  }
+  __syncthreads();
+  const bool size_ok = nch <= ED_SIG_CHARS && (nch & 3u) != 1u && sm_b64_len(nch) == 64u;
+  if (wave == 1 && size_ok) {
+    if (sm_b64_decode(sig_w, sig_shift, nch, sig_b, lane) && lane == 0) flag[0] = 1;
+  }
+  __syncthreads();
+  const bool ok0 = in_ok && size_ok && flag[0] == 0 && Kk.valid != 0 && job_alg(jb) == 10;
+  if (ok0 && wave == 0 && lane == 0) {
+    // SHA-512(R || A || M): the 64-byte prefix as 16 big-endian words, then M
+    const uint32_t* A = a.keyblob + Kk.aux_off;
+    uint32_t pre[16];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      pre[t] = ((uint32_t)sig_b[4 * t] << 24) | ((uint32_t)sig_b[4 * t + 1] << 16) | ((uint32_t)sig_b[4 * t + 2] << 8) |
+               sig_b[4 * t + 3];
+      pre[8 + t] = sha2::bswap32(A[t]);
+    }
+    const uint32_t len = jb.sig_in_len, tot = len + 64;
+    uint64_t h[8];
+    sha2::sha512_init(h, false);
+    const uint32_t nblk = (tot + 17 + 127) / 128;
+#pragma unroll 1
+    for (uint32_t blk = 0; blk < nblk; ++blk) {
+      uint32_t v[32];
+      if (blk == 0) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) v[t] = mp::lane_value(pre[t]);
+        sm_words<16>(in_w, 0, in_shift, len, v + 16);
+      } else {
+        sm_words<32>(in_w, blk * 32 - 16, in_shift, len, v);
+      }
+      if (blk == nblk - 1) { v[30] = tot >> 29; v[31] = tot << 3; }
+      uint64_t w[16];
+#pragma unroll
+      for (int t = 0; t < 16; ++t) w[t] = ((uint64_t)v[2 * t] << 32) | v[2 * t + 1];
+      sha2::sha512_compress(h, w);
+    }
+    // k = H mod L (H little-endian, 512 bits; k_ed_point's reduction)
+    uint32_t hw[16], hl[2 * L];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      hw[2 * q] = sha2::bswap32((uint32_t)(h[q] >> 32));
+      hw[2 * q + 1] = sha2::bswap32((uint32_t)h[q]);
+    }
+    mp::words_to_limbs<2 * L, 16>(hl, hw);
+    uint64_t tt[2 * L];
+#pragma unroll
+    for (int j = 0; j < 2 * L; ++j) tt[j] = hl[j];
+    uint32_t kr[L], rr[L], k[L];
+    mp::mont_reduce<Fl>(kr, tt);
+    mp::set_const<Fl>(rr, Fl::RR);
+    mp::mul<Fl>(k, kr, rr);
+    mp::csub<Fl>(k);
+    recode<WA, NA>(dg + NB, k);
+  }
+  if (ok0 && wave == 1 && lane == 0) {
+    // S: canonical (S < L) and sig[63] & 0xE0 == 0 (R24)
+    uint32_t sw[8], sl[L], lord[L];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      sw[q] = (uint32_t)sig_b[32 + 4 * q] | ((uint32_t)sig_b[33 + 4 * q] << 8) | ((uint32_t)sig_b[34 + 4 * q] << 16) |
+              ((uint32_t)sig_b[35 + 4 * q] << 24);
+    mp::words_to_limbs<L, 8>(sl, sw);
+    mp::set_const<Fl>(lord, Fl::M);
+    const bool sok = (sw[7] & 0xE0000000u) == 0 && lt_limbs(sl, lord);
+    recode<ed_comb_w(true), NB>(dg, sl);
+    flag[1] = sok ? 1 : 0;
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  const bool run = ok0 && flag[1] != 0;          // block-uniform
+  FPt P;                                         // the neutral element (0, 1, 1, 0)
+  fe::set_small(P.X, 0u); fe::set_small(P.Y, 1u); fe::set_small(P.Z, 1u); fe::set_small(P.T, 0u);
+  if (run && lane < S) {
+    const uint32_t* __restrict__ atab = key_table(Kk);
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int w = lane + S * i;
+      if (w < NB) add_window<ed_entries(true)>(P, a.btab, w, dg[w]);
+      if (w < NA) add_window<(1 << (WA - 1))>(P, atab, w, dg[NB + w]);
+    }
+  }
+  // partials of lanes 0..15 added pairwise with the complete law (every lane joins the shuffles)
+#pragma unroll 1
+  for (int off = 1; off < S; off <<= 1) {
+    FPt Q;
+#pragma unroll
+    for (int j = 0; j < fe::L; ++j) {
+      Q.X[j] = __shfl_xor(P.X[j], off);
+      Q.Y[j] = __shfl_xor(P.Y[j], off);
+      Q.Z[j] = __shfl_xor(P.Z[j], off);
+      Q.T[j] = __shfl_xor(P.T[j], off);
+    }
+    add_ext(P, P, Q);
+  }
+  // Z^-1 on lanes 0..3 (lane 0's Z, plain limbs), then lane 0 encodes R'
+  uint32_t zm[L], zp[L], zl[L];
+  fe_to_mont(zm, P.Z);
+  mp::from_mont<Fp>(zp, zm);
+#pragma unroll
+  for (int j = 0; j < L; ++j) zl[j] = (uint32_t)__shfl((int)zp[j], 0);
+  if (lane >= 4) return;
+  uint32_t zi[L];
+  mp::inv_plain_var4<Fp>(zi, zl);
+  if (lane != 0) return;
+  bool ok = false;
+  if (run) {
+    uint32_t zim[L], X[L], Y[L], tt[L], x[L], y[L], enc[8];
+    mp::to_mont<Fp>(zim, zi);
+    fe_to_mont(X, P.X);
+    fe_to_mont(Y, P.Y);
+    mp::mul<Fp>(tt, X, zim); mp::from_mont<Fp>(x, tt);
+    mp::mul<Fp>(tt, Y, zim); mp::from_mont<Fp>(y, tt);
+    mp::limbs_to_words<L, 8>(enc, y);
+    enc[7] = (enc[7] & 0x7fffffffu) | ((x[0] & 1u) << 31);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      diff |= enc[q] ^ ((uint32_t)sig_b[4 * q] | ((uint32_t)sig_b[4 * q + 1] << 8) | ((uint32_t)sig_b[4 * q + 2] << 16) |
+                        ((uint32_t)sig_b[4 * q + 3] << 24));
+    ok = diff == 0;
+  }
+  a.verdict[a.out[blockIdx.x]] = ok ? 1 : 0;
+}
+
 // ------------------------------------------------------------------ staging
 __device__ void niels_entry(uint32_t* out, const EPt& P) {
   uint32_t zi[L], x[L], y[L], t[L], d2[L];
@@ -676,4 +838,16 @@ void launch_ed_btable(uint32_t* tab, hipStream_t s) {
   constexpr int NWIN = ed_windows(true), NE = ed_entries(true);
   hipLaunchKernelGGL(k_ed_table_base_b, dim3((NWIN + 63) / 64), dim3(64), 0, s, tab);
   hipLaunchKernelGGL(k_ed_table_b, dim3((NWIN * NE + 63) / 64), dim3(64), 0, s, tab);
+}
+
+void launch_ed_small(int wa, const EdSmallArgs& a, hipStream_t s) {
+  if (a.n == 0) return;
+  dim3 g(a.n), b(SM_THREADS);
+  switch (wa) {
+    case 24: hipLaunchKernelGGL(k_ed_small<24>, g, b, 0, s, a); break;
+    case 22: hipLaunchKernelGGL(k_ed_small<22>, g, b, 0, s, a); break;
+    case 20: hipLaunchKernelGGL(k_ed_small<20>, g, b, 0, s, a); break;
+    case 18: hipLaunchKernelGGL(k_ed_small<18>, g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL(k_ed_small<16>, g, b, 0, s, a); break;
+  }
 }

@@ -55,3 +55,21 @@ void launch_ed_keyprep(jgk::DevKey* keys, uint32_t* blob, const int32_t* idx, in
 void launch_ed_keytables(int wa, jgk::DevKey* keys, uint32_t* blob, const int32_t* tidx, int tn, hipStream_t s,
                          bool sliced = false);
 void launch_ed_btable(uint32_t* tab, hipStream_t s);
+
+// One-launch verification of a small batch of EdDSA tokens (k_ed_small,
+// ed25519.hip): one two-wave block per token -- SHA-512(R || A || M) on one
+// lane, the comb sum over 16 lanes with pairwise complete additions, Z^-1 by
+// the variable-time safegcd on four lanes, encode(R') == R -- writing
+// verdict[out[i]] (pinned host memory).  Every key of a launch has key-table
+// width `wa`.  Jobs in the arguments, arena read in place (as EcSmallArgs).
+struct EdSmallArgs {
+  const uint8_t* arena;
+  const jgk::DevKey* keys;
+  const uint32_t* keyblob;
+  const uint32_t* btab;
+  uint8_t* verdict;
+  uint32_t n;
+  jgk::JobDev jobs[jgk::SMALL_MAX];
+  uint16_t out[jgk::SMALL_MAX];
+};
+void launch_ed_small(int wa, const EdSmallArgs& a, hipStream_t s);

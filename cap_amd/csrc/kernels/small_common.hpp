@@ -59,11 +59,14 @@ __device__ __forceinline__ void sm_words(const uint32_t* lds, uint32_t w0, uint3
 // into LDS: the dwords holding message bytes, zeros up to the SHA stream of
 // hb bits (+ the alignbyte dword).  Only dwords that hold message bytes are
 // read (no load leaves the message's pages).  Eight loads in flight per lane.
+// `prefix`: bytes hashed before the message (Ed25519's R || A: 64), which
+// shift the stream's blocks.
 __device__ __forceinline__ void sm_stage_input(uint32_t* in_w, const uint32_t* g, uint32_t shift, uint32_t len,
-                                               int hb, int lane) {
+                                               int hb, int lane, uint32_t prefix = 0) {
   const uint32_t ndw = (shift + len + 3) / 4;
-  const uint32_t nblk = hb == 256 ? (len + 9 + 63) / 64 : (len + 17 + 127) / 128;
-  const uint32_t need = nblk * (hb == 256 ? 16u : 32u) + 1u;
+  const uint32_t tot = len + prefix;
+  const uint32_t nblk = hb == 256 ? (tot + 9 + 63) / 64 : (tot + 17 + 127) / 128;
+  const uint32_t need = nblk * (hb == 256 ? 16u : 32u) - prefix / 4 + 1u;
   for (uint32_t base = 0; base < need; base += 64 * 8) {
     uint32_t v[8];
 #pragma unroll

@@ -291,3 +291,51 @@ def _sub(arena, lo, hi):
         out.buf += arena.buf[off:off + rel + sl]
         out.toks.append((len(out.buf) - rel - sl, sil, rel, sl, key, alg))
     return out
+
+
+def test_golden_eddsa_tokens_small_path():
+    """EdDSA on every golden Ed25519 key (small-order and non-canonical A,
+    an invalid key) through k_ed_small, lone and in small batches: verdicts
+    equal to the fixture's, the oracle's and the chain's."""
+    from cap_amd import _lib
+    keys, toks = H.golden()
+    ed = {k["kid"] for k in keys if k["kty"] == "OKP"}
+    toks = [t for t in toks if t["key"] in ed]
+    assert len(toks) >= 15 and sum(t["verdict"] for t in toks) >= 5
+    kid_index = {k["kid"]: i for i, k in enumerate(keys)}
+    ctx = _lib.Context()
+    try:
+        ctx.load_keys([H.abi_key(k) for k in keys])
+        n0 = ctx.debug_small_path()
+        lone = _verify_each(ctx, toks, kid_index, 1)
+        few = _verify_each(ctx, toks, kid_index, 6)
+        assert ctx.debug_small_path() > n0
+        ctx.debug_small_path(False)
+        chain = _verify_each(ctx, toks, kid_index, 6)
+        ctx.debug_small_path(True)
+        bad = [t["name"] for t, a, b, c in zip(toks, lone, few, chain) if not a == b == c == t["verdict"]]
+        assert not bad, bad
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("wa", [24, 22, 20, 18, 16])
+def test_ed25519_comb_tier_small_path(wa):
+    """The Ed25519 comb-tier tokens (last table entry in k's windows at each
+    key width, in S's at the base table) through k_ed_small<wa>."""
+    import bench
+    from cap_amd import _lib
+    s = json.load(open(os.path.join(H.ROOT, "tests", "golden", "comb_tiers.json")))["ed25519"]
+    kid_index = {k["kid"]: i for i, k in enumerate(s["keys"])}
+    ctx = _lib.Context()
+    try:
+        ctx.set_table_budget(bench.table_bytes("ed25519", wa))
+        ctx.load_keys([H.abi_key(k) for k in s["keys"]])
+        assert ctx.table_widths() == [wa]
+        n0 = ctx.debug_small_path()
+        lone = _verify_each(ctx, s["tokens"], kid_index, 1)
+        batch = _verify_each(ctx, s["tokens"], kid_index, 64)
+        assert ctx.debug_small_path() - n0 >= len(s["tokens"])
+        assert lone == batch == [t["verdict"] for t in s["tokens"]]
+    finally:
+        ctx.close()
