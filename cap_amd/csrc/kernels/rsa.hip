@@ -141,21 +141,31 @@ __device__ __forceinline__ void limb_shift(uint64_t* T, bool lane0, uint32_t mla
 #endif
 }
 
+// The row's Montgomery digit m from group lane 0 to the group: a DPP / ds_swizzle
+// broadcast, or -- ONE: the wave runs a single token (k_rsa_small, every group
+// a copy of group 0) -- v_readfirstlane, so m is an SGPR operand and the row's
+// dependent chain skips the swizzle's LDS-path latency.
+template <int G, bool ONE>
+__device__ __forceinline__ uint32_t row_digit(uint32_t x) {
+  if constexpr (ONE) return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+  else return bcast0<G>(x);
+}
+
 // One CIOS iteration on this lane's window T[0..H) of the token's accumulator.
 //   T += a_i * v ; m = T0 * n' (group lane 0, broadcast) ; T += m * n ;
 //   lane 0: T1 += T0 >> 28 ; every lane hands T0 to the lane below, which
 //   places it in its fresh top slot T[H] (the limb shift across lanes).
-template <int H, int G>
+template <int H, int G, bool ONE = false>
 __device__ __forceinline__ void cios_step(uint64_t* T, uint32_t ai, const uint32_t* v, const uint32_t* n,
                                           uint32_t np, bool lane0, uint32_t mlast) {
 #if JG_RSA_BLOCKS
   madv_run(T, ai, v, H);
-  const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
+  const uint32_t m = row_digit<G, ONE>(((uint32_t)T[0] * np) & M28);
   madv_run(T, m, n, H);
 #else
 #pragma unroll
   for (int j = 0; j < H; ++j) mad64(T[j], ai, v[j], j & 1);
-  const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
+  const uint32_t m = row_digit<G, ONE>(((uint32_t)T[0] * np) & M28);
 #pragma unroll
   for (int j = 0; j < H; ++j) mad64(T[j], m, n[j], 2 + (j & 1));
 #endif
@@ -192,7 +202,7 @@ __device__ __forceinline__ void finish_product(uint32_t* v, const uint64_t* P, u
 // v <- (a * v) / R mod n with a streamed from LDS (la[i * TPW], shared by the
 // group's lanes: a broadcast read).  R = 2^(28 H G).  In: v < 2n limb-normalized.
 // Out: v < 2n, limbs < 2^28 (carries rippled across the group).
-template <int H, int G, int U, int TPW>
+template <int H, int G, int U, int TPW, bool ONE = false>
 __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const uint32_t* n, uint32_t np,
                                          bool lane0, uint32_t mlast, uint32_t ml0) {
   constexpr int L = H * G, NB = L / U, REM = L % U;
@@ -204,7 +214,7 @@ __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const 
 #pragma unroll
     for (int u = 0; u < U; ++u) a[u] = la[(ib * U + u) * TPW];
 #pragma unroll
-    for (int u = 0; u < U; ++u) cios_step<H, G>(P + u, a[u], v, n, np, lane0, mlast);
+    for (int u = 0; u < U; ++u) cios_step<H, G, ONE>(P + u, a[u], v, n, np, lane0, mlast);
     if constexpr (2 * L > 250) {
       // keep every 64-bit column < 2^64: a row adds two products of < 2^56 to
       // each column, so normalise within the lane every 80 rows (RSA-4K: once,
@@ -220,7 +230,7 @@ __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const 
     for (int j = H; j < H + U; ++j) P[j] = 0;
   }
 #pragma unroll
-  for (int u = 0; u < REM; ++u) cios_step<H, G>(P + u, la[(NB * U + u) * TPW], v, n, np, lane0, mlast);
+  for (int u = 0; u < REM; ++u) cios_step<H, G, ONE>(P + u, la[(NB * U + u) * TPW], v, n, np, lane0, mlast);
   finish_product<H, G>(v, P + REM, ml0);
 }
 
@@ -239,7 +249,7 @@ __device__ __forceinline__ void mont_mul(uint32_t* v, const uint32_t* la, const 
 // same column totals as the full product.  The x loop is unrolled (the
 // triangle needs compile-time register indices), the r loop is not: one
 // physical shift of the window per H rows.
-template <int H, int G, int TPW>
+template <int H, int G, int TPW, bool ONE = false>
 __device__ __forceinline__ void mont_sqr(uint32_t* v, const uint32_t* la, const uint32_t* n, uint32_t np, int g,
                                          bool lane0, uint32_t mlast, uint32_t ml0) {
   constexpr int L = H * G;
@@ -259,12 +269,12 @@ __device__ __forceinline__ void mont_sqr(uint32_t* v, const uint32_t* la, const 
       const uint32_t a2 = ai << 1;
 #if JG_RSA_BLOCKS
       madv_run(T + x + 1, a2, v + x + 1, H - x - 1);
-      const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
+      const uint32_t m = row_digit<G, ONE>(((uint32_t)T[0] * np) & M28);
       madv_run(T, m, n, H);
 #else
 #pragma unroll
       for (int k = x + 1; k < H; ++k) mad64(T[k], a2, v[k], SQR_SLOT(k));
-      const uint32_t m = bcast0<G>(((uint32_t)T[0] * np) & M28);
+      const uint32_t m = row_digit<G, ONE>(((uint32_t)T[0] * np) & M28);
 #pragma unroll
       for (int k = 0; k < H; ++k) mad64(T[k], m, n[k], SQR_SLOT(k + 2));
 #endif
@@ -768,8 +778,8 @@ __global__ void __launch_bounds__(SM_THREADS) k_rsa_small(RsaSmallArgs a) {
 #pragma unroll
         for (int j = 0; j < H; ++j) v[j] = (j == 0 && lane0) ? 1u : 0u;
       }
-      if (op == SQUARE) mont_sqr<H, G, TPW>(v, la, n, np28, g, lane0, mlast, ml0);
-      else mont_mul<H, G, U, TPW>(v, la, n, np28, lane0, mlast, ml0);
+      if (op == SQUARE) mont_sqr<H, G, TPW, true>(v, la, n, np28, g, lane0, mlast, ml0);
+      else mont_mul<H, G, U, TPW, true>(v, la, n, np28, lane0, mlast, ml0);
       if (op == TOMONT) {
 #pragma unroll
         for (int j = 0; j < H; ++j) xm[j] = v[j];

@@ -137,7 +137,7 @@ def test_exceptional_tokens_small_path(budget):
 
 
 def test_long_signing_input_and_mixed_batches_fall_back():
-    """A signing input past EC_SMALL_IN_MAX (8 KiB) and a batch with RSA jobs
+    """A signing input past SMALL_IN_MAX (8 KiB) and a batch with PS256 jobs
     take the batch chain; verdicts stay exact."""
     import bench
     from cap_amd import _lib
@@ -161,8 +161,8 @@ def test_long_signing_input_and_mixed_batches_fall_back():
         n0 = ctx.debug_small_path()
         assert list(ctx.verify(arena)) == [1, 1, 0]
         assert ctx.debug_small_path() == n0
-        # RSA + ECDSA in one small batch: the chain, exact verdicts
-        rs = [t for t in toks if t["alg"] == "RS256"][:3]
+        # RSASSA-PSS + ECDSA in one small batch: the chain (k_rsa_small is PKCS#1 v1.5 only)
+        rs = [t for t in toks if t["alg"] == "PS256"][:3]
         es = [t for t in toks if t["alg"] == "ES256"][:3]
         mix = rs + es
         arena, slots = H.jobs_from_tokens(mix, kid_index)
