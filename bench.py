@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 KEYDIR = os.path.join(ROOT, "tests", "golden", "keys")
 BENCHKEYS = os.path.join(ROOT, "tools", "benchkeys")
 TOKGEN = os.path.join(ROOT, "tools", "tokgen", "tokgen")
-TRAFFIC = os.path.join(ROOT, "profiles", "r06_s3_pmc_traffic.json")
+TRAFFIC = os.path.join(ROOT, "profiles", "r06_s12_pmc_traffic.json")
 COLL_DEVICE = "cuda"            # device of the timing all-reduce (RCCL); "cpu" under gloo
 
 # measured v_mad_u64_u32 issue rate, chip-wide: the integer multiply-add
@@ -141,12 +141,12 @@ P384_BUDGET = 32 << 30    # main() sets the run's table budget
 
 
 def p384_point_mads_per_token(wq=None, nkeys=1):
-    """P-384 (ecdsa.hpp: L = 15 28-bit limbs, G W = 20, key W = 24 / 20 / 18 / 16
+    """P-384 (ecdsa.hpp: L = 15 28-bit limbs, G W = 24 (20 before round 6), key W = 24 / 20 / 18 / 16
     by the table budget -- 24 for config 3's single key): the hot loop's mulf /
     sqrf use the special-form reduction, 4 signed MADs per row (mp.hpp
     mont_reduce_p384); value folds through freduce (5 non-zero constants of
     2^384 mod p); final check with m+1's 12 non-zero limbs."""
-    return ec_point_mads_per_token(15, 4, 5, 20, wq or p384_key_w(nkeys, P384_BUDGET), 384, 15 * 12, merged=False)
+    return ec_point_mads_per_token(15, 4, 5, 24, wq or p384_key_w(nkeys, P384_BUDGET), 384, 15 * 12, merged=False)
 
 
 def p521_key_w(nkeys, budget):

@@ -58,13 +58,14 @@ constexpr int ec_order_bits(int cls) { return cls == jgk::CLS_P256 ? 256 : cls =
 // hundreds of keys still fits:
 //   P-256: G W=26 (10 windows, 21.5 GB packed), keys W=20 (13 windows, 436 MB each):
 //          22 additions per token (23 with G W=24, 25 with W=20/20, ~32 with 16/16)
-//   P-384: G W=20 (20 windows, 1.3 GB), keys W=16 (25 windows, 105 MB): 44 (65 at 12/12)
+//   P-384: G W=24 (17 windows, 18.3 GB), keys W=16 (25 windows, 105 MB): 41 (65 at 12/12);
+//          round 6 widened G from 20 (20 windows, 1.3 GB): 3 additions fewer per token
 //   P-521: G W=20 (27 windows, 2.3 GB), keys W=16 (33 windows, 173 MB): 59 (87 at 12/12)
 // The top window of each scalar (u < n) never carries out of the last digit.
 // ec_comb_w(cls, false) is the narrowest key window; P-256 keys get a wider
 // one when few keys share the context's table budget (ec_key_w below).
 constexpr int ec_comb_w(int cls, bool gen) {
-  return cls == jgk::CLS_P256 ? (gen ? 26 : 20) : (gen ? 20 : 16);
+  return cls == jgk::CLS_P256 ? (gen ? 26 : 20) : cls == jgk::CLS_P384 ? (gen ? 24 : 16) : (gen ? 20 : 16);
 }
 // Windows per scalar: ceil((bits + 2) / W).  The signed recoding carries +1
 // into the next window whenever a window's value reaches 2^(W-1), so the top

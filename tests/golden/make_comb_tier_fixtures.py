@@ -16,8 +16,8 @@ the scalars are u1 = e/s (generator table, width wg) and u2 = r/s (key table,
 width wq).  For chosen u1, u2 and a message with hash e: s = e/u1, r = u2 s;
 lift a point R0 with x(R0) = r; the key is Q = u2^-1 (R0 - u1 G).  Then
 u1 G + u2 Q = R0 and Go accepts.  One key per token; for every tier
-(P-256 wq 26/24/22/20 with wg 26; P-384 wq 24/20/18/16 and P-521 wq
-20/18/16 with wg 20) six tokens:
+(P-256 wq 26/24/22/20 with wg 26; P-384 wq 24/20/18/16 with wg 24 (20 before
+round 6); P-521 wq 20/18/16 with wg 20) six tokens:
   edge-first-mid  digit -2^(W-1) (the last entry) in window 0 and a middle window
   edge-every      digit -2^(W-1) in every window below the top one
   top-carry       u = n - 1 - x: the top window all ones with a carry in
@@ -40,7 +40,9 @@ and tokens whose s has it in window 0 or a middle window of the base-point
 table (W = 24).  Verdicts: encode([s]B - [k]A) == R (cofactorless), plus an
 s + 1 copy of each.
 
-Usage: python tests/golden/make_comb_tier_fixtures.py
+Usage: python tests/golden/make_comb_tier_fixtures.py [--only CURVE]
+  --only P-384: rebuild that curve's EC tiers (its own RNG stream) and keep
+  every other entry of the committed comb_tiers.json (the Ed25519 scan is slow)
 """
 import hashlib
 import json
@@ -54,7 +56,7 @@ sys.path.insert(0, HERE)
 from make_fixtures import CURVES, claims, enc_json, b64u, ED_L, ED_B, ed_add, ed_mul, ed_encode  # noqa: E402
 from make_ec_edge_fixtures import GEN, ec_add, ec_mul, ec_neg, on_curve, lift_x, go_verify, hash_e  # noqa: E402
 
-EC_TIERS = {"P-256": (26, (26, 24, 22, 20)), "P-384": (20, (24, 20, 18, 16)), "P-521": (20, (20, 18, 16))}
+EC_TIERS = {"P-256": (26, (26, 24, 22, 20)), "P-384": (24, (24, 20, 18, 16)), "P-521": (20, (20, 18, 16))}
 ED_WB, ED_TIERS = 24, (24, 22, 20, 18, 16)
 ALG_OF = {"P-256": "ES256", "P-384": "ES384", "P-521": "ES512"}
 SIZE = {"ES256": 32, "ES384": 48, "ES512": 66}
@@ -291,7 +293,31 @@ def scan_ed(workers=8, chunk=400_000, max_rounds=60):
     return key, toks
 
 
+def hash_seed(name):
+    return int.from_bytes(hashlib.sha256(name.encode()).digest()[:4], "big")
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--only":
+        only = sys.argv[2]
+        path = os.path.join(HERE, "comb_tiers.json")
+        out = json.load(open(path))
+        rng = random.Random(0xC0B ^ hash_seed(only))
+        wg, tiers = EC_TIERS[only]
+        fresh = []
+        for wq in tiers:
+            keys, toks = [], []
+            for i, kind in enumerate(("edge-first-mid", "edge-every", "top-carry", "zeros", "sparse", "max-pos")):
+                k, t = craft_ec(only, wg, wq, kind, i, rng)
+                keys.append(k)
+                toks += t
+            fresh.append(dict(crv=only, wg=wg, wq=wq, keys=keys, tokens=toks))
+            print(f"{only} wq={wq}: {len(keys)} keys, {len(toks)} tokens", flush=True)
+        it = iter(fresh)
+        out["ec"] = [next(it) if e["crv"] == only else e for e in out["ec"]]
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        return
     rng = random.Random(0xC0B)
     out = {"note": "comb-boundary fixtures per key-table width tier; made by make_comb_tier_fixtures.py",
            "ec": [], "ed25519": None}

@@ -50,7 +50,7 @@ GEN = {
               int("011839296a789a3bc0045c8a5fb42c7d1bd998f54449579b446817afbd17273e"
                   "662c97ee72995ef42640c550b9013fad0761353c7086a272c24088be94769fd16650", 16)),
 }
-COMB_W = {"P-256": (26, 20), "P-384": (20, 16), "P-521": (20, 16)}   # (generator, key) -- ecdsa.hpp
+COMB_W = {"P-256": (26, 20), "P-384": (24, 16), "P-521": (20, 16)}   # (generator, key) -- ecdsa.hpp
 ALG_OF = {"P-256": "ES256", "P-384": "ES384", "P-521": "ES512"}
 SIZE = {"ES256": 32, "ES384": 48, "ES512": 66}
 HASH = {"ES256": hashlib.sha256, "ES384": hashlib.sha384, "ES512": hashlib.sha512}

@@ -252,7 +252,7 @@ def test_generator_table_entries(tk, cid):
     p, L = c["p"], c["L"]
     R = 1 << (W * L)
     G = (c["gx"], c["gy"])
-    cw = {1: 26, 2: 20, 3: 20}[cid]                 # ecdsa.hpp ec_comb_w(cls, gen=true)
+    cw = {1: 26, 2: 24, 3: 20}[cid]                 # ecdsa.hpp ec_comb_w(cls, gen=true)
     nwin = -(-(c["n"].bit_length() + 1) // cw)
     ne = 1 << (cw - 1)
     wd = [(0, 1), (0, 2), (0, ne), (1, 1), (1, ne - 1), (5, 64), (nwin - 1, 1), (nwin - 1, ne), (nwin // 2, 77)]
