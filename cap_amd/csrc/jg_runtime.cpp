@@ -80,7 +80,7 @@ bool pipe_trace() {
 hipEvent_t g_trace_ref = nullptr;     // first chunk's H2D start (trace only)
 
 // CAPJWT_RELEASE_GTABLES=1: free a device's fixed-base tables when the last
-// context using them is destroyed (default: kept for the process, ~31 GB per device)
+// context using them is destroyed (default: kept for the process, ~54 GB per device)
 bool release_gtables() {
   static const bool on = [] {
     const char* e = std::getenv("CAPJWT_RELEASE_GTABLES");
@@ -473,7 +473,7 @@ using KeyStateP = std::shared_ptr<const KeyState>;
 // Fixed-base tables of the curve generators / Ed25519 base point depend only
 // on (device, curve): every jg_ctx of the process shares one copy per device,
 // built on first use and kept for the life of the process (they are constants
-// of the curves: ~31 GB per device with all four, the P-256 one 21.5 GB and
+// of the curves: ~54 GB per device with all four, the P-256 one 21.5 GB and
 // ~1.1 s to build -- a process that opens and closes contexts must not pay
 // that again).  Deliberately never freed: the cache outlives static
 // destruction, and the driver reclaims device memory at process exit.

@@ -223,7 +223,7 @@ int jg_set_zero_copy(jg_ctx* ctx, int enable, size_t max_jobs);
  * bench.py key_widths mirrors the rule (tests/test_bench_contract.py).
  * New tables are also sized against free HBM: a load narrows them rather than
  * fail.  Besides the budget, each device holds the generator / base-point
- * tables (about 31 GB with all four curves) for the life of the process
+ * tables (about 54 GB with all four curves) for the life of the process
  * (CAPJWT_RELEASE_GTABLES=1 frees them with the last context).  Returns 0 or -1. */
 int jg_set_table_budget(jg_ctx* ctx, uint64_t bytes);
 
