@@ -2798,9 +2798,25 @@ std::shared_ptr<Ticket> submit_to(jg_ctx* ctx, const KeyStateP& ks, const uint8_
   for (size_t k = 0, i = 0; k < nd && i < items.size(); ++k) {
     if (cut[k + 1] <= cut[k]) continue;
     Device* d = ctx->devs[k].get();
+    Item& it = items[i++];
+    // A small submission (coalesced single-token calls) on a device with
+    // nothing queued is planned and issued on the calling thread: one thread
+    // hand-off fewer on its round trip (the submission thread's wake-up).
+    // The device mutex still orders it against the submission thread.
+    if (it.nchunks == 1 && it.hi - it.lo <= SMALL_SUBMIT) {
+      bool idle;
+      {
+        std::lock_guard<std::mutex> g(d->qmu);
+        idle = d->q.empty();
+      }
+      if (idle) {
+        process_item(d, k, it);
+        continue;
+      }
+    }
     {
       std::lock_guard<std::mutex> g(d->qmu);
-      d->q.push_back(std::move(items[i++]));
+      d->q.push_back(std::move(it));
     }
     d->qcv.notify_one();
   }
