@@ -23,7 +23,7 @@ def child():
     from cap_amd import _lib
     alg = os.environ.get("AB_ALG", "EdDSA")
     kid, mark, madf = ALGS[alg]
-    n = 1 << 20
+    n = int(os.environ.get("AB_N", 1 << 20))              # AB_N: tokens per launch
     pool = bench.gen_tokens(alg, n, bench.golden_keypaths([kid]), 16, "ab" + alg)
     ctx = _lib.Context()
     ctx.set_table_budget(32 << 30)
