@@ -876,7 +876,57 @@ __global__ void __launch_bounds__(64) k_ec_exact(EcArgs a) {
 // S partial chains of NWIN / S additions run side by side, so a token's
 // latency is ~1/S of k_ec_point's plus log2(S) additions; the work per token
 // grows by those additions and the conversions to normalized form.
-template <class CV, int S>
+// Raw table entry for the prefetching chain: the packed words (P-256) or the
+// 2L limbs, converted at use
+template <class CV>
+struct RawEnt {
+  static constexpr int NW = ec_packed(CV::CLS) ? 16 : 2 * CV::Fp::L;
+  uint32_t w[NW];
+};
+template <class CV>
+__device__ __forceinline__ void load_ent(RawEnt<CV>& r, const uint32_t* __restrict__ ent) {
+  if constexpr (RawEnt<CV>::NW % 4 == 0) {
+    const uint4* e4 = reinterpret_cast<const uint4*>(ent);
+#pragma unroll
+    for (int i = 0; i < RawEnt<CV>::NW / 4; ++i) {
+      const uint4 q = e4[i];
+      r.w[4 * i] = q.x; r.w[4 * i + 1] = q.y; r.w[4 * i + 2] = q.z; r.w[4 * i + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < RawEnt<CV>::NW; ++i) r.w[i] = ent[i];
+  }
+}
+template <class CV>
+__device__ __forceinline__ void add_ent(uint32_t* X, uint32_t* Y, uint32_t* Z, bool& empty, const RawEnt<CV>& r, int d) {
+  using Fp = typename CV::Fp;
+  constexpr int L = Fp::L;
+  if (d == 0) return;
+  uint32_t x2[L], y2[L];
+  if constexpr (ec_packed(CV::CLS)) {
+    mp::words_to_limbs<L, 8>(x2, r.w);
+    mp::words_to_limbs<L, 8>(y2, r.w + 8);
+  } else {
+#pragma unroll
+    for (int j = 0; j < L; ++j) { x2[j] = r.w[j]; y2[j] = r.w[L + j]; }
+  }
+  if (d < 0) mp::neg<Fp>(y2, y2);
+  if (empty) {
+    mp::copy<Fp>(X, x2);
+    mp::copy<Fp>(Y, y2); mp::freduce<Fp>(Y);
+    mp::set_const<Fp>(Z, Fp::ONE);
+    empty = false;
+  } else {
+    madd<Fp>(X, Y, Z, x2, y2);
+  }
+}
+
+// PF (launches of about one wave per SIMD, JG_EC_PF_MAX): the lane's chain
+// of additions runs one table entry and two digits ahead -- addition j
+// computes while entry j + 1 and digit j + 2 load.  With no other wave on the
+// SIMD to switch to, each addition otherwise waited on a digit load and then
+// on the dependent entry gather.
+template <class CV, int S, bool PF = false>
 __global__ void __launch_bounds__(64) k_ec_point_split(EcArgs a) {
   using Fp = typename CV::Fp;
   using Fn = typename CV::Fn;
@@ -903,9 +953,38 @@ __global__ void __launch_bounds__(64) k_ec_point_split(EcArgs a) {
     const uint32_t* __restrict__ gtab = a.gtab;
     uint32_t X[L], Y[L], Z[L];
     bool empty = true;
+    if constexpr (PF) {
+      // step j: window sub + S (j / 2), the G comb (even j) or the Q comb (odd j)
+      constexpr int STRIDE = ec_stride(CV::CLS), NEG = ec_entries(CV::CLS, true), NEQ = 1 << (CV::WQ - 1);
+      const int nsteps = sub < NWIN ? 2 * ((NWIN - sub + S - 1) / S) : 0;
+      auto dig = [&](int j) {
+        const int w = sub + S * (j >> 1);
+        const bool q = j & 1;
+        return w < (q ? NQ : NG) ? (int)a.digs[(int64_t)(q ? NG + w : w) * np + p] : 0;
+      };
+      auto ent = [&](int j, int d) {
+        const int ad = d < 0 ? -d : d;
+        const int w = ad ? sub + S * (j >> 1) : 0;      // a zero digit loads window 0's first entry (unused)
+        const int64_t i = ad ? ad - 1 : 0;
+        return (j & 1) ? qtab + ((int64_t)w * NEQ + i) * STRIDE : gtab + ((int64_t)w * NEG + i) * STRIDE;
+      };
+      RawEnt<CV> rn;
+      int dn = nsteps > 0 ? dig(0) : 0, dnn = nsteps > 1 ? dig(1) : 0;
+      if (nsteps > 0) load_ent<CV>(rn, ent(0, dn));
+#pragma unroll 1
+      for (int j = 0; j < nsteps; ++j) {
+        const RawEnt<CV> rc = rn;
+        const int dc = dn;
+        dn = dnn;
+        if (j + 1 < nsteps) load_ent<CV>(rn, ent(j + 1, dn));
+        if (j + 2 < nsteps) dnn = dig(j + 2);
+        add_ent<CV>(X, Y, Z, empty, rc, dc);
+      }
+    } else {
     for (int w = sub; w < NWIN; w += S) {
       if (w < NG) add_window<CV, true>(X, Y, Z, empty, gtab, w, (int)a.digs[(int64_t)w * np + p]);
       if (w < NQ) add_window<CV, false>(X, Y, Z, empty, qtab, w, (int)a.digs[(int64_t)(NG + w) * np + p]);
+    }
     }
     if (!empty) {
       mp::canon<Fp>(X); mp::canon<Fp>(Y); mp::canon<Fp>(Z);
@@ -1108,6 +1187,14 @@ constexpr int64_t EC_SCALAR_SOLO_MAX = JG_EC_SCALAR_SOLO_MAX;   // launches up t
 #define JG_EC_SPLIT2_P256 131072
 #endif
 constexpr int64_t EC_SPLIT2_MAX_P256 = JG_EC_SPLIT2_P256;
+// Launches above the split sizes and up to JG_EC_PF_MAX padded tokens (a
+// mixed batch's EC classes, ~1 wave per SIMD) run the prefetching chain:
+// k_ec_point_split<CV, 2, true> for P-256 (up to EC_SPLIT2_MAX_P256), <CV, 1,
+// true> otherwise (one lane per token, as k_ec_point)
+#ifndef JG_EC_PF_MAX
+#define JG_EC_PF_MAX 131072
+#endif
+constexpr int64_t EC_PF_MAX_TOKENS = JG_EC_PF_MAX;
 constexpr int EC_SPLIT = JG_EC_SPLIT;                    // lanes per token of k_ec_point_split
 constexpr int64_t EC_SPLIT_MAX_TOKENS = JG_EC_SPLIT_MAX;  // launches up to this many padded tokens use it
 
@@ -1146,9 +1233,19 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   }
   if constexpr (CV::CLS == jgk::CLS_P256 && EC_SPLIT2_MAX_P256 > 0) {
     if (!launched && n <= EC_SPLIT2_MAX_P256) {
-      hipLaunchKernelGGL((k_ec_point_split<CV, 2>), dim3((unsigned)((n * 2 + WAVE - 1) / WAVE)), b, 0, s, a);
+      if (n <= EC_PF_MAX_TOKENS)
+        hipLaunchKernelGGL((k_ec_point_split<CV, 2, true>), dim3((unsigned)((n * 2 + WAVE - 1) / WAVE)), b, 0, s, a);
+      else
+        hipLaunchKernelGGL((k_ec_point_split<CV, 2>), dim3((unsigned)((n * 2 + WAVE - 1) / WAVE)), b, 0, s, a);
       launched = true;
     }
+  }
+  // P-521's chain takes 256 VGPRs with the prefetch (one wave per SIMD, 200
+  // without): only launches of under ~one wave per SIMD
+  constexpr int64_t pf_max = CV::CLS == jgk::CLS_P521 ? EC_PF_MAX_TOKENS / 2 : EC_PF_MAX_TOKENS;
+  if (!launched && n <= pf_max) {
+    hipLaunchKernelGGL((k_ec_point_split<CV, 1, true>), dim3((unsigned)((n + WAVE - 1) / WAVE)), b, 0, s, a);
+    launched = true;
   }
   if (!launched) hipLaunchKernelGGL(k_ec_point<CV>, g, b, 0, s, a);
   mk("point");

@@ -74,17 +74,20 @@ def test_ecdsa_comb_tier(crv, wq):
         ctx.close()
 
 
+@pytest.mark.parametrize("n", [40000, 140000])
 @pytest.mark.parametrize("crv,wq", _ec_tiers())
-def test_ecdsa_comb_tier_mid_launch(crv, wq):
+def test_ecdsa_comb_tier_mid_launch(crv, wq, n):
     """The same tokens tiled to ~40 k jobs, so the class launch is past the
     4-lane split's 16 k: P-256 runs the 2-lane k_ec_point_split, P-384 and
-    P-521 the one-lane k_ec_point (ecdsa_impl.hpp launch_chain); every
-    verdict equals the fixture's."""
+    P-521 its one-lane form, both with the prefetching chain (PF, up to 128 k
+    / 64 k tokens); at ~140 k jobs P-256 runs the 2-lane split without PF and
+    P-384 / P-521 k_ec_point (ecdsa_impl.hpp launch_chain).  Every verdict
+    equals the fixture's."""
     import bench
     from cap_amd import _lib
     s = next(x for x in fixtures()["ec"] if x["crv"] == crv and x["wq"] == wq)
     keys = s["keys"]
-    reps = 40000 // len(s["tokens"]) + 1
+    reps = n // len(s["tokens"]) + 1
     toks = s["tokens"] * reps
     assert len(toks) > 16384 * 2
     kid_index = {k["kid"]: i for i, k in enumerate(keys)}
@@ -167,15 +170,17 @@ def test_mixed_width_class_with_exceptions_in_both_runs():
         ctx.close()
 
 
+@pytest.mark.parametrize("n", [20000, 140000])
 @pytest.mark.parametrize("wa", [24, 20, 16])
-def test_ed25519_comb_tier_large_launch(wa):
+def test_ed25519_comb_tier_large_launch(wa, n):
     """The tier's edge tokens tiled past 16 k jobs, so the class launch runs
-    k_ed_point (one lane per token) instead of the 4-lane k_ed_point_split
-    that every smaller launch takes (ed25519.hip launch_ed)."""
+    one lane per token instead of the 4-lane k_ed_point_split that every
+    smaller launch takes: k_ed_point_pf (entries prefetched) up to 128 k
+    tokens, k_ed_point above (ed25519.hip launch_ed)."""
     import bench
     from cap_amd import _lib
     s = fixtures()["ed25519"]
-    reps = 20000 // len(s["tokens"]) + 1
+    reps = n // len(s["tokens"]) + 1
     toks = s["tokens"] * reps
     assert len(toks) > 16384
     kid_index = {k["kid"]: i for i, k in enumerate(s["keys"])}

@@ -42,7 +42,7 @@ def main():
         return child()
     out, specs = sys.argv[1], [a.split("=", 1) for a in sys.argv[2:]]
     res = {}
-    for rep in range(3):
+    for rep in range(int(os.environ.get("AB_REPS", 3))):
         for name, lib in specs:
             env = dict(os.environ, CAPJWT_LIB=os.path.join(ROOT, lib))
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env, capture_output=True,
