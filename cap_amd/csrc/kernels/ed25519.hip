@@ -172,8 +172,45 @@ __device__ __forceinline__ void recode(int* dg, const uint32_t* s, int stride = 
 #ifndef JG_ED_POINT_ATTR
 #define JG_ED_POINT_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
-template <int WA>
-__global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
+// One Niels addition of the table entry at e (30 words: y+x, y-x, 2dxy) for
+// digit d, from registers (k_ed_point's prefetching loop)
+__device__ __forceinline__ void add_entry(FPt& P, const uint32_t* e, int d) {
+  if (d == 0) return;
+  const bool neg = d < 0;
+  uint32_t a1[fe::L], a2[fe::L], nt[fe::L], t2d[fe::L];
+#pragma unroll
+  for (int j = 0; j < fe::L; ++j) t2d[j] = e[2 * fe::L + j];
+  fe::neg(nt, t2d);
+#pragma unroll
+  for (int j = 0; j < fe::L; ++j) {
+    a1[j] = neg ? e[fe::L + j] : e[j];
+    a2[j] = neg ? e[j] : e[fe::L + j];
+    t2d[j] = neg ? nt[j] : t2d[j];
+  }
+  add_niels(P, a1, a2, t2d);
+}
+
+// 30 words of a table entry as 7 x 16 B + 8 B loads
+struct EdEnt { uint4 q[7]; uint2 t; };
+__device__ __forceinline__ void load_ent(EdEnt& r, const uint32_t* __restrict__ ent) {
+  const uint4* e4 = reinterpret_cast<const uint4*>(ent);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) r.q[i] = e4[i];
+  r.t = reinterpret_cast<const uint2*>(ent)[14];
+}
+__device__ __forceinline__ void ent_words(uint32_t* w, const EdEnt& r) {
+#pragma unroll
+  for (int i = 0; i < 7; ++i) { w[4 * i] = r.q[i].x; w[4 * i + 1] = r.q[i].y; w[4 * i + 2] = r.q[i].z; w[4 * i + 3] = r.q[i].w; }
+  w[28] = r.t.x; w[29] = r.t.y;
+}
+
+// PF (launches below ~2 waves per SIMD, JG_ED_PF_MAX): the entry of addition
+// k + 1 is loaded while addition k computes.  At full occupancy other waves
+// hide the gathers' latency; a launch of under one wave per SIMD (configs[4]'s
+// Ed25519 class, ~38 k tokens) has no other wave, and its 22 additions each
+// waited ~2 us on their entry (k_ed_point ran at 0.20 of the MAD roofline).
+template <int WA, bool PF>
+__device__ __forceinline__ void ed_point_body(const EdArgs& a) {
   const int64_t p = a.begin + (int64_t)blockIdx.x * WAVE + threadIdx.x;
   const int64_t np = a.npad;
   const JobDev jb = a.jobs[p];
@@ -220,6 +257,34 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
   FPt P;                                      // the neutral element (0, 1, 1, 0)
   fe::set_small(P.X, 0u); fe::set_small(P.Y, 1u); fe::set_small(P.Z, 1u); fe::set_small(P.T, 0u);
   const uint32_t* __restrict__ atab = key_table(K);
+  if constexpr (PF) {
+    // additions k = 0 .. 2 NW - 1: B window k / 2 (even k), -A window k / 2 (odd)
+    constexpr int NEB = ed_entries(true), NEA = 1 << (WA - 1);
+    auto digit = [&](int k) {
+      const int w = k >> 1;
+      return (k & 1) ? (w < NA ? dg[(NB + w) * WAVE + lane] : 0) : (w < NB ? dg[w * WAVE + lane] : 0);
+    };
+    auto entry = [&](int k, int d) {
+      const int ad = d < 0 ? -d : d;
+      const int w = ad ? k >> 1 : 0;                 // a zero digit loads window 0's first entry (unused)
+      const int64_t i = ad ? ad - 1 : 0;
+      return (k & 1) ? atab + ((int64_t)w * NEA + i) * ED_STRIDE : a.btab + ((int64_t)w * NEB + i) * ED_STRIDE;
+    };
+    EdEnt rn;
+    int dn = digit(0);
+    load_ent(rn, entry(0, dn));
+#pragma unroll 1
+    for (int k = 0; k < 2 * NW; ++k) {
+      uint32_t e[30];
+      ent_words(e, rn);
+      const int dc = dn;
+      if (k + 1 < 2 * NW) {
+        dn = digit(k + 1);
+        load_ent(rn, entry(k + 1, dn));
+      }
+      add_entry(P, e, dc);
+    }
+  } else {
 #pragma unroll 1
   for (int w = 0; w < NW; ++w) {
     // each lane reads back only its own digits: no barrier needed
@@ -227,6 +292,7 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
     const int e2 = w < NA ? dg[(NB + w) * WAVE + lane] : 0;
     add_window<ed_entries(true)>(P, a.btab, w, e1);
     add_window<(1 << (WA - 1))>(P, atab, w, e2);
+  }
   }
 #pragma unroll
   for (int j = 0; j < fe::L; ++j) {                // radix-2^25.5 limbs (k_ed_finish converts)
@@ -237,6 +303,18 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
   if (!ok) a.status[p] = ST_REJECT;
 }
 
+template <int WA>
+__global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
+  ed_point_body<WA, false>(a);
+}
+#ifndef JG_ED_POINT_PF_ATTR
+#define JG_ED_POINT_PF_ATTR __attribute__((amdgpu_waves_per_eu(2)))
+#endif
+template <int WA>
+__global__ void __launch_bounds__(64) JG_ED_POINT_PF_ATTR k_ed_point_pf(EdArgs a) {
+  ed_point_body<WA, true>(a);
+}
+
 // k_ed_point with S lanes per token (S = 2 or 4), for launches that fill the
 // GPU poorly (a coalesced single-token batch, a mixed batch's Ed25519 class):
 // the first S/2 lanes sum the [S]B windows, the others the [k](-A) windows,
@@ -245,7 +323,9 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point(EdArgs a) {
 // the sum.  A token's latency falls to about 2/S of k_ed_point's for
 // log2(S) extra additions on its path (S - 1 in all).  The B-side lanes check
 // S, the A-side lanes derive k = H mod L.
-template <int WA, int S>
+// PF: the lane's next table entry loads while its current addition computes
+// (as k_ed_point_pf)
+template <int WA, int S, bool PF = false>
 __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point_split(EdArgs a) {
   static_assert(S == 2 || S == 4, "two or four lanes per token");
   constexpr int H = S / 2;                        // lanes per scalar
@@ -300,6 +380,29 @@ __global__ void __launch_bounds__(64) JG_ED_POINT_ATTR k_ed_point_split(EdArgs a
   if (live) {
     const uint32_t* __restrict__ tab = side ? key_table(K) : a.btab;
     const int ne = side ? (1 << (WA - 1)) : ed_entries(true);
+    if constexpr (PF) {
+      // step i: window par + H i (rows past the scalar's windows hold digit 0)
+      const int nst = par < NW ? (NW - par + H - 1) / H : 0;
+      auto entry = [&](int i, int d) {
+        const int ad = d < 0 ? -d : d;
+        const int w = ad ? par + H * i : 0;           // a zero digit loads window 0's first entry (unused)
+        return tab + ((int64_t)w * ne + (ad ? ad - 1 : 0)) * ED_STRIDE;
+      };
+      EdEnt rn;
+      int dn = nst > 0 ? dg[par * WAVE + lane] : 0;
+      if (nst > 0) load_ent(rn, entry(0, dn));
+#pragma unroll 1
+      for (int i = 0; i < nst; ++i) {
+        uint32_t e[30];
+        ent_words(e, rn);
+        const int dc = dn;
+        if (i + 1 < nst) {
+          dn = dg[(par + H * (i + 1)) * WAVE + lane];
+          load_ent(rn, entry(i + 1, dn));
+        }
+        add_entry(P, e, dc);
+      }
+    } else
 #pragma unroll 1
     for (int w = par; w < NW; w += H) {
       const int d = dg[w * WAVE + lane];        // this lane's own digit row: no barrier needed
@@ -766,16 +869,28 @@ __global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_
 #endif
 constexpr int64_t ED_SPLIT_MAX_TOKENS = JG_ED_SPLIT_MAX;  // launches up to this many padded tokens: k_ed_point_split
 constexpr int64_t ED_SPLIT4_MAX_TOKENS = JG_ED_SPLIT4_MAX;  // ... with 4 lanes per token above ED_SPLIT_MAX_TOKENS
+// launches up to this many padded tokens (above the split sizes): k_ed_point_pf
+#ifndef JG_ED_PF_MAX
+#define JG_ED_PF_MAX 131072
+#endif
+constexpr int64_t ED_PF_MAX_TOKENS = JG_ED_PF_MAX;
+// ... and up to this many: two lanes per token (k_ed_point_split<2, true>).
+// A/B knob, off: at configs[4]'s 38912-token class it ran 0.089 ms against
+// k_ed_point_pf's 0.069 (profiles/r06_s16/pf2.txt)
+#ifndef JG_ED_SPLIT2_PF_MAX
+#define JG_ED_SPLIT2_PF_MAX 0
+#endif
+constexpr int64_t ED_SPLIT2_PF_MAX_TOKENS = JG_ED_SPLIT2_PF_MAX;
 
-template <int S>
+template <int S, bool PF = false>
 void launch_ed_split(const EdArgs& a, int64_t waves, hipStream_t s) {
   dim3 g((unsigned)(S * waves)), b(WAVE);
   switch (a.wa) {
-    case 24: hipLaunchKernelGGL((k_ed_point_split<24, S>), g, b, 0, s, a); break;
-    case 22: hipLaunchKernelGGL((k_ed_point_split<22, S>), g, b, 0, s, a); break;
-    case 20: hipLaunchKernelGGL((k_ed_point_split<20, S>), g, b, 0, s, a); break;
-    case 18: hipLaunchKernelGGL((k_ed_point_split<18, S>), g, b, 0, s, a); break;
-    default: hipLaunchKernelGGL((k_ed_point_split<16, S>), g, b, 0, s, a); break;
+    case 24: hipLaunchKernelGGL((k_ed_point_split<24, S, PF>), g, b, 0, s, a); break;
+    case 22: hipLaunchKernelGGL((k_ed_point_split<22, S, PF>), g, b, 0, s, a); break;
+    case 20: hipLaunchKernelGGL((k_ed_point_split<20, S, PF>), g, b, 0, s, a); break;
+    case 18: hipLaunchKernelGGL((k_ed_point_split<18, S, PF>), g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL((k_ed_point_split<16, S, PF>), g, b, 0, s, a); break;
   }
 }
 
@@ -788,6 +903,16 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
     launch_ed_split<JG_ED_SPLIT_LANES>(a, waves, s);
   } else if (a.end - a.begin <= ED_SPLIT4_MAX_TOKENS) {
     launch_ed_split<4>(a, waves, s);
+  } else if (a.end - a.begin <= ED_SPLIT2_PF_MAX_TOKENS) {
+    launch_ed_split<2, true>(a, waves, s);
+  } else if (a.end - a.begin <= ED_PF_MAX_TOKENS) {
+    switch (a.wa) {
+      case 24: hipLaunchKernelGGL(k_ed_point_pf<24>, g, b, 0, s, a); break;
+      case 22: hipLaunchKernelGGL(k_ed_point_pf<22>, g, b, 0, s, a); break;
+      case 20: hipLaunchKernelGGL(k_ed_point_pf<20>, g, b, 0, s, a); break;
+      case 18: hipLaunchKernelGGL(k_ed_point_pf<18>, g, b, 0, s, a); break;
+      default: hipLaunchKernelGGL(k_ed_point_pf<16>, g, b, 0, s, a); break;
+    }
   } else {
   switch (a.wa) {
     case 24: hipLaunchKernelGGL(k_ed_point<24>, g, b, 0, s, a); break;
