@@ -1179,20 +1179,24 @@ constexpr int64_t EC_SCALAR_SOLO_MAX = JG_EC_SCALAR_SOLO_MAX;   // launches up t
 #ifndef JG_EC_SPLIT_MAX
 #define JG_EC_SPLIT_MAX 16384
 #endif
-// P-256 launches of 16 k ... 128 k tokens (a mixed batch's P-256 class) run
-// two lanes per token: point 0.30 -> 0.34-0.35 of the MAD roofline at
-// configs[4], the batch within the box noise (82.1 vs 81.4 / 84.2 M/s,
-// profiles/r05_s2/q_ab/); P-384 / P-521 lost there (split_ab) and stay whole.
+// P-256 launches of 16 k ... JG_EC_SPLIT2_P256 tokens run two lanes per token
+// (round 5: point 0.30 -> 0.34-0.35 of the MAD roofline at configs[4],
+// profiles/r05_s2/q_ab/).  Off since the prefetching one-lane chain (PF
+// below): 62 k ES256 tokens 0.1325 -> 0.1046 ms (0.33 -> 0.41), 125 k 0.218
+// -> 0.184 ms (0.40 -> 0.47) against the two-lane PF split
+// (profiles/r06_s16/pf3.txt).
 #ifndef JG_EC_SPLIT2_P256
-#define JG_EC_SPLIT2_P256 131072
+#define JG_EC_SPLIT2_P256 0
 #endif
 constexpr int64_t EC_SPLIT2_MAX_P256 = JG_EC_SPLIT2_P256;
 // Launches above the split sizes and up to JG_EC_PF_MAX padded tokens (a
-// mixed batch's EC classes, ~1 wave per SIMD) run the prefetching chain:
-// k_ec_point_split<CV, 2, true> for P-256 (up to EC_SPLIT2_MAX_P256), <CV, 1,
-// true> otherwise (one lane per token, as k_ec_point)
+// mixed batch's EC classes, ~1-4 waves per SIMD) run the prefetching chain
+// k_ec_point_split<CV, 1, true> (one lane per token, as k_ec_point)
+// (262 k-token launches: P-256 point 0.3467 -> 0.3428 ms, P-384 1.150 ->
+// 1.146 ms with it, profiles/r06_s16/pf4.txt; the 1 M headline launch keeps
+// k_ec_point and its four waves per SIMD)
 #ifndef JG_EC_PF_MAX
-#define JG_EC_PF_MAX 131072
+#define JG_EC_PF_MAX 262144
 #endif
 constexpr int64_t EC_PF_MAX_TOKENS = JG_EC_PF_MAX;
 constexpr int EC_SPLIT = JG_EC_SPLIT;                    // lanes per token of k_ec_point_split
@@ -1242,7 +1246,7 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   }
   // P-521's chain takes 256 VGPRs with the prefetch (one wave per SIMD, 200
   // without): only launches of under ~one wave per SIMD
-  constexpr int64_t pf_max = CV::CLS == jgk::CLS_P521 ? EC_PF_MAX_TOKENS / 2 : EC_PF_MAX_TOKENS;
+  constexpr int64_t pf_max = CV::CLS == jgk::CLS_P521 ? std::min<int64_t>(EC_PF_MAX_TOKENS, 65536) : EC_PF_MAX_TOKENS;
   if (!launched && n <= pf_max) {
     hipLaunchKernelGGL((k_ec_point_split<CV, 1, true>), dim3((unsigned)((n + WAVE - 1) / WAVE)), b, 0, s, a);
     launched = true;

@@ -551,7 +551,6 @@ __global__ void __launch_bounds__(SM_THREADS) k_ed_small(EdSmallArgs a) {
   __shared__ uint32_t in_w[SM_IN_DW];
   __shared__ uint32_t sig_w[ED_SIG_CHARS / 4 + 2];
   __shared__ uint8_t sig_b[3 * (ED_SIG_CHARS / 4) + 4];
-  __shared__ uint32_t dig_w[16];
   __shared__ int32_t dg[NB + NA];
   __shared__ int32_t flag[2];                    // [0] characters bad, [1] the token runs
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;

@@ -77,12 +77,11 @@ def test_ecdsa_comb_tier(crv, wq):
 @pytest.mark.parametrize("n", [40000, 140000])
 @pytest.mark.parametrize("crv,wq", _ec_tiers())
 def test_ecdsa_comb_tier_mid_launch(crv, wq, n):
-    """The same tokens tiled to ~40 k jobs, so the class launch is past the
-    4-lane split's 16 k: P-256 runs the 2-lane k_ec_point_split, P-384 and
-    P-521 its one-lane form, both with the prefetching chain (PF, up to 128 k
-    / 64 k tokens); at ~140 k jobs P-256 runs the 2-lane split without PF and
-    P-384 / P-521 k_ec_point (ecdsa_impl.hpp launch_chain).  Every verdict
-    equals the fixture's."""
+    """The same tokens tiled to ~40 k and ~140 k jobs, so the class launch is
+    past the 4-lane split's 16 k: every curve runs the one-lane prefetching
+    chain (k_ec_point_split<CV, 1, true>, up to 256 k tokens; P-521 up to
+    64 k), except P-521 at 140 k, which runs k_ec_point (ecdsa_impl.hpp
+    launch_chain).  Every verdict equals the fixture's."""
     import bench
     from cap_amd import _lib
     s = next(x for x in fixtures()["ec"] if x["crv"] == crv and x["wq"] == wq)
