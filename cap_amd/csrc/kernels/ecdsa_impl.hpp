@@ -1181,17 +1181,20 @@ constexpr int64_t EC_SCALAR_SOLO_MAX = JG_EC_SCALAR_SOLO_MAX;   // launches up t
 #endif
 // P-256 launches of 16 k ... JG_EC_SPLIT2_P256 tokens run two lanes per token
 // (round 5: point 0.30 -> 0.34-0.35 of the MAD roofline at configs[4],
-// profiles/r05_s2/q_ab/).  Off since the prefetching one-lane chain (PF
-// below): 62 k ES256 tokens 0.1325 -> 0.1046 ms (0.33 -> 0.41), 125 k 0.218
-// -> 0.184 ms (0.40 -> 0.47) against the two-lane PF split
-// (profiles/r06_s16/pf3.txt).
+// profiles/r05_s2/q_ab/), with the prefetch (PF below).  On one key at W = 24
+// the one-lane PF chain was faster (62 k tokens 0.1325 -> 0.1046 ms,
+// profiles/r06_s16/pf3.txt), but in configs[4] -- four keys at W = 26, 86 GB
+// of key tables, so slower gathers -- the class took 0.161 ms one-lane
+// against 0.153 two-lane (profiles/r06_s17 vs r06_s16/cfg_head.json): the
+// second wave per SIMD hides more of the gather than one entry of prefetch.
 #ifndef JG_EC_SPLIT2_P256
-#define JG_EC_SPLIT2_P256 0
+#define JG_EC_SPLIT2_P256 131072
 #endif
 constexpr int64_t EC_SPLIT2_MAX_P256 = JG_EC_SPLIT2_P256;
 // Launches above the split sizes and up to JG_EC_PF_MAX padded tokens (a
-// mixed batch's EC classes, ~1-4 waves per SIMD) run the prefetching chain
-// k_ec_point_split<CV, 1, true> (one lane per token, as k_ec_point)
+// mixed batch's EC classes, ~1-4 waves per SIMD) run the prefetching chain:
+// k_ec_point_split<CV, 2, true> for P-256 up to EC_SPLIT2_MAX_P256, <CV, 1,
+// true> otherwise (one lane per token, as k_ec_point)
 // (262 k-token launches: P-256 point 0.3467 -> 0.3428 ms, P-384 1.150 ->
 // 1.146 ms with it, profiles/r06_s16/pf4.txt; the 1 M headline launch keeps
 // k_ec_point and its four waves per SIMD)

@@ -78,9 +78,10 @@ def test_ecdsa_comb_tier(crv, wq):
 @pytest.mark.parametrize("crv,wq", _ec_tiers())
 def test_ecdsa_comb_tier_mid_launch(crv, wq, n):
     """The same tokens tiled to ~40 k and ~140 k jobs, so the class launch is
-    past the 4-lane split's 16 k: every curve runs the one-lane prefetching
-    chain (k_ec_point_split<CV, 1, true>, up to 256 k tokens; P-521 up to
-    64 k), except P-521 at 140 k, which runs k_ec_point (ecdsa_impl.hpp
+    past the 4-lane split's 16 k: P-256 runs the two-lane prefetching split
+    (k_ec_point_split<CV, 2, true>, up to 128 k tokens) and then the one-lane
+    prefetching chain (<CV, 1, true>, up to 256 k), P-384 the one-lane chain,
+    P-521 the one-lane chain at 40 k and k_ec_point at 140 k (ecdsa_impl.hpp
     launch_chain).  Every verdict equals the fixture's."""
     import bench
     from cap_amd import _lib
