@@ -38,7 +38,8 @@ MARKS = {
                    "void (anonymous namespace)::k_ec_point_split<(anonymous namespace)::CurveP384W<"],
     "p521_point": ["void (anonymous namespace)::k_ec_point<(anonymous namespace)::CurveP521W<",
                    "void (anonymous namespace)::k_ec_point_split<(anonymous namespace)::CurveP521W<"],
-    "ed25519_point": ["void (anonymous namespace)::k_ed_point<", "void (anonymous namespace)::k_ed_point_split<"],
+    "ed25519_point": ["void (anonymous namespace)::k_ed_point<", "void (anonymous namespace)::k_ed_point_split<",
+                      "void (anonymous namespace)::k_ed_point_pf<"],
     "ed25519_prep": ["(anonymous namespace)::k_prep_ed("],
     "ed25519_finish": ["(anonymous namespace)::k_ed_finish("],
     "p384_prep": ["void (anonymous namespace)::k_prep<4, "],
