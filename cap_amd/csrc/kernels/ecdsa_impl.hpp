@@ -1202,6 +1202,14 @@ constexpr int64_t EC_SPLIT2_MAX_P256 = JG_EC_SPLIT2_P256;
 #define JG_EC_PF_MAX 262144
 #endif
 constexpr int64_t EC_PF_MAX_TOKENS = JG_EC_PF_MAX;
+// JG_EC_SPLIT_PF: the prefetching chain in the small-launch split too (lone
+// ES256 chain batches of 256 / 2048 / 8000 tokens: p50 163 -> 157, 182 -> 179,
+// 269 -> 267 us; profiles/r06_s20/pf5.txt).  Off: the two-slot multi-device
+// leg, whose chunk ramp starts with split-size launches, read 105.6 / 98.3 /
+// 79.7 M/s with it against 104.5-106.4 without (profiles/r06_s20/md_ab.txt)
+#ifndef JG_EC_SPLIT_PF
+#define JG_EC_SPLIT_PF 0
+#endif
 constexpr int EC_SPLIT = JG_EC_SPLIT;                    // lanes per token of k_ec_point_split
 constexpr int64_t EC_SPLIT_MAX_TOKENS = JG_EC_SPLIT_MAX;  // launches up to this many padded tokens use it
 
@@ -1234,8 +1242,8 @@ void launch_chain(const EcArgs& a, hipStream_t s, const Marker& mk) {
   // (k_ec_point_split): one wave per SIMD leaves the madd chain's latency bare
   bool launched = false;
   if (n <= EC_SPLIT_MAX_TOKENS) {
-    hipLaunchKernelGGL((k_ec_point_split<CV, EC_SPLIT>), dim3((unsigned)((n * EC_SPLIT + WAVE - 1) / WAVE)), b, 0, s,
-                       a);
+    hipLaunchKernelGGL((k_ec_point_split<CV, EC_SPLIT, JG_EC_SPLIT_PF != 0>),
+                       dim3((unsigned)((n * EC_SPLIT + WAVE - 1) / WAVE)), b, 0, s, a);
     launched = true;
   }
   if constexpr (CV::CLS == jgk::CLS_P256 && EC_SPLIT2_MAX_P256 > 0) {

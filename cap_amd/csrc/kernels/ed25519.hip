@@ -866,6 +866,13 @@ __global__ void k_ed_table_keys(const DevKey* keys, uint32_t* blob, const int32_
 #ifndef JG_ED_SPLIT4_MAX
 #define JG_ED_SPLIT4_MAX 0
 #endif
+// JG_ED_SPLIT_PF: the prefetching loop in the small-launch split too (lone
+// EdDSA chain batches of 256 / 8000 tokens: p50 156 -> 154, 240 -> 229 us;
+// 2048: 174 -> 177; profiles/r06_s20/pf5.txt).  Off with JG_EC_SPLIT_PF
+// (ecdsa_impl.hpp)
+#ifndef JG_ED_SPLIT_PF
+#define JG_ED_SPLIT_PF 0
+#endif
 constexpr int64_t ED_SPLIT_MAX_TOKENS = JG_ED_SPLIT_MAX;  // launches up to this many padded tokens: k_ed_point_split
 constexpr int64_t ED_SPLIT4_MAX_TOKENS = JG_ED_SPLIT4_MAX;  // ... with 4 lanes per token above ED_SPLIT_MAX_TOKENS
 // launches up to this many padded tokens (above the split sizes): k_ed_point_pf
@@ -899,7 +906,7 @@ void launch_ed(const EdArgs& a, hipStream_t s, const Marker& mk) {
   dim3 g((unsigned)waves), b(WAVE);
   if (a.end - a.begin <= ED_SPLIT_MAX_TOKENS) {
     // a launch of fewer waves than ~2 per SIMD: S lanes per token
-    launch_ed_split<JG_ED_SPLIT_LANES>(a, waves, s);
+    launch_ed_split<JG_ED_SPLIT_LANES, JG_ED_SPLIT_PF != 0>(a, waves, s);
   } else if (a.end - a.begin <= ED_SPLIT4_MAX_TOKENS) {
     launch_ed_split<4>(a, waves, s);
   } else if (a.end - a.begin <= ED_SPLIT2_PF_MAX_TOKENS) {
